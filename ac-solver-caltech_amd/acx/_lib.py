@@ -1,0 +1,76 @@
+"""Loader for libacx.so, the C-ABI declared in include/acx.h.
+
+The library is loaded with ctypes *after* torch: its NEEDED libamdhip64.so.7 then binds to
+the HIP runtime torch has already mapped (same soname), so torch's device pointers and
+streams are valid in it.  There is no fallback: if the library (or a GPU) is missing, every
+compute call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before libacx.so is loaded)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ACX_LIB", os.path.join(HERE, "libacx.so"))
+
+OK, E_ARG, E_LAUNCH = 0, -1, -2
+ERR_NONE, ERR_INVALID, ERR_EMPTY_CONJ, ERR_DOMAIN, ERR_ACTION = 0, 1, 2, 3, 4
+MAX_L = 128
+
+# every entry point declared in include/acx.h, with its ctypes signature
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+SIGNATURES = {
+    "acx_step": ([_P] * 12 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_rollout": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_expand12": ([_P] * 6 + [_I64, _I32, _I32, _P], ctypes.c_int),
+    "acx_canonicalize": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),
+    "acx_unpack_keys": ([_P] * 3 + [_I64, _I32, _P], ctypes.c_int),
+    "acx_key_words": ([_I32], ctypes.c_int32),
+    "acx_version": ([], ctypes.c_char_p),
+    # host-side search engine (ac-solver-caltech_amd/csrc/acx_search.cpp)
+    "acx_search_create": ([_I32, _I32, _P, _I64], ctypes.c_void_p),
+    "acx_search_destroy": ([_P], None),
+    "acx_search_next_batch": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_search_feed": ([_P, _P, _I64], ctypes.c_int32),
+    "acx_search_status": ([_P, _P, _P, _P], ctypes.c_int32),
+    "acx_search_path": ([_P, _P, _P, _I64], ctypes.c_int64),
+}
+
+_lib = None
+
+
+class ACXError(RuntimeError):
+    pass
+
+
+def load():
+    """Return the loaded libacx.so (raises ACXError if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ACXError(
+                f"libacx.so not found at {LIB_PATH}; build it with `python ac-solver-caltech_amd/build.py` "
+                "(there is no CPU fallback for the acx kernels)"
+            )
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = lib
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != OK:
+        kind = {E_ARG: "bad argument", E_LAUNCH: "kernel launch failed"}.get(status, f"status {status}")
+        raise ACXError(f"{what}: {kind}")
+
+
+def key_words(L: int) -> int:
+    return (4 * L + 16 + 63) // 64

@@ -1,0 +1,245 @@
+"""ACEnvConfig / ACEnv with the reference's API (ac_solver/envs/ac_env.py), GPU-backed,
+plus VecACEnv, the batched environment the MI355X design is built around.
+
+ACEnv      one env; state lives on the device as a (1, 2L) int32 tensor, `step` returns
+           numpy like the reference (one acx_step launch + one device->host copy).
+VecACEnv   B envs; state (B, 2L) int32 on the device; `step` is one acx_step launch with
+           same-step autoreset to each env's starting state (the contract gymnasium's
+           SyncVectorEnv gives the reference's PPO loop, environment.py:96-101,
+           training.py:238-240); `rollout(T)` is T fused steps in one launch.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Union
+
+import numpy as np
+import torch
+
+from .. import _lib, ops
+from .ac_moves import raise_for_err
+from .utils import is_array_valid_presentation
+
+
+class Discrete:
+    """Minimal stand-in for gymnasium.spaces.Discrete (gymnasium is not a dependency)."""
+
+    def __init__(self, n: int):
+        self.n = n
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        return int(rng.integers(self.n))
+
+
+class Box:
+    """Minimal stand-in for gymnasium.spaces.Box."""
+
+    def __init__(self, low, high, dtype=np.int8):
+        self.low, self.high, self.dtype = np.asarray(low), np.asarray(high), dtype
+        self.shape = self.low.shape
+
+
+@dataclass
+class ACEnvConfig:
+    """ac_env.py:14-49 (same fields, defaults and validation)."""
+
+    initial_state: Union[np.ndarray, list] = field(default_factory=lambda: np.array([1, 0, 2, 0]))
+    horizon_length: int = 1000
+    use_supermoves: bool = False
+
+    def __post_init__(self):
+        if isinstance(self.initial_state, list):
+            self.initial_state = np.array(self.initial_state)
+        if not isinstance(self.initial_state, np.ndarray):
+            raise TypeError("initial_state must be a numpy array")
+        if self.initial_state.ndim != 1:
+            raise ValueError("initial_state must be a 1-dimensional array")
+        if len(self.initial_state) % 2 != 0:
+            raise ValueError("initial state must have even length")
+        if not is_array_valid_presentation(self.initial_state):
+            raise ValueError("initial state must be a valid presentation")
+
+    @property
+    def max_relator_length(self):
+        return len(self.initial_state) // 2
+
+    @classmethod
+    def from_dict(cls, config_dict):
+        return cls(
+            initial_state=np.array(config_dict.get("initial_state", cls().initial_state)),
+            horizon_length=config_dict.get("horizon_length", cls().horizon_length),
+            use_supermoves=config_dict.get("use_supermoves", cls().use_supermoves),
+        )
+
+
+def _check_domain(state: np.ndarray) -> None:
+    if np.any(np.abs(state) > 2):
+        raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
+
+
+class ACEnv:
+    """ac_env.py:52-132 on the GPU.  `device` selects the ROCm device (default cuda)."""
+
+    def __init__(self, config: ACEnvConfig = None, device=None):
+        config = config if config is not None else ACEnvConfig()
+        self.n_gen = 2
+        self.max_relator_length = config.max_relator_length
+        self.initial_state = config.initial_state
+        self.horizon_length = config.horizon_length
+        if config.use_supermoves:
+            raise NotImplementedError("ACEnv with supermoves is not yet implemented in this library.")
+        _check_domain(self.initial_state)
+        L = self.max_relator_length
+        self.observation_space = Box(np.full(2 * L, -self.n_gen, np.int8), np.full(2 * L, self.n_gen, np.int8))
+        self.action_space = Discrete(12)
+        self.max_reward = self.horizon_length * self.max_relator_length * self.n_gen
+        self.device = torch.device(device if device is not None else "cuda")
+        self._dtype = self.initial_state.dtype
+        dev = self.device
+        self._state = torch.empty((1, 2 * L), dtype=torch.int32, device=dev)
+        self._action = torch.empty((1,), dtype=torch.int32, device=dev)
+        self._count = torch.zeros((1,), dtype=torch.int32, device=dev)
+        self._reward = torch.empty((1,), dtype=torch.int32, device=dev)
+        self._done = torch.empty((1,), dtype=torch.uint8, device=dev)
+        self._trunc = torch.empty((1,), dtype=torch.uint8, device=dev)
+        self._lens = torch.empty((1, 2), dtype=torch.int32, device=dev)
+        self._err = torch.empty((1,), dtype=torch.uint8, device=dev)
+        self._set_state(np.copy(self.initial_state))
+        self.actions = []
+
+    def _set_state(self, state: np.ndarray) -> None:
+        L = self.max_relator_length
+        self.state = np.asarray(state)
+        self._state.copy_(torch.as_tensor(self.state.astype(np.int32)).reshape(1, 2 * L))
+        self.lengths = [int(np.count_nonzero(self.state[i * L : (i + 1) * L])) for i in range(self.n_gen)]
+        self.count_steps = 0
+        self._count.zero_()
+
+    @property
+    def state_tensor(self) -> torch.Tensor:
+        """The (1, 2L) int32 device tensor backing the env."""
+        return self._state
+
+    def step(self, action):
+        self.actions += [action]
+        self._action.fill_(int(action))
+        ops.step(self._state, self._action, state_out=self._state, step_count=self._count,
+                 horizon=self.horizon_length, cyclical=True, reward=self._reward, done=self._done,
+                 truncated=self._trunc, lengths=self._lens, err=self._err)
+        L = self.max_relator_length
+        host = torch.cat([self._state.reshape(-1), self._lens.reshape(-1), self._reward,
+                          self._done.to(torch.int32), self._trunc.to(torch.int32), self._err.to(torch.int32)]).cpu()
+        h = host.numpy()
+        raise_for_err(int(h[-1]), "ACEnv.step")
+        self.state = h[: 2 * L].astype(self._dtype)
+        self.lengths = [int(h[2 * L]), int(h[2 * L + 1])]
+        reward, done, truncated = int(h[2 * L + 2]), bool(h[2 * L + 3]), bool(h[2 * L + 4])
+        self.count_steps += 1
+        return self.state, reward, done, truncated, ({"actions": self.actions.copy()} if done else {})
+
+    def reset(self, *, seed=None, options=None):
+        start = options["starting_state"] if options and "starting_state" in options else self.initial_state
+        start = np.copy(start)
+        _check_domain(start)
+        self._set_state(start)
+        self.actions = []
+        return self.state, {}
+
+    def render(self):
+        pass
+
+    @property
+    def unwrapped(self):
+        return self
+
+
+class VecACEnv:
+    """B Andrews-Curtis envs stepped by one kernel launch per step.
+
+    initial_states: (B, 2L) array/tensor of starting presentations (each env resets to its
+    own row).  All buffers live on `device`; `step` takes a (B,) int32 device tensor of
+    move ids and returns device tensors (obs, reward, done, truncated, info) where obs is
+    the post-autoreset state and info["final_observation"] holds, for rows with
+    done | truncated, the state before the reset.
+    """
+
+    def __init__(self, initial_states, horizon_length: int = 1000, device=None, cyclical: bool = True,
+                 track_final_obs: bool = True, check_errors: bool = False):
+        self.device = torch.device(device if device is not None else "cuda")
+        init = torch.as_tensor(np.asarray(initial_states) if not torch.is_tensor(initial_states) else initial_states)
+        if init.dim() != 2 or init.shape[1] % 2:
+            raise ValueError("initial_states must be (B, 2L)")
+        init_np = init.cpu().numpy()
+        for row in init_np[: min(len(init_np), 4096)]:
+            if not is_array_valid_presentation(row):
+                raise ValueError(f"initial state {row} is not a valid presentation")
+        _check_domain(init_np)
+        self.num_envs = init.shape[0]
+        self.max_relator_length = init.shape[1] // 2
+        self.horizon_length = int(horizon_length)
+        self.cyclical = bool(cyclical)
+        self.check_errors = check_errors
+        B, L, dev = self.num_envs, self.max_relator_length, self.device
+        self.max_reward = self.horizon_length * L * 2
+        self.reset_state = init.to(dev, torch.int32).contiguous()
+        self.state = self.reset_state.clone()
+        self.step_count = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.reward = torch.empty(B, dtype=torch.int32, device=dev)
+        self.done = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.truncated = torch.empty(B, dtype=torch.uint8, device=dev)
+        self.lengths = torch.empty((B, 2), dtype=torch.int32, device=dev)
+        self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.final_obs = torch.zeros_like(self.state) if track_final_obs else None
+        self.action_space = Discrete(12)
+        self.single_observation_space = Box(np.full(2 * L, -2, np.int8), np.full(2 * L, 2, np.int8))
+
+    def reset(self, *, seed=None, options=None):
+        """Reset every env to its starting state (options["starting_states"] replaces them)."""
+        if options and "starting_states" in options:
+            s = torch.as_tensor(np.asarray(options["starting_states"])).to(self.device, torch.int32)
+            self.reset_state.copy_(s.reshape(self.reset_state.shape))
+        self.state.copy_(self.reset_state)
+        self.step_count.zero_()
+        return self.state, {}
+
+    def reset_env(self, i: int, starting_state) -> None:
+        """envs.envs[i].reset(options={"starting_state": s}) (training.py:351-352): env i now
+        starts (and later autoresets) from `starting_state`."""
+        s = np.asarray(starting_state)
+        if not is_array_valid_presentation(s):
+            raise ValueError("starting_state must be a valid presentation")
+        _check_domain(s)
+        t = torch.as_tensor(s.astype(np.int32), device=self.device)
+        self.reset_state[i].copy_(t)
+        self.state[i].copy_(t)
+        self.step_count[i] = 0
+
+    def step(self, actions: torch.Tensor):
+        if actions.dtype != torch.int32 or actions.device != self.device:
+            actions = actions.to(self.device, torch.int32)
+        ops.step(self.state, actions.contiguous(), state_out=self.state, reset_state=self.reset_state,
+                 step_count=self.step_count, horizon=self.horizon_length, cyclical=self.cyclical,
+                 reward=self.reward, done=self.done, truncated=self.truncated, lengths=self.lengths,
+                 final_obs=self.final_obs, err=self.err, err_count=self.err_count)
+        if self.check_errors:
+            self.raise_if_errors()
+        info = {"final_observation": self.final_obs} if self.final_obs is not None else {}
+        return self.state, self.reward, self.done, self.truncated, info
+
+    def rollout(self, actions: torch.Tensor, obs_traj: Optional[torch.Tensor] = None, reward_traj=None,
+                done_traj=None, trunc_traj=None):
+        """T = actions.shape[0] steps in one launch; trajectories optional (T, B, ...)."""
+        ops.rollout(self.state, actions, self.reset_state, self.step_count, horizon=self.horizon_length,
+                    cyclical=self.cyclical, obs_traj=obs_traj, reward_traj=reward_traj, done_traj=done_traj,
+                    trunc_traj=trunc_traj, err=self.err, err_count=self.err_count)
+        if self.check_errors:
+            self.raise_if_errors()
+
+    def raise_if_errors(self) -> None:
+        n = int(self.err_count.item())
+        if n:
+            codes = self.err[self.err != 0]
+            raise_for_err(int(codes[0].item()), f"VecACEnv ({n} env(s) failed)")

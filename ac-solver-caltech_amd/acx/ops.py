@@ -1,0 +1,221 @@
+"""Torch-facing wrappers of the libacx.so kernels (include/acx.h).
+
+Every function takes/returns torch tensors on a ROCm device, launches on the current
+torch stream and never synchronises.  Presentations are (B, 2L) int32 tensors.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+_INT32 = torch.int32
+_UINT8 = torch.uint8
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need_gpu(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise _lib.ACXError(f"{name} must be a ROCm device tensor (acx has no CPU path)")
+
+
+def _check(t: Optional[torch.Tensor], name: str, dtype: torch.dtype, shape, device) -> None:
+    if t is None:
+        return
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if t.device != device:
+        raise ValueError(f"{name}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _L_of(states: torch.Tensor) -> int:
+    if states.dim() != 2 or states.shape[1] % 2:
+        raise ValueError(f"presentations must be (B, 2L), got {tuple(states.shape)}")
+    L = states.shape[1] // 2
+    if not 1 <= L <= _lib.MAX_L:
+        raise ValueError(f"max_relator_length {L} outside [1, {_lib.MAX_L}]")
+    return L
+
+
+def step(
+    state_in: torch.Tensor,
+    action: torch.Tensor,
+    *,
+    state_out: Optional[torch.Tensor] = None,
+    reset_state: Optional[torch.Tensor] = None,
+    step_count: Optional[torch.Tensor] = None,
+    horizon: int = 0,
+    cyclical: bool = True,
+    reward: Optional[torch.Tensor] = None,
+    done: Optional[torch.Tensor] = None,
+    truncated: Optional[torch.Tensor] = None,
+    lengths: Optional[torch.Tensor] = None,
+    final_obs: Optional[torch.Tensor] = None,
+    err: Optional[torch.Tensor] = None,
+    err_count: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    """acx_step: batched ACEnv.step / ACMove.  Returns state_out (in place if given as state_in)."""
+    lib = _lib.load()
+    _need_gpu(state_in, "state_in")
+    L = _L_of(state_in)
+    B = state_in.shape[0]
+    dev = state_in.device
+    if state_out is None:
+        state_out = torch.empty_like(state_in)
+    _check(state_in, "state_in", _INT32, (B, 2 * L), dev)
+    _check(state_out, "state_out", _INT32, (B, 2 * L), dev)
+    _check(action, "action", _INT32, (B,), dev)
+    _check(reset_state, "reset_state", _INT32, (B, 2 * L), dev)
+    _check(step_count, "step_count", _INT32, (B,), dev)
+    _check(reward, "reward", _INT32, (B,), dev)
+    _check(done, "done", _UINT8, (B,), dev)
+    _check(truncated, "truncated", _UINT8, (B,), dev)
+    _check(lengths, "lengths", _INT32, (B, 2), dev)
+    _check(final_obs, "final_obs", _INT32, (B, 2 * L), dev)
+    _check(err, "err", _UINT8, (B,), dev)
+    _check(err_count, "err_count", _INT32, (1,), dev)
+    st = lib.acx_step(
+        _ptr(state_in), _ptr(state_out), _ptr(action), _ptr(reset_state), _ptr(step_count), _ptr(reward),
+        _ptr(done), _ptr(truncated), _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count),
+        B, L, int(horizon), int(bool(cyclical)), _stream(dev),
+    )
+    _lib.check(st, "acx_step")
+    return state_out
+
+
+def rollout(
+    state: torch.Tensor,
+    actions: torch.Tensor,
+    reset_state: torch.Tensor,
+    step_count: torch.Tensor,
+    *,
+    horizon: int,
+    cyclical: bool = True,
+    obs_traj: Optional[torch.Tensor] = None,
+    reward_traj: Optional[torch.Tensor] = None,
+    done_traj: Optional[torch.Tensor] = None,
+    trunc_traj: Optional[torch.Tensor] = None,
+    err: Optional[torch.Tensor] = None,
+    err_count: Optional[torch.Tensor] = None,
+) -> None:
+    """acx_rollout: T = actions.shape[0] fused env steps; state/step_count updated in place."""
+    lib = _lib.load()
+    _need_gpu(state, "state")
+    L = _L_of(state)
+    B = state.shape[0]
+    T = actions.shape[0]
+    dev = state.device
+    _check(state, "state", _INT32, (B, 2 * L), dev)
+    _check(actions, "actions", _INT32, (T, B), dev)
+    _check(reset_state, "reset_state", _INT32, (B, 2 * L), dev)
+    _check(step_count, "step_count", _INT32, (B,), dev)
+    _check(obs_traj, "obs_traj", _INT32, (T, B, 2 * L), dev)
+    _check(reward_traj, "reward_traj", _INT32, (T, B), dev)
+    _check(done_traj, "done_traj", _UINT8, (T, B), dev)
+    _check(trunc_traj, "trunc_traj", _UINT8, (T, B), dev)
+    _check(err, "err", _UINT8, (B,), dev)
+    _check(err_count, "err_count", _INT32, (1,), dev)
+    st = lib.acx_rollout(
+        _ptr(state), _ptr(actions), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj),
+        _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon),
+        int(bool(cyclical)), _stream(dev),
+    )
+    _lib.check(st, "acx_rollout")
+
+
+def expand12(
+    parents: torch.Tensor,
+    *,
+    cyclical: bool = False,
+    children: bool = True,
+    lengths: bool = True,
+    keys: bool = False,
+    err: bool = True,
+    out: Optional[dict] = None,
+):
+    """acx_expand12: all 12 ACMove children of every parent.
+
+    Returns a dict with (as requested) "children" (N,12,2L) int32, "lengths" (N,12,2) int32,
+    "keys" (N,12,KW) int64 (packed states), "err" (N,12) uint8.  Pass `out` (a dict of
+    preallocated tensors with those names) to reuse buffers.
+    """
+    lib = _lib.load()
+    _need_gpu(parents, "parents")
+    L = _L_of(parents)
+    N = parents.shape[0]
+    dev = parents.device
+    kw = _lib.key_words(L)
+    _check(parents, "parents", _INT32, (N, 2 * L), dev)
+    res = {}
+    spec = {
+        "children": (children, _INT32, (N, 12, 2 * L)),
+        "lengths": (lengths, _INT32, (N, 12, 2)),
+        "keys": (keys, torch.int64, (N, 12, kw)),
+        "err": (err, _UINT8, (N, 12)),
+    }
+    for name, (want, dt, shape) in spec.items():
+        if not want:
+            continue
+        t = out.get(name) if out else None
+        if t is None:
+            t = torch.empty(shape, dtype=dt, device=dev)
+        else:
+            t = t[: shape[0]] if t.shape[0] != shape[0] else t
+            _check(t, name, dt, shape, dev)
+        res[name] = t
+    st = lib.acx_expand12(
+        _ptr(parents), _ptr(res.get("children")), _ptr(res.get("lengths")), _ptr(res.get("keys")),
+        _ptr(res.get("err")), None, N, L, int(bool(cyclical)), _stream(dev),
+    )
+    _lib.check(st, "acx_expand12")
+    return res
+
+
+def canonicalize(states: torch.Tensor, *, cyclical: bool = True, out: Optional[torch.Tensor] = None):
+    """acx_canonicalize: simplify_presentation over a batch -> (states, lengths (B,2), err (B,))."""
+    lib = _lib.load()
+    _need_gpu(states, "states")
+    L = _L_of(states)
+    B = states.shape[0]
+    dev = states.device
+    _check(states, "states", _INT32, (B, 2 * L), dev)
+    if out is None:
+        out = torch.empty_like(states)
+    lens = torch.empty((B, 2), dtype=_INT32, device=dev)
+    err = torch.empty((B,), dtype=_UINT8, device=dev)
+    st = lib.acx_canonicalize(_ptr(states), _ptr(out), _ptr(lens), _ptr(err), None, B, L, int(bool(cyclical)),
+                              _stream(dev))
+    _lib.check(st, "acx_canonicalize")
+    return out, lens, err
+
+
+def unpack_keys(keys: torch.Tensor, L: int, *, out: Optional[torch.Tensor] = None, lengths: bool = False):
+    """acx_unpack_keys: packed keys (M, KW) int64 -> presentations (M, 2L) int32 (+ lengths)."""
+    lib = _lib.load()
+    _need_gpu(keys, "keys")
+    kw = _lib.key_words(L)
+    keys = keys.reshape(-1, kw)
+    M = keys.shape[0]
+    dev = keys.device
+    _check(keys, "keys", torch.int64, (M, kw), dev)
+    if out is None:
+        out = torch.empty((M, 2 * L), dtype=_INT32, device=dev)
+    _check(out, "out", _INT32, (M, 2 * L), dev)
+    lens = torch.empty((M, 2), dtype=_INT32, device=dev) if lengths else None
+    st = lib.acx_unpack_keys(_ptr(keys), _ptr(out), _ptr(lens), M, int(L), _stream(dev))
+    _lib.check(st, "acx_unpack_keys")
+    return (out, lens) if lengths else out

@@ -1,0 +1,93 @@
+"""Driver shared by greedy_search and bfs: GPU 12-way expansion (acx_expand12 -> packed
+child keys) + the host search engine in libacx.so (csrc/acx_search.cpp), which replays the
+reference's sequential pop / expand / dedup / budget logic on those keys."""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _lib, ops
+from ..envs.utils import is_array_valid_presentation
+
+BFS, GREEDY = 0, 1
+
+
+def _pack_key(state: np.ndarray, L: int) -> np.ndarray:
+    """Host packing of one presentation into the acx key format (acx.h: r0 codes, r1
+    codes, n0, n1; codes x=0, x^-1=1, y=2, y^-1=3)."""
+    kw = _lib.key_words(L)
+    bits = np.zeros(kw * 64, dtype=np.uint8)
+    code = {1: 0, -1: 1, 2: 2, -2: 3}
+    lens = []
+    for h in range(2):
+        word = state[h * L : (h + 1) * L]
+        n = int(np.count_nonzero(word))
+        lens.append(n)
+        for i in range(n):
+            c = code[int(word[i])]
+            bits[2 * (h * L + i)] = c & 1
+            bits[2 * (h * L + i) + 1] = (c >> 1) & 1
+    for j in range(8):
+        bits[4 * L + j] = (lens[0] >> j) & 1
+        bits[4 * L + 8 + j] = (lens[1] >> j) & 1
+    words = np.packbits(bits.reshape(kw, 64)[:, ::-1], axis=1).view(">u8").reshape(kw).astype(np.uint64)
+    return words
+
+
+def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, device=None, batch=None):
+    p = np.asarray(presentation)
+    assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
+    L = len(p) // 2
+    if np.any(np.abs(p) > 2):
+        raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
+    dev = torch.device(device if device is not None else "cuda")
+    lib = _lib.load()
+    kw = _lib.key_words(L)
+    # the start node is the (unreduced) input itself, as in the reference
+    start_key = _pack_key(p.astype(np.int64), L)
+    h = lib.acx_search_create(mode, L, start_key.ctypes.data, int(max_nodes_to_explore))
+    if not h:
+        raise _lib.ACXError("acx_search_create failed")
+    if batch is None:
+        batch = 65536 if mode == BFS else 512
+    try:
+        parent_keys = np.zeros((batch, kw), dtype=np.uint64)
+        pinned_in = torch.empty((batch, kw), dtype=torch.int64).pin_memory()
+        pinned_out = torch.empty((batch, 12, kw), dtype=torch.int64).pin_memory()
+        dev_keys = torch.empty((batch, kw), dtype=torch.int64, device=dev)
+        dev_states = torch.empty((batch, 2 * L), dtype=torch.int32, device=dev)
+        out = {"keys": torch.empty((batch, 12, kw), dtype=torch.int64, device=dev)}
+        status = 0
+        while status == 0:
+            n = lib.acx_search_next_batch(h, parent_keys.ctypes.data, batch)
+            if n == 0:
+                break
+            pinned_in[:n].numpy()[:] = parent_keys[:n].view(np.int64)
+            dev_keys[:n].copy_(pinned_in[:n], non_blocking=True)
+            ops.unpack_keys(dev_keys[:n], L, out=dev_states[:n])
+            res = ops.expand12(dev_states[:n], cyclical=cyclical, children=False, lengths=False, keys=True,
+                               err=False, out=out)
+            pinned_out[:n].copy_(res["keys"][:n], non_blocking=False)
+            status = lib.acx_search_feed(h, pinned_out.data_ptr(), n)
+        budget = ctypes.c_int32(0)
+        min_len = ctypes.c_int32(0)
+        n_nodes = ctypes.c_int64(0)
+        status = lib.acx_search_status(h, ctypes.byref(budget), ctypes.byref(min_len), ctypes.byref(n_nodes))
+        if verbose:
+            print(f"Minimal total length found: {min_len.value}")
+        if budget.value:
+            print(
+                f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
+                f"{max_nodes_to_explore}"
+            )
+        cap = 1 << 16
+        acts = np.zeros(cap, np.int32)
+        tots = np.zeros(cap, np.int32)
+        m = lib.acx_search_path(h, acts.ctypes.data, tots.ctypes.data, cap)
+        path = [(int(acts[i]), int(tots[i])) for i in range(min(m, cap))]
+        return status == 1, path
+    finally:
+        lib.acx_search_destroy(h)

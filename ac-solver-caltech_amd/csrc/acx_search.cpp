@@ -1,0 +1,325 @@
+// acx_search.cpp -- host-side search engine for greedy_search / bfs over GPU expansions.
+//
+// The reference searches (ac_solver/search/greedy.py:15-121, breadth_first.py:15-97) pop
+// one node, call ACMove 12 times, and keep a Python set of state tuples.  Here the GPU
+// expands many parents per launch (acx_expand12 -> packed child keys) and this engine
+// replays the reference's sequential logic exactly on those keys:
+//   * BFS: FIFO queue; per popped parent, children in action order: success test
+//     (n0+n1 == 2), dedup-insert, enqueue; budget test after each parent
+//     (breadth_first.py:61-95).  Parents are expanded ahead in FIFO order, which cannot
+//     change the result because expansion is a pure function of the state.
+//   * greedy: priority order (total length, path length, state tuple) -- a total order,
+//     so heapq's pop sequence equals walking an ordered set from its minimum
+//     (greedy.py:181-239).  The smallest not-yet-expanded nodes are expanded
+//     speculatively in one launch; children are cached until their parent is popped.
+// Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
+// acx_key_words(L) uint64 words.
+#include <cstdint>
+#include <cstring>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#include "acx.h"
+
+namespace {
+
+constexpr int ACT = 12;
+
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+struct Engine {
+    int mode;  // 0 bfs, 1 greedy
+    int L, kw;
+    int64_t max_nodes;
+    // node storage
+    std::vector<uint64_t> keys;  // node * kw
+    std::vector<int64_t> parent;
+    std::vector<int8_t> action;
+    std::vector<int16_t> total;
+    std::vector<int32_t> depth;
+    std::vector<int8_t> lex;  // greedy only: node * 2L letters + 2 (tuple order)
+    // open-addressing hash set of node ids (-1 empty)
+    std::vector<int64_t> table;
+    uint64_t mask = 0;
+    int64_t n_set = 0;
+    // BFS queue
+    std::vector<int64_t> queue;
+    size_t head = 0, requested = 0;
+    // greedy ordered frontier
+    struct Cmp {
+        const Engine* e;
+        bool operator()(int64_t a, int64_t b) const {
+            if (e->total[a] != e->total[b]) return e->total[a] < e->total[b];
+            if (e->depth[a] != e->depth[b]) return e->depth[a] < e->depth[b];
+            const int n = 2 * e->L;
+            const int c = std::memcmp(&e->lex[(size_t)a * n], &e->lex[(size_t)b * n], (size_t)n);
+            if (c != 0) return c < 0;
+            return a < b;
+        }
+    };
+    std::set<int64_t, Cmp>* frontier = nullptr;
+    std::unordered_map<int64_t, size_t> pending;  // requested, children not yet fed
+    // children cache: node -> offset into cache_keys (ACT * kw words)
+    std::unordered_map<int64_t, size_t> cache;
+    std::vector<uint64_t> cache_keys;
+    std::vector<size_t> free_slots;
+    // last request (order of nodes handed to next_batch)
+    std::vector<int64_t> batch;
+    // result
+    int status = 0;  // 0 running, 1 success, 2 failed (budget or exhausted)
+    int64_t found_parent = -1;
+    int found_action = -1, found_len = -1;
+    int last_action = -1, last_len = -1;
+    int64_t last_popped = -1;
+    int min_length = 0;
+    int budget_hit = 0;
+
+    Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
+        table.assign(1 << 12, -1);
+        mask = table.size() - 1;
+        if (mode == 1) frontier = new std::set<int64_t, Cmp>(Cmp{this});
+    }
+    ~Engine() { delete frontier; }
+
+    uint64_t hash_key(const uint64_t* k) const {
+        uint64_t h = 0x9e3779b97f4a7c15ull;
+        for (int i = 0; i < kw; ++i) h = mix64(h ^ k[i]) + (uint64_t)i;
+        return h;
+    }
+    void grow() {
+        std::vector<int64_t> old;
+        old.swap(table);
+        table.assign(old.size() * 2, -1);
+        mask = table.size() - 1;
+        for (int64_t id : old)
+            if (id >= 0) {
+                uint64_t p = hash_key(&keys[(size_t)id * kw]) & mask;
+                while (table[p] >= 0) p = (p + 1) & mask;
+                table[p] = id;
+            }
+    }
+    // find key; returns node id or -1; *slot gets the insert position
+    int64_t find(const uint64_t* k, uint64_t* slot) const {
+        uint64_t p = hash_key(k) & mask;
+        while (true) {
+            const int64_t id = table[p];
+            if (id < 0) { *slot = p; return -1; }
+            if (std::memcmp(&keys[(size_t)id * kw], k, sizeof(uint64_t) * kw) == 0) return id;
+            p = (p + 1) & mask;
+        }
+    }
+    static int key_len(const uint64_t* k, int L) {
+        const int bit = 4 * L;
+        const uint64_t lo = k[bit >> 6] >> (bit & 63);
+        const uint64_t hi = (bit & 63) > 48 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
+        const uint64_t v = lo | hi;
+        return (int)(v & 0xff) + (int)((v >> 8) & 0xff);
+    }
+    void decode_lex(const uint64_t* k, int8_t* out) const {
+        // letters of r0 then r1 (padded), stored as value + 2 (unsigned order == numeric)
+        int n[2];
+        {
+            const int bit = 4 * L;
+            const uint64_t lo = k[bit >> 6] >> (bit & 63);
+            const uint64_t hi = (bit & 63) > 48 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
+            n[0] = (int)((lo | hi) & 0xff);
+            n[1] = (int)(((lo | hi) >> 8) & 0xff);
+        }
+        static const int8_t dec[4] = {1, -1, 2, -2};
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < L; ++i) {
+                const int bit = 2 * (h * L + i);
+                const int code = (int)((k[bit >> 6] >> (bit & 63)) & 3u);
+                out[h * L + i] = (int8_t)((i < n[h] ? dec[code] : 0) + 2);
+            }
+    }
+    int64_t add_node(const uint64_t* k, uint64_t slot, int64_t par, int act, int tot, int dep) {
+        const int64_t id = (int64_t)parent.size();
+        keys.insert(keys.end(), k, k + kw);
+        parent.push_back(par);
+        action.push_back((int8_t)act);
+        total.push_back((int16_t)tot);
+        depth.push_back(dep);
+        if (mode == 1) {
+            lex.resize(lex.size() + 2 * L);
+            decode_lex(k, &lex[(size_t)id * 2 * L]);
+        }
+        table[slot] = id;
+        ++n_set;
+        if ((uint64_t)n_set * 2 > table.size()) grow();
+        return id;
+    }
+
+    void start(const uint64_t* k) {
+        uint64_t slot;
+        find(k, &slot);
+        const int tot = key_len(k, L);
+        min_length = tot;
+        const int64_t id = add_node(k, slot, -1, -1, tot, 0);
+        if (mode == 0) queue.push_back(id);
+        else frontier->insert(id);
+    }
+
+    int64_t next_batch(uint64_t* out, int64_t cap) {
+        batch.clear();
+        if (status != 0) return 0;
+        if (mode == 0) {
+            while ((int64_t)batch.size() < cap && requested < queue.size()) {
+                const int64_t id = queue[requested++];
+                batch.push_back(id);
+            }
+        } else {
+            for (auto it = frontier->begin(); it != frontier->end() && (int64_t)batch.size() < cap; ++it) {
+                if (cache.count(*it)) continue;
+                batch.push_back(*it);
+            }
+        }
+        for (size_t i = 0; i < batch.size(); ++i)
+            std::memcpy(out + i * kw, &keys[(size_t)batch[i] * kw], sizeof(uint64_t) * kw);
+        return (int64_t)batch.size();
+    }
+
+    void store_children(int64_t id, const uint64_t* ck) {
+        size_t off;
+        if (!free_slots.empty()) {
+            off = free_slots.back();
+            free_slots.pop_back();
+        } else {
+            off = cache_keys.size();
+            cache_keys.resize(off + (size_t)ACT * kw);
+        }
+        std::memcpy(&cache_keys[off], ck, sizeof(uint64_t) * ACT * kw);
+        cache[id] = off;
+    }
+
+    // expand one popped node from its cached children; returns true when the search ends
+    bool visit(int64_t id) {
+        const size_t off = cache[id];
+        const uint64_t* ck = &cache_keys[off];
+        last_popped = id;
+        bool ended = false;
+        for (int a = 0; a < ACT && !ended; ++a) {
+            const uint64_t* k = ck + (size_t)a * kw;
+            const int len = key_len(k, L);
+            last_action = a;
+            last_len = len;
+            if (len < min_length) min_length = len;
+            if (len == 2) {  // greedy.py:217, breadth_first.py:84
+                status = 1;
+                found_parent = id;
+                found_action = a;
+                found_len = len;
+                ended = true;
+                break;
+            }
+            uint64_t slot;
+            if (find(k, &slot) < 0) {
+                const int64_t nid = add_node(k, slot, id, a, len, depth[id] + 1);
+                if (mode == 0) queue.push_back(nid);
+                else frontier->insert(nid);
+            }
+        }
+        cache.erase(id);
+        free_slots.push_back(off);
+        if (!ended && n_set >= max_nodes) {  // greedy.py:241, breadth_first.py:91
+            status = 2;
+            budget_hit = 1;
+            ended = true;
+        }
+        return ended;
+    }
+
+    int feed(const uint64_t* child_keys, int64_t count) {
+        for (int64_t i = 0; i < count && i < (int64_t)batch.size(); ++i)
+            store_children(batch[i], child_keys + (size_t)i * ACT * kw);
+        batch.clear();
+        // advance as far as the cache allows
+        while (status == 0) {
+            if (mode == 0) {
+                if (head >= queue.size()) { status = 2; break; }
+                const int64_t id = queue[head];
+                if (!cache.count(id)) return 0;
+                ++head;
+                if (visit(id)) break;
+            } else {
+                if (frontier->empty()) { status = 2; break; }
+                const int64_t id = *frontier->begin();
+                if (!cache.count(id)) return 0;
+                frontier->erase(frontier->begin());
+                if (visit(id)) break;
+            }
+        }
+        return status;
+    }
+
+    // path of node `id` as (action, total) pairs from the root (root = (-1, total))
+    int64_t path(int64_t id, int32_t* acts, int32_t* lens, int64_t cap, bool append_found) const {
+        std::vector<int64_t> chain;
+        for (int64_t v = id; v >= 0; v = parent[v]) chain.push_back(v);
+        int64_t n = 0;
+        for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+            if (n < cap) {
+                acts[n] = action[*it];
+                lens[n] = total[*it];
+            }
+            ++n;
+        }
+        if (append_found) {
+            if (n < cap) {
+                acts[n] = found_action >= 0 ? found_action : last_action;
+                lens[n] = found_action >= 0 ? found_len : last_len;
+            }
+            ++n;
+        }
+        return n;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+void* acx_search_create(int32_t mode, int32_t L, const uint64_t* start_key, int64_t max_nodes) {
+    if ((mode != 0 && mode != 1) || L < 1 || L > ACX_MAX_L || !start_key) return nullptr;
+    Engine* e = new Engine(mode, L, max_nodes);
+    e->start(start_key);
+    return e;
+}
+
+void acx_search_destroy(void* h) { delete static_cast<Engine*>(h); }
+
+int64_t acx_search_next_batch(void* h, uint64_t* parent_keys, int64_t cap) {
+    return static_cast<Engine*>(h)->next_batch(parent_keys, cap);
+}
+
+int32_t acx_search_feed(void* h, const uint64_t* child_keys, int64_t count) {
+    return static_cast<Engine*>(h)->feed(child_keys, count);
+}
+
+// 0 running, 1 success, 2 failed; *budget_hit = 1 when the node budget ended the search
+int32_t acx_search_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {
+    Engine* e = static_cast<Engine*>(h);
+    if (budget_hit) *budget_hit = e->budget_hit;
+    if (min_length) *min_length = e->min_length;
+    if (n_nodes) *n_nodes = e->n_set;
+    return e->status;
+}
+
+// success: path of the found child; failure (greedy): path of the last popped node plus its
+// last child (greedy.py:247).  Returns the number of (action, total) entries.
+int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap) {
+    Engine* e = static_cast<Engine*>(h);
+    if (e->status == 1) return e->path(e->found_parent, actions, totals, cap, true);
+    if (e->last_popped < 0) return 0;
+    return e->path(e->last_popped, actions, totals, cap, true);
+}
+
+}  // extern "C"

@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec at batch 2^20, max_relator_length 36 (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): PPO rollout collection -- 2^20 envs per GPU,
+L = 36, env horizon 200, Miller-Schupp starting states (env i starts at presentation
+i mod 1190 of all_presentations.txt), uniform random move ids pre-generated on the device
+(torch.Generator, seed 0 + rank), same-step autoreset.  One bench "step" = one env step of
+the whole batch; the K timed steps are ONE acx_rollout launch that writes the full
+(K, B, 2L) int32 observation trajectory plus reward/done/truncated per step.  Inputs are
+resident in HBM before the timed region.
+
+Also measured (reported under "variants"): the per-call acx_step API (one launch per step,
+state read+written in HBM each step) on the same batch.
+
+Multi-GPU: one process per GPU (torchrun), envs sharded by index (weak scaling: 2^20
+envs per rank); no collective on the data path, a barrier + max-over-ranks of the timed
+region only.
+
+CPU baseline (rank 0, N = 1): oracle/np_port.py -- a numpy restatement with the reference's
+per-env ACEnv.step call pattern -- one process per host core (bounded at 16), 64 envs each,
+~10 s, same starting states and action stream.  Run before the GPU is touched.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(REPO, "ac-solver-caltech_amd")
+sys.path.insert(0, PKG_ROOT)
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def ms_starts(L: int, B: int, offset: int = 0) -> np.ndarray:
+    ms = np.load(os.path.join(PKG_ROOT, "acx", "data", "all_presentations.npy"))
+    idx = (np.arange(B) + offset) % len(ms)
+    src = ms[idx]
+    out = np.zeros((B, 2 * L), np.int32)
+    for h in range(2):
+        half = src[:, h * 18 : (h + 1) * 18]
+        out[:, h * L : h * L + 18] = half
+    return out
+
+
+def cpu_baseline(L: int, horizon: int, seconds: float, max_procs: int = 16):
+    """numpy reference-structured port, one process per core, bounded sample."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs_n = max(1, min(cores, max_procs))
+    code = (
+        "import sys,json,numpy as np; sys.path.insert(0,%r); sys.path.insert(0,%r);"
+        "from bench import ms_starts; from oracle import np_port;"
+        "r=int(sys.argv[1]); s=ms_starts(%d,64,offset=64*r).astype(np.int64);"
+        "a=np.random.default_rng(r).integers(0,12,size=(4096,64));"
+        "n,el=np_port.run_sample(s,a,%d,%f); print(json.dumps([n,el]))"
+    ) % (REPO, PKG_ROOT, L, horizon, seconds)
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, "-c", code, str(r)], stdout=subprocess.PIPE, env=env)
+          for r in range(procs_n)]
+    total = 0.0
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds * 10 + 120)
+        n, el = json.loads(out.decode().strip().splitlines()[-1])
+        total += n / el
+    return {
+        "value": total,
+        "unit": "env-steps/s",
+        "cores": procs_n,
+        "kind": "port",
+        "sample": f"oracle/np_port.py ACEnv.step restatement, {procs_n} procs x 64 envs x {seconds:.0f}s, "
+                  f"L={L}, horizon {horizon}, Miller-Schupp starts, uniform actions",
+    }
+
+
+def cpu_baseline_c(L: int, horizon: int, seconds: float):
+    """C oracle (oracle/acx_oracle.c), one core, batch of 65536 envs (second CPU number)."""
+    from oracle import oracle as O
+
+    B = 65536
+    starts = ms_starts(L, B)
+    state = starts.copy()
+    cnt = np.zeros(B, np.int32)
+    rng = np.random.default_rng(0)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.env_step(state, rng.integers(0, 12, size=B).astype(np.int32), L, horizon, cnt, reset_state=starts)
+        steps += B
+    el = time.perf_counter() - t0
+    return {"value": steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/acx_oracle.c env_step, 1 core, B=65536, {el:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--L", type=int, default=36)
+    ap.add_argument("--horizon", type=int, default=200)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-step-api", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    L, B, K, W, H = args.L, args.batch, args.steps, args.warmup, args.horizon
+
+    cpu = None
+    cpu_c = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # before anything touches the GPU
+        cpu = cpu_baseline(L, H, args.cpu_seconds)
+        cpu_c = cpu_baseline_c(L, H, min(5.0, args.cpu_seconds))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import acx
+    from acx import ops
+
+    starts = torch.as_tensor(ms_starts(L, B, offset=rank * B)).to(dev)
+    state = starts.clone()
+    count = torch.zeros(B, dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0 + rank)
+    T_buf = max(K, W)
+    actions = torch.randint(0, 12, (W + K, B), dtype=torch.int32, device=dev, generator=g)
+    obs = torch.empty((T_buf, B, 2 * L), dtype=torch.int32, device=dev)
+    rew = torch.empty((T_buf, B), dtype=torch.int32, device=dev)
+    done = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
+    trunc = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
+    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    err_count = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def roll(a, T):
+        ops.rollout(state, a, starts, count, horizon=H, cyclical=True, obs_traj=obs[:T], reward_traj=rew[:T],
+                    done_traj=done[:T], trunc_traj=trunc[:T], err=err, err_count=err_count)
+
+    # warmup (W env steps, untimed)
+    if W > 0:
+        roll(actions[:W], W)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    roll(actions[W : W + K], K)
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_err = int(err_count.item())
+
+    # algorithmic bytes of the rollout launch (DESIGN.md "Roofline"): per env-step action 4 B
+    # + obs 8L B + reward 4 + done 1 + truncated 1; per env per launch state in/out 2*8L,
+    # reset state 8L, step count in/out 8, err 1
+    step_bytes = 4 + 8 * L + 4 + 1 + 1
+    launch_bytes = K * B * step_bytes + B * (24 * L + 8 + 1)
+    achieved = launch_bytes / kernel_s / 1e9
+
+    variants = {}
+    if not args.no_step_api:
+        # per-call acx_step API: one launch per env step, state in/out of HBM each step
+        rew1 = torch.empty(B, dtype=torch.int32, device=dev)
+        dn1 = torch.empty(B, dtype=torch.uint8, device=dev)
+        tr1 = torch.empty(B, dtype=torch.uint8, device=dev)
+        lens1 = torch.empty((B, 2), dtype=torch.int32, device=dev)
+        st1 = starts.clone()
+        cnt1 = torch.zeros(B, dtype=torch.int32, device=dev)
+
+        def step(a):
+            ops.step(st1, a, state_out=st1, reset_state=starts, step_count=cnt1, horizon=H, cyclical=True,
+                     reward=rew1, done=dn1, truncated=tr1, lengths=lens1, err=err, err_count=err_count)
+
+        for t in range(W):
+            step(actions[t])
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for t in range(K):
+            step(actions[W + t])
+        e1.record()
+        torch.cuda.synchronize()
+        s_api = e0.elapsed_time(e1) / 1e3
+        # per env-step: state in 8L + action 4 + count in 4 + state out 8L + lengths 8 +
+        # reward 4 + done 1 + truncated 1 + count out 4 + err 1
+        sb = 16 * L + 27
+        variants["step_api"] = {
+            "value": world * B * K / s_api if world == 1 else None,
+            "unit": "env-steps/s",
+            "ms_per_step": s_api / K * 1e3,
+            "roofline": {"bound": "hbm", "achieved": B * sb / (s_api / K) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS,
+                         "bytes_per_env_step": sb},
+        }
+        n_err = int(err_count.item())
+
+    value = world * B * K / elapsed
+    line = {
+        "metric": "env-steps/sec at batch 2^20, max_relator_len 36; 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: Miller-Schupp starting states (all_presentations.txt, env i -> i mod 1190), "
+                "uniform random move ids (torch.Generator seed 0+rank)",
+        "config": {
+            "workload": "PPO rollout collection (BASELINE configs[2]): 2^20 envs/GPU, L=36, horizon 200, "
+                        "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
+                        "one acx_rollout launch of K steps",
+            "global_batch": world * B,
+            "envs_per_gpu": B,
+            "max_relator_length": L,
+            "horizon": H,
+            "parallelism": f"env-index shards x{world}, no data-path collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "acx::rollout_kernel<3,36,4>",
+            "bytes_per_env_step": step_bytes,
+            "launch_bytes": launch_bytes,
+            "kernel_ms": kernel_s * 1e3,
+        },
+        "cpu_baseline": cpu,
+        "cpu_baseline_c_oracle": cpu_c,
+        "variants": variants,
+        "env_errors": n_err,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

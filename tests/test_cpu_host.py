@@ -1,0 +1,166 @@
+"""CPU-only checks of the host side: the C-ABI library loads and exports every symbol
+include/acx.h declares (no compute calls without a GPU), host helpers match the
+reference's unit cases, the host search engine (csrc/acx_search.cpp) reproduces the
+reference's search results when fed expansions from the oracle, and nothing silently
+falls back to CPU."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, REPO
+from oracle import oracle as O
+
+import acx
+from acx import _lib
+from acx.envs import utils as U
+from acx.search import _engine as E
+
+
+def test_library_exports_header_symbols():
+    lib = _lib.load()
+    with open(os.path.join(REPO, "include", "acx.h")) as f:
+        hdr = f.read()
+    names = set(re.findall(r"\b(acx_\w+)\s*\(", hdr))
+    assert {"acx_step", "acx_rollout", "acx_expand12", "acx_canonicalize", "acx_unpack_keys"} <= names
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, n
+    assert lib.acx_key_words(36) == 3
+    assert lib.acx_key_words(128) == 9
+    assert lib.acx_version().startswith(b"acx")
+
+
+def test_no_cpu_fallback():
+    s = torch.zeros((4, 8), dtype=torch.int32)
+    a = torch.zeros(4, dtype=torch.int32)
+    with pytest.raises(_lib.ACXError):
+        acx.ops.step(s, a)
+    with pytest.raises(_lib.ACXError):
+        acx.ops.expand12(s)
+
+
+def test_host_utils_match_reference_cases():
+    with open(os.path.join(GOLDEN, "unit_cases.json")) as f:
+        unit = json.load(f)
+    for c in unit["valid"]:
+        assert U.is_array_valid_presentation(np.array(c["p"])) == c["out"], c
+    for c in unit["trivial"]:
+        assert U.is_presentation_trivial(np.array(c["p"])) == c["out"], c
+    for L in (1, 2, 3, 4, 36):
+        st = U.generate_trivial_states(L)
+        assert st.shape == (8, 2 * L)
+        for s in st:
+            assert U.is_presentation_trivial(s)
+    p = U.convert_relators_to_presentation([1, 2], [-1], 4)
+    assert p.dtype == np.int8 and p.tolist() == [1, 2, 0, 0, -1, 0, 0, 0]
+    q = U.change_max_relator_length_of_presentation(p, 6)
+    assert q.tolist() == [1, 2, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0]
+
+
+def test_acenvconfig_validation():
+    from acx import ACEnvConfig
+    c = ACEnvConfig()
+    assert c.max_relator_length == 2 and c.horizon_length == 1000
+    with pytest.raises(ValueError):
+        ACEnvConfig(initial_state=[1, 0, 2])
+    with pytest.raises(ValueError):
+        ACEnvConfig(initial_state=[1, 0, 2, 0, 0, 0, 0, 1])
+    with pytest.raises(ValueError):
+        ACEnvConfig(initial_state=np.zeros((2, 2)))
+    with pytest.raises(TypeError):
+        ACEnvConfig(initial_state=(1, 0, 2, 0))
+    d = ACEnvConfig.from_dict({"initial_state": [1, 2, 0, -1, 0, 0], "horizon_length": 7})
+    assert d.max_relator_length == 3 and d.horizon_length == 7
+
+
+def _oracle_keys(states, L, cyclical):
+    ch, lens, err = O.expand12(states, L, cyclical)
+    kw = _lib.key_words(L)
+    keys = np.zeros((states.shape[0], 12, kw), np.uint64)
+    for i in range(states.shape[0]):
+        for a in range(12):
+            keys[i, a] = E._pack_key(ch[i, a], L)
+    return keys
+
+
+def _unpack_key_host(k, L):
+    bits = np.unpackbits(k.astype(">u8").view(np.uint8).reshape(-1, 8), axis=1)[:, ::-1].reshape(-1)
+    lens = [int(sum(int(bits[4 * L + 8 * h + j]) << j for j in range(8))) for h in range(2)]
+    dec = {0: 1, 1: -1, 2: 2, 3: -2}
+    out = np.zeros(2 * L, np.int32)
+    for h in range(2):
+        for i in range(lens[h]):
+            c = int(bits[2 * (h * L + i)]) | (int(bits[2 * (h * L + i) + 1]) << 1)
+            out[h * L + i] = dec[c]
+    return out
+
+
+def _drive(mode, pres, budget, cyclical=False):
+    """The production engine, with the GPU expansion replaced by the oracle (test only)."""
+    import ctypes
+    p = np.asarray(pres)
+    L = len(p) // 2
+    lib = _lib.load()
+    kw = _lib.key_words(L)
+    h = lib.acx_search_create(mode, L, E._pack_key(p.astype(np.int64), L).ctypes.data, budget)
+    try:
+        buf = np.zeros((256, kw), np.uint64)
+        status = 0
+        while status == 0:
+            n = lib.acx_search_next_batch(h, buf.ctypes.data, 256)
+            if n == 0:
+                break
+            parents = np.stack([_unpack_key_host(buf[i], L) for i in range(n)])
+            keys = np.ascontiguousarray(_oracle_keys(parents, L, cyclical))
+            status = lib.acx_search_feed(h, keys.ctypes.data, n)
+        status = lib.acx_search_status(h, None, None, None)
+        acts = np.zeros(4096, np.int32)
+        tots = np.zeros(4096, np.int32)
+        m = lib.acx_search_path(h, acts.ctypes.data, tots.ctypes.data, 4096)
+        return status == 1, [(int(acts[i]), int(tots[i])) for i in range(m)]
+    finally:
+        lib.acx_search_destroy(h)
+
+
+def test_key_packing_roundtrip():
+    rng = np.random.default_rng(0)
+    for L in (1, 7, 36, 50, 128):
+        for _ in range(20):
+            s = np.zeros(2 * L, np.int64)
+            for h in range(2):
+                n = int(rng.integers(0, L + 1))
+                s[h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+            assert np.array_equal(_unpack_key_host(E._pack_key(s, L), L), s)
+
+
+def test_engine_matches_reference_searches_on_oracle_expansions():
+    with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+        kat = json.load(f)
+    ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+    ok, path = _drive(E.BFS, ak2, 10 ** 6)
+    assert [ok, path] == [kat["bfs_ak2"][0], [tuple(x) for x in kat["bfs_ak2"][1]]]
+    ok, path = _drive(E.BFS, ak2, 10)
+    assert not ok and kat["bfs_ak2_budget10"] == [False, None]
+    ok, path = _drive(E.GREEDY, ak2, 10 ** 6)
+    assert [ok, path] == [kat["greedy_ak2"][0], [tuple(x) for x in kat["greedy_ak2"][1]]]
+    ok, path = _drive(E.GREEDY, ak2, 10)
+    assert [ok, path] == [kat["greedy_ak2_budget10"][0], [tuple(x) for x in kat["greedy_ak2_budget10"][1]]]
+
+
+@pytest.mark.slow
+def test_engine_miller_schupp_cases_on_oracle_expansions():
+    with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+        kat = json.load(f)
+    case = kat["miller_schupp"][2]  # bfs, n in [1,2], |w| in [1,2], budget 1e4
+    solved, paths = [], []
+    for pres in case["presentations"]:
+        ok, path = _drive(E.BFS, np.array(pres), case["budget"])
+        if ok:
+            solved.append(pres)
+            paths.append([list(x) for x in path])
+    assert solved == case["solved"]
+    assert paths == case["paths"]

@@ -1,0 +1,338 @@
+"""GPU parity: the HIP kernels (through libacx.so) against the reference-pinned fixtures and
+the CPU oracle, bit-exact.  Needs an MI355X: run with `pytest -m gpu`."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def _gpu_move(states, actions, L, cyc):
+    import acx
+    s = torch.as_tensor(np.ascontiguousarray(states, dtype=np.int32)).to(DEV)
+    a = torch.as_tensor(np.ascontiguousarray(actions, dtype=np.int32)).to(DEV)
+    B = s.shape[0]
+    lens = torch.empty((B, 2), dtype=torch.int32, device=DEV)
+    err = torch.empty((B,), dtype=torch.uint8, device=DEV)
+    out = acx.ops.step(s, a, cyclical=bool(cyc), lengths=lens, err=err)
+    return out.cpu().numpy(), lens.cpu().numpy(), err.cpu().numpy()
+
+
+def _has_inner_zero(states, L):
+    bad = np.zeros(states.shape[0], bool)
+    for h in range(2):
+        half = states[:, h * L : (h + 1) * L]
+        nz = half != 0
+        n = nz.sum(1)
+        idx = np.arange(L)[None, :]
+        bad |= (nz & (idx >= n[:, None])).any(1)
+    return bad
+
+
+@pytest.mark.parametrize("L", [7, 18, 36, 128])
+@pytest.mark.parametrize("cyc", [1, 0])
+def test_transitions_fixture(L, cyc):
+    d = _load("transitions.npz")
+    k = f"L{L}_c{cyc}_"
+    out, lens, err = _gpu_move(d[k + "state_in"], d[k + "action"], L, cyc)
+    assert np.array_equal(err, d[k + "err"].astype(np.uint8))
+    ok = err == 0
+    assert np.array_equal(out[ok], d[k + "state_out"][ok].astype(np.int32))
+    assert np.array_equal(lens[ok], d[k + "lengths"][ok].astype(np.int32))
+    # an env with err keeps its input
+    assert np.array_equal(out[~ok], d[k + "state_in"][~ok].astype(np.int32))
+
+
+@pytest.mark.parametrize("L", range(1, 10))
+def test_smallL_fixture_including_errors(L):
+    d = _load("smallL_random.npz")
+    s, a, c = d[f"L{L}_state_in"], d[f"L{L}_action"], d[f"L{L}_cyclical"]
+    exp_out, exp_len, exp_err = d[f"L{L}_state_out"], d[f"L{L}_lengths"], d[f"L{L}_err"]
+    inner = _has_inner_zero(s, L)
+    for cyc in (0, 1):
+        m = c == cyc
+        out, lens, err = _gpu_move(s[m], a[m], L, cyc)
+        dom = ~inner[m]
+        # inside the domain: identical outputs and identical error classes
+        assert np.array_equal(err[dom], exp_err[m][dom].astype(np.uint8))
+        ok = dom & (err == 0)
+        assert np.array_equal(out[ok], exp_out[m][ok].astype(np.int32))
+        assert np.array_equal(lens[ok], exp_len[m][ok].astype(np.int32))
+        # zeros inside a relator: flagged, input untouched
+        assert (err[~dom] == 3).all()
+        assert np.array_equal(out[~dom], s[m][~dom].astype(np.int32))
+
+
+@pytest.mark.parametrize("L", [2, 5, 13, 16, 17, 36, 47, 64, 65, 100, 128])
+@pytest.mark.parametrize("cyc", [1, 0])
+def test_random_walks_vs_oracle(L, cyc):
+    """Random walks from random (partly unreduced) states, every step checked against the oracle."""
+    rng = np.random.default_rng(L * 10 + cyc)
+    B = 4096
+    s = np.zeros((B, 2 * L), np.int32)
+    for b in range(B):
+        for h in range(2):
+            n = int(rng.integers(1, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    for t in range(6):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        exp, elen, eerr = O.move_batch(s, a, L, cyc)
+        out, lens, err = _gpu_move(s, a, L, cyc)
+        assert np.array_equal(err, eerr), t
+        assert np.array_equal(out, exp), t
+        ok = err == 0
+        assert np.array_equal(lens[ok], elen[ok])
+        s = exp
+
+
+def test_bad_action_and_domain_errors():
+    L = 4
+    s = np.array([[1, 2, 0, 0, -1, 0, 0, 0]] * 4, np.int32)
+    out, lens, err = _gpu_move(s, [12, -1, 3, 7], L, 1)
+    assert err.tolist()[:2] == [4, 4]
+    s2 = np.array([[1, 3, 0, 0, -1, 0, 0, 0], [1, 0, 0, 0, -1, 0, 0, 0],
+                   [1, 2, 0, 0, 700, 0, 0, 0], [1, 0, 2, 0, -1, 0, 0, 0]], np.int32)
+    out, lens, err = _gpu_move(s2, [0, 0, 0, 0], L, 1)
+    assert err.tolist() == [3, 0, 3, 3]
+    assert np.array_equal(out[[0, 2, 3]], s2[[0, 2, 3]])
+
+
+def test_expand12_goldens_and_keys():
+    import acx
+    d = _load("expand12.npz")
+    for tag, L in (("AK3_L36", 36), ("AK2_L7", 7)):
+        par = torch.as_tensor(d[tag + "_parents"].astype(np.int32)).to(DEV)
+        res = acx.ops.expand12(par, cyclical=False, keys=True)
+        assert not res["err"].any()
+        assert np.array_equal(res["children"].cpu().numpy(), d[tag + "_children"].astype(np.int32))
+        assert np.array_equal(res["lengths"].cpu().numpy(), d[tag + "_lengths"].astype(np.int32))
+        back, lens = acx.ops.unpack_keys(res["keys"].reshape(-1, res["keys"].shape[-1]), L, lengths=True)
+        assert torch.equal(back, res["children"].reshape(-1, 2 * L))
+        assert torch.equal(lens, res["lengths"].reshape(-1, 2))
+        # equal keys <=> equal states
+        k = res["keys"].reshape(-1, res["keys"].shape[-1]).cpu().numpy()
+        c = res["children"].reshape(-1, 2 * L).cpu().numpy()
+        _, ik = np.unique(k, axis=0, return_inverse=True)
+        _, ic = np.unique(c, axis=0, return_inverse=True)
+        assert np.array_equal(ik.reshape(-1), ic.reshape(-1))
+
+
+@pytest.mark.parametrize("L", [7, 36, 128])
+@pytest.mark.parametrize("cyc", [0, 1])
+def test_expand12_vs_oracle(L, cyc):
+    import acx
+    rng = np.random.default_rng(L + cyc)
+    N = 1000
+    s = np.zeros((N, 2 * L), np.int32)
+    for b in range(N):
+        for h in range(2):
+            n = int(rng.integers(1, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    ch, lens, err = O.expand12(s, L, cyc)
+    res = acx.ops.expand12(torch.as_tensor(s).to(DEV), cyclical=bool(cyc), keys=True)
+    assert np.array_equal(res["err"].cpu().numpy(), err)
+    assert np.array_equal(res["children"].cpu().numpy(), ch)
+    ok = err == 0
+    assert np.array_equal(res["lengths"].cpu().numpy()[ok], lens[ok])
+
+
+@pytest.mark.parametrize("L", [3, 36, 128])
+def test_canonicalize_vs_oracle(L):
+    import acx
+    rng = np.random.default_rng(L)
+    B = 2000
+    s = np.zeros((B, 2 * L), np.int32)
+    for b in range(B):
+        for h in range(2):
+            n = int(rng.integers(0 if b % 50 == 0 else 1, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    for cyc in (0, 1):
+        out, lens, err = acx.ops.canonicalize(torch.as_tensor(s).to(DEV), cyclical=bool(cyc))
+        out, lens, err = out.cpu().numpy(), lens.cpu().numpy(), err.cpu().numpy()
+        for b in range(B):
+            e, le, ee = O.simplify_presentation(s[b], L, cyc)
+            assert err[b] == ee, b
+            if ee == 0:
+                assert np.array_equal(out[b], e) and lens[b].tolist() == le
+
+
+def test_kat_paths_through_acmove():
+    from acx import ACMove
+    from acx.envs.utils import is_presentation_trivial
+    with open(os.path.join(GOLDEN, "kat_paths.json")) as f:
+        paths = json.load(f)
+    for p in paths:
+        # long paths replayed in one batched walk: a (1, 2L) state stepped len(actions) times
+        L = p["L"]
+        s = np.array(p["start"], np.int64)
+        totals = []
+        if len(p["actions"]) <= 60:
+            for a in p["actions"]:
+                s, lens = ACMove(a, s, L, None, cyclical=bool(p["cyclical"]))
+                totals.append(sum(lens))
+        else:
+            st = s.astype(np.int32)[None]
+            for a in p["actions"]:
+                st, lens, err = _gpu_move(st, [a], L, p["cyclical"])
+                assert err[0] == 0
+                totals.append(int(lens[0].sum()))
+            s = st[0]
+        assert totals == p["totals"], p["name"]
+        assert list(map(int, s)) == p["final"]
+        assert is_presentation_trivial(s) == p["trivial"]
+
+
+def test_env_config1():
+    from acx import ACEnv, ACEnvConfig
+    with open(os.path.join(GOLDEN, "config1.json")) as f:
+        rows = json.load(f)
+    for row in rows:
+        env = ACEnv(ACEnvConfig(initial_state=[1, 0, 2, 0]))
+        env.reset()
+        s, r, d, tr, info = env.step(row["action"])
+        assert s.tolist() == row["state"]
+        assert (r, d, tr) == (row["reward"], row["done"], row["truncated"])
+        assert {k: list(v) for k, v in info.items()} == row["info"]
+        assert env.lengths == row["lengths"]
+
+
+def test_vec_env_episodes_fixture():
+    """VecACEnv.step (same-step autoreset) against ACEnv episodes run by the reference."""
+    from acx import VecACEnv
+    d = _load("env_episodes.npz")
+    env = VecACEnv(d["initial"].astype(np.int32), horizon_length=int(d["horizon"]), device=DEV)
+    for t in range(d["actions"].shape[0]):
+        obs, rew, done, trunc, info = env.step(torch.as_tensor(d["actions"][t].astype(np.int32)).to(DEV))
+        assert np.array_equal(rew.cpu().numpy(), d["reward"][t]), t
+        assert np.array_equal(done.cpu().numpy(), d["done"][t].astype(np.uint8)), t
+        assert np.array_equal(trunc.cpu().numpy(), d["truncated"][t].astype(np.uint8)), t
+        assert np.array_equal(obs.cpu().numpy(), d["obs"][t].astype(np.int32)), t
+        m = (d["done"][t] | d["truncated"][t]).astype(bool)
+        assert np.array_equal(info["final_observation"].cpu().numpy()[m], d["final_obs"][t][m].astype(np.int32))
+    assert int(env.err_count.item()) == 0
+
+
+def test_rollout_equals_repeated_step_and_fixture():
+    from acx import VecACEnv
+    d = _load("env_episodes.npz")
+    L, H = int(d["L"]), int(d["horizon"])
+    init = d["initial"].astype(np.int32)
+    acts = torch.as_tensor(d["actions"].astype(np.int32)).to(DEV)
+    T, B = acts.shape
+    env = VecACEnv(init, horizon_length=H, device=DEV)
+    obs = torch.empty((T, B, 2 * L), dtype=torch.int32, device=DEV)
+    rew = torch.empty((T, B), dtype=torch.int32, device=DEV)
+    dn = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    tr = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    # two launches (T/2 each) to also check the carried step_count / state
+    env.rollout(acts[: T // 2], obs[: T // 2], rew[: T // 2], dn[: T // 2], tr[: T // 2])
+    env.rollout(acts[T // 2 :], obs[T // 2 :], rew[T // 2 :], dn[T // 2 :], tr[T // 2 :])
+    assert np.array_equal(obs.cpu().numpy(), d["obs"].astype(np.int32))
+    assert np.array_equal(rew.cpu().numpy(), d["reward"])
+    assert np.array_equal(dn.cpu().numpy(), d["done"].astype(np.uint8))
+    assert np.array_equal(tr.cpu().numpy(), d["truncated"].astype(np.uint8))
+    assert int(env.err_count.item()) == 0
+
+
+def _ms_starts(L, B):
+    import acx
+    ms = np.load(os.path.join(os.path.dirname(acx.__file__), "data", "all_presentations.npy"))
+    out = np.zeros((B, 2 * L), np.int32)
+    for i in range(B):
+        p = ms[i % len(ms)]
+        a, b = p[:18][p[:18] != 0], p[18:][p[18:] != 0]
+        out[i, : len(a)] = a
+        out[i, L : L + len(b)] = b
+    return out
+
+
+@pytest.mark.parametrize("L", [36, 128])
+def test_full_size_rollout_properties_and_sampled_parity(L):
+    """Full batch (2^20 envs at L=36, 2^17 at L=128): size-independent invariants on every env
+    (valid, freely + cyclically reduced, lengths = letter counts) and bit-exact oracle replay
+    of a sample of envs."""
+    from acx import VecACEnv
+    B = (1 << 20) if L == 36 else (1 << 17)
+    T, H = 24, 10
+    init = _ms_starts(L, B)
+    env = VecACEnv(init, horizon_length=H, device=DEV, track_final_obs=False)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(0)
+    acts = torch.randint(0, 12, (T, B), dtype=torch.int32, device=DEV, generator=g)
+    obs = torch.empty((T, B, 2 * L), dtype=torch.int32, device=DEV)
+    rew = torch.empty((T, B), dtype=torch.int32, device=DEV)
+    dn = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    tr = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    env.rollout(acts, obs, rew, dn, tr)
+    assert int(env.err_count.item()) == 0
+    # invariants on the final states of every env
+    st = env.state
+    nz = st != 0
+    r0, r1 = st[:, :L], st[:, L:]
+    n0, n1 = nz[:, :L].sum(1), nz[:, L:].sum(1)
+    idx = torch.arange(L, device=DEV)[None]
+    assert not (nz[:, :L] & (idx >= n0[:, None])).any() and not (nz[:, L:] & (idx >= n1[:, None])).any()
+    assert (n0 > 0).all() and (n1 > 0).all()
+    for r, n in ((r0, n0), (r1, n1)):
+        adj = (r[:, :-1] == -r[:, 1:]) & (r[:, :-1] != 0)
+        assert not adj.any()
+        last = torch.gather(r, 1, (n - 1).clamp(min=0)[:, None])[:, 0]
+        assert not ((r[:, 0] == -last) & (n > 1)).any()
+    # sampled bit-exact replay
+    rng = np.random.default_rng(1)
+    sample = rng.choice(B, size=512, replace=False)
+    s = init[sample].copy()
+    cnt = np.zeros(len(sample), np.int32)
+    A = acts[:, torch.as_tensor(sample, device=DEV)].cpu().numpy()
+    O_obs = obs[:, torch.as_tensor(sample, device=DEV)].cpu().numpy()
+    O_rew = rew[:, torch.as_tensor(sample, device=DEV)].cpu().numpy()
+    for t in range(T):
+        r, d_, t_, e, _, _ = O.env_step(s, A[t], L, H, cnt, reset_state=init[sample])
+        assert not e.any()
+        assert np.array_equal(s, O_obs[t]), t
+        assert np.array_equal(r, O_rew[t]), t
+
+
+def test_search_kat_ak2():
+    from acx import bfs, greedy_search
+    with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+        kat = json.load(f)
+    ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+    ok, path = bfs(presentation=ak2, max_nodes_to_explore=int(1e6))
+    assert [ok, [list(x) for x in path]] == kat["bfs_ak2"]
+    assert list(bfs(presentation=ak2, max_nodes_to_explore=10)) == [False, None]
+    ok, path = greedy_search(presentation=ak2, max_nodes_to_explore=int(1e6))
+    assert [ok, [list(x) for x in path]] == kat["greedy_ak2"]
+    ok, path = greedy_search(presentation=ak2, max_nodes_to_explore=10)
+    assert [ok, [list(x) for x in path]] == kat["greedy_ak2_budget10"]
+
+
+def test_search_kat_miller_schupp():
+    from acx import bfs, greedy_search
+    with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+        kat = json.load(f)
+    for case in kat["miller_schupp"]:
+        fn = greedy_search if case["search_fn"] == "greedy_search" else bfs
+        solved, unsolved, paths = [], [], []
+        for pres in case["presentations"]:
+            ok, path = fn(presentation=np.array(pres), max_nodes_to_explore=case["budget"])
+            if ok:
+                solved.append(pres)
+                paths.append([list(x) for x in path])
+            else:
+                unsolved.append(pres)
+        assert solved == case["solved"], case["search_fn"]
+        assert unsolved == case["unsolved"], case["search_fn"]
+        assert paths == case["paths"], case["search_fn"]
