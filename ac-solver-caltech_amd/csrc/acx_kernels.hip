@@ -25,14 +25,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "acx.h"
 
 namespace acx {
+
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;  // waves per block
 constexpr uint32_t P55 = 0x55555555u;
+
+// Minimum waves per SIMD requested from the register allocator (__launch_bounds__ 2nd
+// argument).  At L = 36 the step and rollout kernels fit 64 VGPRs without spilling, so
+// 8 waves/SIMD = 8 blocks of 256 per CU: 2048 resident blocks, and a 2^20-env batch
+// (4096 blocks) runs in exactly two full rounds with no partially filled tail round.
+template <int LC>
+struct Occupancy {
+    static constexpr int waves_per_simd = (LC == 36) ? 8 : 1;
+};
 
 // ---------------------------------------------------------------------------------
 // multiword (2 bits per letter) helpers; every loop is over the compile-time NW
@@ -303,7 +315,17 @@ __device__ __forceinline__ bool is_trivial(const Word<NW>& w0, int n0, const Wor
 }
 
 // ---------------------------------------------------------------------------------
-// LDS staging: a wave's tile of up to 64 rows, int8 letters, padded rows
+// LDS staging.  A wave owns a tile of up to 64 consecutive envs.  The tile is moved
+// HBM <-> LDS with coalesced 16-byte (or 8-byte) accesses by all 64 lanes, as int8
+// letters; then each lane packs / unpacks its own row.  Two implementations with one
+// interface:
+//   FastTile   compile-time L with L % 4 == 0 (the L = 36 and L = 128 configs): the LDS
+//              tile is the int8 image of the global tile, row stride S dwords with
+//              S = 2 mod 4 so each lane's 8-byte row reads/writes hit distinct bank
+//              pairs; addresses are affine in the chunk index; pack/unpack are SWAR over
+//              4 letters per dword.
+//   GenericTile  runtime L (parity tests at any L <= 128): per-letter pack/unpack.
+// Rows holding a value outside {-2..2} are flagged (flags[row]) at load time.
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -311,169 +333,20 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// int32 letter -> int8; values outside {-2..2} become 0x7F and flag the row
+// int32 letter -> int8; values outside {-2..2} become 0x7F and set `bad`
 __device__ __forceinline__ uint32_t to_i8(int32_t v, bool& bad) {
     const bool ok = (uint32_t)(v + 2) <= 4u;
     bad |= !ok;
     return ok ? ((uint32_t)v & 0xffu) : 0x7fu;
 }
 
-// Compile-time geometry when LC > 0 (L == LC), runtime L otherwise.  LMAX letters are
-// scanned per relator (compile-time loop bound); rows are LROW bytes so that reading
-// LMAX letters of relator 1 stays inside the row.
-template <int NW, int LC>
-struct Geo {
-    static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
-    int L, twoL, rowb;
-    __device__ __forceinline__ Geo(int L_) {
-        L = LC > 0 ? LC : L_;
-        twoL = 2 * L;
-        const int bytes = (LC > 0) ? 2 * LC : (L + LMAX);
-        int dw = (bytes + 3) >> 2;
-        dw |= 1;  // odd dword stride: lane l's k-th dword is in bank (l*dw + k) mod 32
-        rowb = dw * 4;
-    }
-};
-
-// (row, pos) of the first element of chunk `c`, chunks of VEC int32 (never straddle rows)
-struct ChunkIter {
-    int row, pos, dq, dr, twoL;
-    __device__ __forceinline__ ChunkIter(int c0, int vec, int twoL_, int stride_chunks) : twoL(twoL_) {
-        const int e0 = c0 * vec;
-        row = e0 / twoL;
-        pos = e0 - row * twoL;
-        const int de = stride_chunks * vec;
-        dq = de / twoL;
-        dr = de - dq * twoL;
-    }
-    __device__ __forceinline__ void next() {
-        pos += dr;
-        row += dq;
-        if (pos >= twoL) { pos -= twoL; ++row; }
-    }
-};
-
-constexpr int STAGE_UNROLL = 8;
-
-// global (R rows of 2L int32, row pitch `gpitch` elements) -> LDS tile; flags[row] = 1
-// for rows holding a letter outside {-2..2}.  All 64 lanes must call.
-template <int VEC>
-__device__ __forceinline__ void stage_in(const int32_t* __restrict__ g, int64_t gpitch, int R, int twoL,
-                                         int rowb, char* lds, uint8_t* flags, int lane) {
-    flags[lane] = 0;
-    wave_sync();
-    const int nc = (R * twoL) / VEC;
-    ChunkIter it(lane, VEC, twoL, WAVE);
-    for (int base = lane; base < nc; base += WAVE * STAGE_UNROLL) {
-        int rows[STAGE_UNROLL], poss[STAGE_UNROLL];
-        int32_t v[STAGE_UNROLL][VEC];
-#pragma unroll
-        for (int u = 0; u < STAGE_UNROLL; ++u) {
-            rows[u] = it.row;
-            poss[u] = it.pos;
-            it.next();
-            const int c = base + u * WAVE;
-            if (c < nc) {
-                const int32_t* src = g + (int64_t)rows[u] * gpitch + poss[u];
-                if constexpr (VEC == 4) {
-                    const int4 x = *reinterpret_cast<const int4*>(src);
-                    v[u][0] = x.x; v[u][1] = x.y; v[u][2] = x.z; v[u][3] = x.w;
-                } else {
-                    const int2 x = *reinterpret_cast<const int2*>(src);
-                    v[u][0] = x.x; v[u][1] = x.y;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < STAGE_UNROLL; ++u) {
-            const int c = base + u * WAVE;
-            if (c < nc) {
-                bool bad = false;
-                char* dst = lds + rows[u] * rowb + poss[u];
-                if constexpr (VEC == 4) {
-                    const uint32_t p = to_i8(v[u][0], bad) | (to_i8(v[u][1], bad) << 8) |
-                                       (to_i8(v[u][2], bad) << 16) | (to_i8(v[u][3], bad) << 24);
-                    *reinterpret_cast<uint32_t*>(dst) = p;
-                } else {
-                    const uint32_t p = to_i8(v[u][0], bad) | (to_i8(v[u][1], bad) << 8);
-                    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)p;
-                }
-                if (bad) flags[rows[u]] = 1;
-            }
-        }
-    }
-    wave_sync();
-}
-
-// LDS tile -> global (R rows, row pitch `gpitch` elements).  Rows with flags[row] set
-// are copied from `fallback` (pitch `fpitch`) instead (the original int32 input of an
-// env whose letters do not fit int8).  All 64 lanes must call.
-template <int VEC>
-__device__ __forceinline__ void stage_out(int32_t* g, int64_t gpitch, int R, int twoL, int rowb,
-                                          const char* lds, const uint8_t* flags, const int32_t* fallback,
-                                          int64_t fpitch, int lane) {
-    const int nc = (R * twoL) / VEC;
-    ChunkIter it(lane, VEC, twoL, WAVE);
-    for (int c = lane; c < nc; c += WAVE) {
-        const int row = it.row, pos = it.pos;
-        it.next();
-        int32_t* dst = g + (int64_t)row * gpitch + pos;
-        const char* src = lds + row * rowb + pos;
-        if (flags[row] && fallback) {
-            const int32_t* f = fallback + (int64_t)row * fpitch + pos;
-            if constexpr (VEC == 4) *reinterpret_cast<int4*>(dst) = *reinterpret_cast<const int4*>(f);
-            else *reinterpret_cast<int2*>(dst) = *reinterpret_cast<const int2*>(f);
-            continue;
-        }
-        if constexpr (VEC == 4) {
-            const uint32_t p = *reinterpret_cast<const uint32_t*>(src);
-            int4 x;
-            x.x = (int32_t)(int8_t)(p & 0xffu);
-            x.y = (int32_t)(int8_t)((p >> 8) & 0xffu);
-            x.z = (int32_t)(int8_t)((p >> 16) & 0xffu);
-            x.w = (int32_t)(int8_t)(p >> 24);
-            *reinterpret_cast<int4*>(dst) = x;
-        } else {
-            const uint32_t p = *reinterpret_cast<const uint16_t*>(src);
-            int2 x;
-            x.x = (int32_t)(int8_t)(p & 0xffu);
-            x.y = (int32_t)(int8_t)(p >> 8);
-            *reinterpret_cast<int2*>(dst) = x;
-        }
-    }
-}
-
-// one relator: LDS int8 letters -> packed word; `layout_bad` if a letter follows a zero
-template <int NW, int LC>
-__device__ __forceinline__ void pack_relator(const int8_t* src, int L, Word<NW>& w, int& n, bool& layout_bad) {
-    constexpr int LMAX = Geo<NW, LC>::LMAX;
-    w = wzero<NW>();
-    n = 0;
-    bool zero_seen = false;
-#pragma unroll
-    for (int k = 0; k < LMAX; ++k) {
-        int b = src[k];
-        if (LC == 0) b = (k < L) ? b : 0;
-        const bool nz = b != 0;
-        const uint32_t code = nz ? ((((uint32_t)~b & 1u) << 1) | (((uint32_t)b >> 7) & 1u)) : 0u;
-        w.w[k >> 4] |= code << (2 * (k & 15));
-        n += nz;
-        layout_bad |= nz && zero_seen;
-        zero_seen |= !nz;
-    }
-}
-
-// packed word -> LDS int8 letters (L bytes, zero padded)
-template <int NW, int LC>
-__device__ __forceinline__ void unpack_relator(int8_t* dst, int L, const Word<NW>& w, int n) {
-    constexpr int LMAX = Geo<NW, LC>::LMAX;
-#pragma unroll
-    for (int k = 0; k < LMAX; ++k) {
-        const uint32_t code = (w.w[k >> 4] >> (2 * (k & 15))) & 3u;
-        // code 0..3 -> 1, -1, 2, -2
-        const uint32_t letter = (0xFE02FF01u >> (code << 3)) & 0xffu;
-        if (LC > 0 || k < L) dst[k] = (int8_t)(k < n ? letter : 0u);
-    }
+__device__ __forceinline__ int4 widen4(uint32_t p) {
+    int4 x;
+    x.x = (int32_t)(int8_t)(p & 0xffu);
+    x.y = (int32_t)(int8_t)((p >> 8) & 0xffu);
+    x.z = (int32_t)(int8_t)((p >> 16) & 0xffu);
+    x.w = (int32_t)(int8_t)(p >> 24);
+    return x;
 }
 
 template <int NW>
@@ -481,6 +354,387 @@ struct PresRegs {
     Word<NW> w0, w1;
     int n0, n1;
 };
+
+constexpr int STAGE_UNROLL = 8;
+constexpr int ACT_BLOCK = 8;  // steps per packed action register (4 bits each)
+
+// SWAR: 4 int8 letters (one dword) -> 8-bit code field (2 bits per letter, x=0 X=1 y=2 Y=3,
+// zero letters -> 0) and a 4-bit non-zero mask
+__device__ __forceinline__ void swar_pack4(uint32_t d, uint32_t& c8, uint32_t& nz4) {
+    const uint32_t nz = (d | (d >> 1)) & 0x01010101u;            // letter != 0
+    const uint32_t c1 = ~d & nz;                                  // code bit 1: |letter| == 2
+    const uint32_t c0 = (d >> 7) & 0x01010101u;                   // code bit 0: letter < 0
+    const uint32_t cb = (c1 << 1) | c0;                           // one code per byte
+    const uint32_t t = cb | (cb >> 6);
+    c8 = (t & 0xfu) | ((t >> 12) & 0xf0u);
+    const uint32_t u = nz | (nz >> 7);
+    nz4 = (u & 3u) | ((u >> 14) & 0xcu);
+}
+
+// SWAR: 8-bit code field -> 4 int8 letters, letters at index >= n_in (0..4) zeroed
+__device__ __forceinline__ uint32_t swar_unpack4(uint32_t c8, int n_in) {
+    const uint32_t b = (c8 & 3u) | ((c8 & 0xcu) << 6) | ((c8 & 0x30u) << 12) | ((c8 & 0xc0u) << 18);
+    const uint32_t b0 = b & 0x01010101u;
+    const uint32_t b1 = (b >> 1) & 0x01010101u;
+    const uint32_t m0 = b0 * 0xffu;  // 0xff in bytes of negative letters
+    const uint32_t v = (m0 & ~b1) | (~m0 & (0x01010101u + b1));
+    const uint32_t keep = n_in >= 4 ? 0xffffffffu : (n_in <= 0 ? 0u : ((1u << (8 * n_in)) - 1u));
+    return v & keep;
+}
+
+template <int NW, int LC>
+struct FastTile {
+    static_assert(LC > 0 && LC % 4 == 0, "FastTile needs a compile-time L multiple of 4");
+    static constexpr int L = LC;
+    static constexpr int twoL = 2 * LC;
+    static constexpr int CPR = LC / 2;  // 16-byte chunks (4 letters) per row
+    static constexpr int S = (CPR % 4 == 2) ? CPR : CPR + 2;  // LDS row stride (dwords), = 2 mod 4
+    static constexpr int HALF = CPR / 2;  // dwords per relator
+    static_assert(S % 4 == 2, "row stride must be 2 mod 4 dwords");
+    static constexpr int LOAD_BATCH = 6;
+
+    uint32_t* lds;
+    uint8_t* flags;
+    bool tile_bad = false;  // wave-uniform: some row of the last load was flagged
+
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    __device__ __forceinline__ FastTile(char* base, int) {
+        lds = reinterpret_cast<uint32_t*>(base);
+        flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
+    }
+    __device__ __forceinline__ int Lr() const { return L; }
+    __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(lds + r * S); }
+
+    // LDS dword index of chunk c = lane + 64u (compile-time u)
+    __device__ __forceinline__ static int lds_index(int ln, int u) {
+        if constexpr (S == CPR) return ln + WAVE * u;           // unpadded: LDS image is flat
+        else if constexpr (CPR == WAVE) return u * S + ln;      // one row per wave-instruction
+        else {
+            const int c = ln + WAVE * u;
+            const int r = c / CPR;
+            return r * S + (c - r * CPR);
+        }
+    }
+
+    // global rows (contiguous, 2L int32 each) -> LDS
+    __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // keep the address math here (no hoisting into the caller)
+        flags[ln] = 0;
+        wave_sync();
+        const int nc = R * CPR;
+        const int4* src = reinterpret_cast<const int4*>(g) + ln;
+        bool any_bad = false;
+        if (R == WAVE) {  // full tile (wave-uniform): unguarded, LOAD_BATCH loads in flight
+#pragma unroll
+            for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
+                int4 v[LOAD_BATCH];
+#pragma unroll
+                for (int u = 0; u < LOAD_BATCH; ++u)
+                    if (u0 + u < CPR) v[u] = src[(u0 + u) * WAVE];
+#pragma unroll
+                for (int u = 0; u < LOAD_BATCH; ++u) {
+                    if (u0 + u >= CPR) continue;
+                    bool bad = false;
+                    const uint32_t p = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
+                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                    lds[lds_index(ln, u0 + u)] = p;
+                    if (bad) flags[(ln + (u0 + u) * WAVE) / CPR] = 1;
+                    any_bad |= bad;
+                }
+            }
+        } else {
+            for (int u = 0; u < CPR; ++u) {
+                const int c = ln + u * WAVE;
+                if (c < nc) {
+                    const int4 v = src[u * WAVE];
+                    bool bad = false;
+                    const uint32_t p = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
+                                       (to_i8(v.w, bad) << 24);
+                    const int r = c / CPR;
+                    lds[r * S + (c - r * CPR)] = p;
+                    if (bad) flags[r] = 1;
+                    any_bad |= bad;
+                }
+            }
+        }
+        tile_bad = __any(any_bad);
+        wave_sync();
+    }
+
+    // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from fallback
+    template <bool FB>
+    __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
+                                          int64_t fpitch, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        if (gpitch == twoL && !(FB && tile_bad)) {
+            // contiguous rows, nothing flagged: chunk c goes to g + 4c (immediate offsets)
+            int4* dst = reinterpret_cast<int4*>(g) + ln;
+#pragma unroll
+            for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+                uint32_t p[STAGE_UNROLL];
+#pragma unroll
+                for (int u = 0; u < STAGE_UNROLL; ++u)
+                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
+#pragma unroll
+                for (int u = 0; u < STAGE_UNROLL; ++u)
+                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) dst[(u0 + u) * WAVE] = widen4(p[u]);
+            }
+            return;
+        }
+#pragma unroll
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                const int c = ln + (u0 + u) * WAVE;
+                if (u0 + u < CPR && c < nc) {
+                    const int r = c / CPR;
+                    const int pos = 4 * (c - r * CPR);
+                    int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
+                    if (FB && flags[r]) *dst = *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos);
+                    else *dst = widen4(p[u]);
+                }
+            }
+        }
+    }
+
+    // lane's row -> packed registers; returns true if the row is outside the domain
+    __device__ __forceinline__ bool pack(int lane, PresRegs<NW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t* src = lds + ln * S;
+        uint32_t d[CPR];
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) {
+            const uint2 x = *reinterpret_cast<const uint2*>(src + k);
+            d[k] = x.x;
+            d[k + 1] = x.y;
+        }
+        bool bad = flags[ln] != 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            Word<NW> w = wzero<NW>();
+            uint64_t mlo = 0, mhi = 0;
+#pragma unroll
+            for (int k = 0; k < HALF; ++k) {
+                uint32_t c8, nz4;
+                swar_pack4(d[h * HALF + k], c8, nz4);
+                w.w[k >> 2] |= c8 << (8 * (k & 3));
+                if (k < 16) mlo |= (uint64_t)nz4 << (4 * k);
+                else mhi |= (uint64_t)nz4 << (4 * (k - 16));
+            }
+            const int n = __builtin_popcountll(mlo) + __builtin_popcountll(mhi);
+            // zeros only as right padding <=> mask == low n bits
+            const uint64_t elo = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+            const uint64_t ehi = n <= 64 ? 0ull : (n >= 128 ? ~0ull : ((1ull << (n - 64)) - 1ull));
+            bad |= (mlo != elo) || (mhi != ehi);
+            if (h == 0) { p.w0 = w; p.n0 = n; }
+            else        { p.w1 = w; p.n1 = n; }
+        }
+        return bad;
+    }
+
+    // packed registers -> lane's row
+    __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        uint32_t d[CPR];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const Word<NW>& w = h ? p.w1 : p.w0;
+            const int n = h ? p.n1 : p.n0;
+#pragma unroll
+            for (int k = 0; k < HALF; ++k)
+                d[h * HALF + k] = swar_unpack4((w.w[k >> 2] >> (8 * (k & 3))) & 0xffu, n - 4 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
+    }
+};
+
+template <int NW, int LC, int VEC>
+struct GenericTile {
+    static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
+    int L, twoL, rowb;
+    char* base;
+    uint8_t* flags;
+
+    static __host__ __device__ int row_bytes(int L_) {
+        const int bytes = (LC > 0) ? 2 * LC : (L_ + LMAX);
+        return (((bytes + 3) >> 2) | 1) * 4;  // odd dword stride: conflict-free per-lane reads
+    }
+    static __host__ __device__ size_t wave_bytes(int L_) { return (size_t)WAVE * row_bytes(L_) + WAVE; }
+    __device__ __forceinline__ GenericTile(char* b, int L_) {
+        L = LC > 0 ? LC : L_;
+        twoL = 2 * L;
+        rowb = row_bytes(L);
+        base = b;
+        flags = reinterpret_cast<uint8_t*>(b + WAVE * rowb);
+    }
+    __device__ __forceinline__ int Lr() const { return L; }
+    __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(base + r * rowb); }
+
+    // (row, pos) of a chunk of VEC int32; chunks never straddle rows (2L % VEC == 0)
+    struct It {
+        int row, pos, dq, dr, twoL;
+        __device__ __forceinline__ It(int c0, int twoL_) : twoL(twoL_) {
+            const int e0 = c0 * VEC;
+            row = e0 / twoL;
+            pos = e0 - row * twoL;
+            dq = (WAVE * VEC) / twoL;
+            dr = WAVE * VEC - dq * twoL;
+        }
+        __device__ __forceinline__ void next() {
+            pos += dr;
+            row += dq;
+            if (pos >= twoL) { pos -= twoL; ++row; }
+        }
+    };
+
+    __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
+        flags[lane] = 0;
+        wave_sync();
+        const int nc = (R * twoL) / VEC;
+        It it(lane, twoL);
+        for (int b0 = lane; b0 < nc; b0 += WAVE * STAGE_UNROLL) {
+            int rows[STAGE_UNROLL], poss[STAGE_UNROLL];
+            int32_t v[STAGE_UNROLL][VEC];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                rows[u] = it.row;
+                poss[u] = it.pos;
+                it.next();
+                if (b0 + u * WAVE < nc) {
+                    const int32_t* src = g + (int64_t)rows[u] * twoL + poss[u];
+                    if constexpr (VEC == 4) {
+                        const int4 x = *reinterpret_cast<const int4*>(src);
+                        v[u][0] = x.x; v[u][1] = x.y; v[u][2] = x.z; v[u][3] = x.w;
+                    } else {
+                        const int2 x = *reinterpret_cast<const int2*>(src);
+                        v[u][0] = x.x; v[u][1] = x.y;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                if (b0 + u * WAVE < nc) {
+                    bool bad = false;
+                    char* dst = base + rows[u] * rowb + poss[u];
+                    if constexpr (VEC == 4) {
+                        *reinterpret_cast<uint32_t*>(dst) = to_i8(v[u][0], bad) | (to_i8(v[u][1], bad) << 8) |
+                                                            (to_i8(v[u][2], bad) << 16) | (to_i8(v[u][3], bad) << 24);
+                    } else {
+                        *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(to_i8(v[u][0], bad) | (to_i8(v[u][1], bad) << 8));
+                    }
+                    if (bad) flags[rows[u]] = 1;
+                }
+            }
+        }
+        wave_sync();
+    }
+
+    template <bool FB>
+    __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
+                                          int64_t fpitch, int lane) const {
+        const int nc = (R * twoL) / VEC;
+        It it(lane, twoL);
+        for (int b0 = lane; b0 < nc; b0 += WAVE * STAGE_UNROLL) {
+            int rows[STAGE_UNROLL], poss[STAGE_UNROLL];
+            uint32_t p[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                rows[u] = it.row;
+                poss[u] = it.pos;
+                it.next();
+                p[u] = 0;
+                if (b0 + u * WAVE < nc) {
+                    const char* src = base + rows[u] * rowb + poss[u];
+                    if constexpr (VEC == 4) p[u] = *reinterpret_cast<const uint32_t*>(src);
+                    else p[u] = *reinterpret_cast<const uint16_t*>(src);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                if (b0 + u * WAVE >= nc) continue;
+                int32_t* dst = g + (int64_t)rows[u] * gpitch + poss[u];
+                const bool fb = FB && flags[rows[u]];
+                const int32_t* f = fallback + (int64_t)rows[u] * fpitch + poss[u];
+                if constexpr (VEC == 4) {
+                    *reinterpret_cast<int4*>(dst) = fb ? *reinterpret_cast<const int4*>(f) : widen4(p[u]);
+                } else {
+                    int2 x;
+                    x.x = (int32_t)(int8_t)(p[u] & 0xffu);
+                    x.y = (int32_t)(int8_t)((p[u] >> 8) & 0xffu);
+                    *reinterpret_cast<int2*>(dst) = fb ? *reinterpret_cast<const int2*>(f) : x;
+                }
+            }
+        }
+    }
+
+    __device__ __forceinline__ void pack_relator(const int8_t* src, Word<NW>& w, int& n, bool& bad) const {
+        w = wzero<NW>();
+        n = 0;
+        bool zero_seen = false;
+#pragma unroll
+        for (int k = 0; k < LMAX; ++k) {
+            int b = src[k];
+            if (LC == 0) b = (k < L) ? b : 0;
+            const bool nz = b != 0;
+            const uint32_t code = nz ? ((((uint32_t)~b & 1u) << 1) | (((uint32_t)b >> 7) & 1u)) : 0u;
+            w.w[k >> 4] |= code << (2 * (k & 15));
+            n += nz;
+            bad |= nz && zero_seen;
+            zero_seen |= !nz;
+        }
+    }
+    __device__ __forceinline__ bool pack(int lane, PresRegs<NW>& p) const {
+        const int8_t* r = row(lane);
+        bool bad = flags[lane] != 0;
+        pack_relator(r, p.w0, p.n0, bad);
+        pack_relator(r + L, p.w1, p.n1, bad);
+        return bad;
+    }
+    __device__ __forceinline__ void unpack_relator(int8_t* dst, const Word<NW>& w, int n) const {
+#pragma unroll
+        for (int k = 0; k < LMAX; ++k) {
+            const uint32_t code = (w.w[k >> 4] >> (2 * (k & 15))) & 3u;
+            const uint32_t letter = (0xFE02FF01u >> (code << 3)) & 0xffu;  // code -> 1, -1, 2, -2
+            if (LC > 0 || k < L) dst[k] = (int8_t)(k < n ? letter : 0u);
+        }
+    }
+    __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const {
+        int8_t* r = row(lane);
+        unpack_relator(r, p.w0, p.n0);
+        unpack_relator(r + L, p.w1, p.n1);
+    }
+};
+
+template <int NW, int LC, int VEC>
+using TileFor = typename std::conditional<(LC > 0 && LC % 4 == 0), FastTile<NW, LC>, GenericTile<NW, LC, VEC>>::type;
+
+// common per-wave prologue: tile index, rows in the tile, LDS slice
+struct WaveCtx {
+    int lane, wid;
+    int64_t r0;
+    int R;
+    bool active;
+};
+__device__ __forceinline__ bool wave_ctx(int64_t rows, WaveCtx& w) {
+    w.lane = threadIdx.x & (WAVE - 1);
+    w.wid = threadIdx.x / WAVE;
+    w.r0 = ((int64_t)blockIdx.x * WPB + w.wid) * WAVE;
+    if (w.r0 >= rows) return false;
+    w.R = (int)((rows - w.r0) < WAVE ? (rows - w.r0) : WAVE);
+    w.active = w.lane < w.R;
+    return true;
+}
 
 // ---------------------------------------------------------------------------------
 // kernels
@@ -503,60 +757,44 @@ struct StepArgs {
 };
 
 template <int NW, int LC, int VEC>
-__global__ __launch_bounds__(BLOCK) void step_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Geo<NW, LC> geo(a.L);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x / WAVE;
-    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * WAVE;
-    if (r0 >= a.B) return;
-    const int R = (int)((a.B - r0) < WAVE ? (a.B - r0) : WAVE);
-    char* tile = smem + wid * (WAVE * geo.rowb + WAVE);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(tile + WAVE * geo.rowb);
-    const int64_t env = r0 + lane;
-    const bool active = lane < R;
+    WaveCtx w;
+    if (!wave_ctx(a.B, w)) return;
+    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    const int64_t env = w.r0 + w.lane;
 
-    stage_in<VEC>(a.state_in + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, lane);
+    tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
 
-    int e = ACX_ERR_NONE;
-    if (active) {
-        int8_t* row = reinterpret_cast<int8_t*>(tile + lane * geo.rowb);
+    if (w.active) {
         PresRegs<NW> p;
-        bool layout_bad = flags[lane] != 0;
-        pack_relator<NW, LC>(row, geo.L, p.w0, p.n0, layout_bad);
-        pack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1, layout_bad);
         const int act = a.action[env];
-        if (layout_bad) {
-            e = ACX_ERR_DOMAIN;
-        } else {
-            e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, geo.L, a.cyclical != 0);
-        }
-        if (e == ACX_ERR_NONE) {
-            unpack_relator<NW, LC>(row, geo.L, p.w0, p.n0);
-            unpack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1);
-        }
+        int cnt = a.step_count ? a.step_count[env] + 1 : 0;
+        const bool bad = tile.pack(w.lane, p);
+        int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, a.cyclical != 0);
+        if (e == ACX_ERR_NONE) tile.unpack(w.lane, p);
         const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
-        const int total = p.n0 + p.n1;
-        int cnt = 0;
-        if (a.step_count) cnt = a.step_count[env] + 1;
         const bool trunc = a.step_count ? (cnt >= a.horizon) : false;
-        if (a.reward) a.reward[env] = triv ? a.horizon * geo.L * 2 : -total;
+        if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
         int l0 = p.n0, l1 = p.n1;
         if ((triv || trunc) && a.reset_state && e == ACX_ERR_NONE) {
-            // same-step autoreset: final_obs <- post-move state, state <- reset row
+            // same-step autoreset (rare): final_obs <- post-move state, state <- reset row
+            int8_t* row = tile.row(w.lane);
             if (a.final_obs) {
-                int32_t* fo = a.final_obs + env * geo.twoL;
-                for (int k = 0; k < geo.twoL; ++k) fo[k] = (int32_t)row[k];
+                int32_t* fo = a.final_obs + env * twoL;
+                for (int k = 0; k < twoL; ++k) fo[k] = (int32_t)row[k];
             }
-            const int32_t* rs = a.reset_state + env * geo.twoL;
+            const int32_t* rs = a.reset_state + env * twoL;
             l0 = 0;
             l1 = 0;
-            for (int k = 0; k < geo.twoL; ++k) {
+            for (int k = 0; k < twoL; ++k) {
                 const int32_t v = rs[k];
                 row[k] = (int8_t)v;
-                if (k < geo.L) l0 += v != 0;
+                if (k < L) l0 += v != 0;
                 else l1 += v != 0;
             }
             cnt = 0;
@@ -570,8 +808,7 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(StepArgs a) {
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
     wave_sync();
-    stage_out<VEC>(a.state_out + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags,
-                   a.state_in + r0 * geo.twoL, geo.twoL, lane);
+    tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
 }
 
 struct RolloutArgs {
@@ -590,47 +827,57 @@ struct RolloutArgs {
 };
 
 template <int NW, int LC, int VEC>
-__global__ __launch_bounds__(BLOCK) void rollout_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_kernel(RolloutArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Geo<NW, LC> geo(a.L);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x / WAVE;
-    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * WAVE;
-    if (r0 >= a.B) return;
-    const int R = (int)((a.B - r0) < WAVE ? (a.B - r0) : WAVE);
-    char* tile = smem + wid * (WAVE * geo.rowb + WAVE);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(tile + WAVE * geo.rowb);
-    const int64_t env = r0 + lane;
-    const bool active = lane < R;
-    int8_t* row = reinterpret_cast<int8_t*>(tile + lane * geo.rowb);
+    WaveCtx w;
+    if (!wave_ctx(a.B, w)) return;
+    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    const int64_t env = w.r0 + w.lane;
 
     // the reset (starting) state stays packed in registers for the whole rollout
     PresRegs<NW> rs;
     bool bad = false;
-    stage_in<VEC>(a.reset_state + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, lane);
-    if (active) {
-        bad = flags[lane] != 0;
-        pack_relator<NW, LC>(row, geo.L, rs.w0, rs.n0, bad);
-        pack_relator<NW, LC>(row + geo.L, geo.L, rs.w1, rs.n1, bad);
-    }
+    tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+    if (w.active) bad = tile.pack(w.lane, rs);
     wave_sync();
     PresRegs<NW> p;
-    stage_in<VEC>(a.state + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, lane);
+    tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
     int cnt = 0;
-    if (active) {
-        bad |= flags[lane] != 0;
-        pack_relator<NW, LC>(row, geo.L, p.w0, p.n0, bad);
-        pack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1, bad);
+    if (w.active) {
+        bad |= tile.pack(w.lane, p);
         cnt = a.step_count[env];
         if (bad) first_err = ACX_ERR_DOMAIN;
     }
-    const int32_t max_reward = a.horizon * geo.L * 2;
+    const int32_t max_reward = a.horizon * L * 2;
+    // Drain the prologue's loads here: otherwise the waitcnt pass carries the pending
+    // step_count load around the loop back-edge and waits vmcnt(0) (= for every store of
+    // the previous step) at each use of `cnt`.
+    __builtin_amdgcn_s_waitcnt(0);
+    // move ids of ACT_BLOCK consecutive steps packed 4 bits each into one register: one
+    // vector-memory wait per ACT_BLOCK steps instead of one per step (a wait for a load
+    // also waits for every store issued before it, i.e. the previous step's trajectory)
+    uint32_t acts = 0;
     for (int t = 0; t < a.T; ++t) {
         const int64_t ti = (int64_t)t * a.B;
-        if (active) {
-            const int act = a.actions[ti + env];
-            int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, geo.L, a.cyclical != 0);
+        if ((t & (ACT_BLOCK - 1)) == 0 && w.active) {
+            int32_t v[ACT_BLOCK];
+#pragma unroll
+            for (int k = 0; k < ACT_BLOCK; ++k)
+                v[k] = (t + k < a.T) ? a.actions[(int64_t)(t + k) * a.B + env] : 0;
+            acts = 0;
+#pragma unroll
+            for (int k = 0; k < ACT_BLOCK; ++k) {
+                // ids outside [0,12) -> 15 (ACX_ERR_ACTION in ac_move)
+                const uint32_t id = (uint32_t)v[k] < 12u ? (uint32_t)v[k] : 15u;
+                acts |= id << (4 * k);
+            }
+        }
+        if (w.active) {
+            const int act = (int)((acts >> (4 * (t & (ACT_BLOCK - 1)))) & 15u);
+            const int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, a.cyclical != 0);
             if (first_err == ACX_ERR_NONE) first_err = e;
             const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
             ++cnt;
@@ -642,31 +889,23 @@ __global__ __launch_bounds__(BLOCK) void rollout_kernel(RolloutArgs a) {
                 p = rs;
                 cnt = 0;
             }
-            if (a.obs_traj && !bad) {
-                unpack_relator<NW, LC>(row, geo.L, p.w0, p.n0);
-                unpack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1);
-            }
+            if (a.obs_traj && !bad) tile.unpack(w.lane, p);
         }
         if (a.obs_traj) {
             wave_sync();
-            stage_out<VEC>(a.obs_traj + (ti + r0) * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags,
-                           nullptr, 0, lane);
+            tile.template store<false>(a.obs_traj + (ti + w.r0) * twoL, twoL, w.R, nullptr, 0, w.lane);
             wave_sync();
         }
     }
-    if (active) {
-        if (!bad) {
-            unpack_relator<NW, LC>(row, geo.L, p.w0, p.n0);
-            unpack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1);
-        }
+    if (w.active) {
+        if (!bad) tile.unpack(w.lane, p);
         a.step_count[env] = cnt;
         if (a.err) a.err[env] = (uint8_t)first_err;
         if (first_err != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
     wave_sync();
     // rows flagged out-of-domain keep their (untouched) global contents
-    stage_out<VEC>(a.state + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags,
-                   a.state + r0 * geo.twoL, geo.twoL, lane);
+    tile.template store<true>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL, w.lane);
 }
 
 // packed key: r0 letters, r1 letters, n0 (8 bits), n1 (8 bits); KW64 uint64 words
@@ -717,33 +956,24 @@ struct ExpandArgs {
 };
 
 template <int NW, int LC, int VEC>
-__global__ __launch_bounds__(BLOCK) void expand12_kernel(ExpandArgs a) {
+__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12_kernel(ExpandArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Geo<NW, LC> geo(a.L);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x / WAVE;
-    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * WAVE;
-    if (r0 >= a.N) return;
-    const int R = (int)((a.N - r0) < WAVE ? (a.N - r0) : WAVE);
-    char* tile = smem + wid * (WAVE * geo.rowb + WAVE);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(tile + WAVE * geo.rowb);
-    const int64_t par = r0 + lane;
-    const bool active = lane < R;
-    int8_t* row = reinterpret_cast<int8_t*>(tile + lane * geo.rowb);
+    WaveCtx w;
+    if (!wave_ctx(a.N, w)) return;
+    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    const int64_t par = w.r0 + w.lane;
 
-    stage_in<VEC>(a.parents + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, lane);
+    tile.load(a.parents + w.r0 * twoL, w.R, w.lane);
     PresRegs<NW> p;
     bool bad = false;
-    if (active) {
-        bad = flags[lane] != 0;
-        pack_relator<NW, LC>(row, geo.L, p.w0, p.n0, bad);
-        pack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1, bad);
-    }
+    if (w.active) bad = tile.pack(w.lane, p);
     int nerr = 0;
     for (int act = 0; act < 12; ++act) {
-        if (active) {
+        if (w.active) {
             PresRegs<NW> q = p;
-            const int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, geo.L, a.cyclical != 0);
+            const int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, a.cyclical != 0);
             const int64_t ci = par * 12 + act;
             nerr += e != ACX_ERR_NONE;
             if (a.err) a.err[ci] = (uint8_t)e;
@@ -751,16 +981,13 @@ __global__ __launch_bounds__(BLOCK) void expand12_kernel(ExpandArgs a) {
                 a.child_len[2 * ci] = q.n0;
                 a.child_len[2 * ci + 1] = q.n1;
             }
-            if (a.child_key) store_key<NW>(a.child_key + ci * a.kw64, a.kw64, geo.L, q);
-            if (a.children && !bad) {
-                unpack_relator<NW, LC>(row, geo.L, q.w0, q.n0);
-                unpack_relator<NW, LC>(row + geo.L, geo.L, q.w1, q.n1);
-            }
+            if (a.child_key) store_key<NW>(a.child_key + ci * a.kw64, a.kw64, L, q);
+            if (a.children && !bad) tile.unpack(w.lane, q);
         }
         if (a.children) {
             wave_sync();
-            stage_out<VEC>(a.children + (r0 * 12 + act) * geo.twoL, (int64_t)12 * geo.twoL, R, geo.twoL, geo.rowb,
-                           tile, flags, a.parents + r0 * geo.twoL, geo.twoL, lane);
+            tile.template store<true>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
+                                      a.parents + w.r0 * twoL, twoL, w.lane);
             wave_sync();
         }
     }
@@ -780,29 +1007,22 @@ struct CanonArgs {
 // simplify_presentation (utils.py:246-283): assert valid, then reduce both relators
 template <int NW, int LC, int VEC>
 __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Geo<NW, LC> geo(a.L);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x / WAVE;
-    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * WAVE;
-    if (r0 >= a.B) return;
-    const int R = (int)((a.B - r0) < WAVE ? (a.B - r0) : WAVE);
-    char* tile = smem + wid * (WAVE * geo.rowb + WAVE);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(tile + WAVE * geo.rowb);
-    const int64_t env = r0 + lane;
-    int8_t* row = reinterpret_cast<int8_t*>(tile + lane * geo.rowb);
-    stage_in<VEC>(a.state_in + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, lane);
-    if (lane < R) {
+    WaveCtx w;
+    if (!wave_ctx(a.B, w)) return;
+    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    const int64_t env = w.r0 + w.lane;
+    tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
+    if (w.active) {
         PresRegs<NW> p;
-        bool bad = flags[lane] != 0;
-        pack_relator<NW, LC>(row, geo.L, p.w0, p.n0, bad);
-        pack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1, bad);
-        int e = bad ? ACX_ERR_DOMAIN : ((p.n0 == 0 || p.n1 == 0) ? ACX_ERR_INVALID : ACX_ERR_NONE);
+        const bool bad = tile.pack(w.lane, p);
+        const int e = bad ? ACX_ERR_DOMAIN : ((p.n0 == 0 || p.n1 == 0) ? ACX_ERR_INVALID : ACX_ERR_NONE);
         if (e == ACX_ERR_NONE) {
             simplify<NW>(p.w0, p.n0, a.cyclical != 0);
             simplify<NW>(p.w1, p.n1, a.cyclical != 0);
-            unpack_relator<NW, LC>(row, geo.L, p.w0, p.n0);
-            unpack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1);
+            tile.unpack(w.lane, p);
         }
         if (a.lengths_out) {
             a.lengths_out[2 * env] = p.n0;
@@ -812,8 +1032,7 @@ __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
     wave_sync();
-    stage_out<VEC>(a.state_out + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags,
-                   a.state_in + r0 * geo.twoL, geo.twoL, lane);
+    tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
 }
 
 struct UnpackArgs {
@@ -826,30 +1045,24 @@ struct UnpackArgs {
 
 template <int NW, int LC, int VEC>
 __global__ __launch_bounds__(BLOCK) void unpack_keys_kernel(UnpackArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Geo<NW, LC> geo(a.L);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wid = threadIdx.x / WAVE;
-    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * WAVE;
-    if (r0 >= a.M) return;
-    const int R = (int)((a.M - r0) < WAVE ? (a.M - r0) : WAVE);
-    char* tile = smem + wid * (WAVE * geo.rowb + WAVE);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(tile + WAVE * geo.rowb);
-    const int64_t k = r0 + lane;
-    flags[lane] = 0;
-    if (lane < R) {
+    WaveCtx w;
+    if (!wave_ctx(a.M, w)) return;
+    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    const int64_t k = w.r0 + w.lane;
+    if (w.active) {
         PresRegs<NW> p;
-        load_key<NW>(a.keys + k * a.kw64, a.kw64, geo.L, p);
-        int8_t* row = reinterpret_cast<int8_t*>(tile + lane * geo.rowb);
-        unpack_relator<NW, LC>(row, geo.L, p.w0, p.n0);
-        unpack_relator<NW, LC>(row + geo.L, geo.L, p.w1, p.n1);
+        load_key<NW>(a.keys + k * a.kw64, a.kw64, L, p);
+        tile.unpack(w.lane, p);
         if (a.lengths_out) {
             a.lengths_out[2 * k] = p.n0;
             a.lengths_out[2 * k + 1] = p.n1;
         }
     }
     wave_sync();
-    stage_out<VEC>(a.states + r0 * geo.twoL, geo.twoL, R, geo.twoL, geo.rowb, tile, flags, nullptr, 0, lane);
+    tile.template store<false>(a.states + w.r0 * twoL, twoL, w.R, nullptr, 0, w.lane);
 }
 
 // ---------------------------------------------------------------------------------
@@ -859,13 +1072,9 @@ static inline int nw_for(int L) {
     return L <= 16 ? 1 : L <= 32 ? 2 : L <= 48 ? 3 : L <= 64 ? 4 : 8;
 }
 
-template <int NW, int LC>
+template <int NW, int LC, int VEC>
 static inline size_t smem_bytes(int L) {
-    const int lmax = LC > 0 ? LC : 16 * NW;
-    const int bytes = (LC > 0) ? 2 * LC : (L + lmax);
-    int dw = (bytes + 3) >> 2;
-    dw |= 1;
-    return (size_t)WPB * ((size_t)WAVE * dw * 4 + WAVE);
+    return (size_t)WPB * TileFor<NW, LC, VEC>::wave_bytes(L);
 }
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -875,6 +1084,10 @@ template <class F>
 static int dispatch(int L, F&& f) {
     const bool v4 = (2 * L) % 4 == 0;
     if (L == 36) return f.template go<3, 36, 4>();
+#ifdef ACX_ISA_L36_ONLY  // faster builds for ISA inspection only
+    (void)v4;
+    return ACX_E_ARG;
+#else
     if (L == 128) return f.template go<8, 128, 4>();
     switch (nw_for(L)) {
         case 1: return v4 ? f.template go<1, 0, 4>() : f.template go<1, 0, 2>();
@@ -883,6 +1096,7 @@ static int dispatch(int L, F&& f) {
         case 4: return v4 ? f.template go<4, 0, 4>() : f.template go<4, 0, 2>();
         default: return v4 ? f.template go<8, 0, 4>() : f.template go<8, 0, 2>();
     }
+#endif
 }
 
 static inline int finish_launch() {
@@ -898,7 +1112,7 @@ struct StepLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC>(a.L);
+        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         step_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
@@ -908,7 +1122,7 @@ struct RolloutLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC>(a.L);
+        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         rollout_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
@@ -918,7 +1132,7 @@ struct ExpandLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC>(a.L);
+        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         expand12_kernel<NW, LC, VEC><<<dim3(grid_for(a.N)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
@@ -928,7 +1142,7 @@ struct CanonLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC>(a.L);
+        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         canon_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
@@ -938,7 +1152,7 @@ struct UnpackLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC>(a.L);
+        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         unpack_keys_kernel<NW, LC, VEC><<<dim3(grid_for(a.M)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }

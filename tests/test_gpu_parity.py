@@ -105,7 +105,10 @@ def test_bad_action_and_domain_errors():
     s2 = np.array([[1, 3, 0, 0, -1, 0, 0, 0], [1, 0, 0, 0, -1, 0, 0, 0],
                    [1, 2, 0, 0, 700, 0, 0, 0], [1, 0, 2, 0, -1, 0, 0, 0]], np.int32)
     out, lens, err = _gpu_move(s2, [0, 0, 0, 0], L, 1)
-    assert err.tolist() == [3, 0, 3, 3]
+    # row 1: r1 <- r1 r0 = x^-1 x empties r1 -> reference AssertionError (err 1)
+    assert err.tolist() == [3, 1, 3, 3]
+    exp, _, eerr = O.move_batch(s2[1:2], [0], L, 1)
+    assert eerr[0] == 1
     assert np.array_equal(out[[0, 2, 3]], s2[[0, 2, 3]])
 
 
@@ -126,7 +129,9 @@ def test_expand12_goldens_and_keys():
         c = res["children"].reshape(-1, 2 * L).cpu().numpy()
         _, ik = np.unique(k, axis=0, return_inverse=True)
         _, ic = np.unique(c, axis=0, return_inverse=True)
-        assert np.array_equal(ik.reshape(-1), ic.reshape(-1))
+        ik, ic = ik.reshape(-1), ic.reshape(-1)
+        pairs = np.unique(np.stack([ik, ic], 1), axis=0)
+        assert len(pairs) == len(np.unique(ik)) == len(np.unique(ic))
 
 
 @pytest.mark.parametrize("L", [7, 36, 128])
