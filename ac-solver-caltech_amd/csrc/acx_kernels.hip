@@ -308,6 +308,89 @@ __device__ __forceinline__ int ac_move(Word<NW>& w0, int& n0, Word<NW>& w1, int&
     return ACX_ERR_NONE;
 }
 
+// A presentation is "clean" when both relators are non-empty and reduced: freely, and
+// cyclically too when `cyc`.  Every successful ac_move output is clean, and a move on a
+// clean input keeps the reduced words reduced (junction/end cancellation only, SURVEY
+// A.5), so a stream of moves only needs the general reduction when a state enters it.
+template <int NW>
+__device__ __forceinline__ bool relator_clean(const Word<NW>& w, int n, bool cyc) {
+    if (n <= 0) return false;
+    if (wnonzero<NW>(adjacent_pairs<NW>(w, n))) return false;
+    if (cyc && n > 1 && (w.w[0] & 3u) == (wletter<NW>(w, n - 1) ^ 1u)) return false;
+    return true;
+}
+
+template <int NW>
+__device__ __forceinline__ bool is_clean(const Word<NW>& w0, int n0, const Word<NW>& w1, int n1, bool cyc) {
+    return relator_clean<NW>(w0, n0, cyc) && relator_clean<NW>(w1, n1, cyc);
+}
+
+// ac_move for a clean input (same results as ac_move, far less work):
+//   concatenation: junction cancellation + splice; when cyclical, peel the new word
+//     (the untouched relator is already reduced);
+//   conjugation, cyclical: g r g^-1 reduces back to r unless one end cancels, in which
+//     case the result is r rotated by one letter (both ends cannot cancel in a
+//     cyclically reduced r); the length gate never binds (the length is unchanged);
+//   conjugation, not cyclical: splice as in ac_move (the result is freely reduced).
+// The only possible error is a concatenation that empties r_i (r_i = r_j^{-sign}).
+template <int NW>
+__device__ __forceinline__ int ac_move_clean(Word<NW>& w0, int& n0, Word<NW>& w1, int& n1, int action, int L,
+                                             bool cyc) {
+    if ((unsigned)action >= 12u) return ACX_ERR_ACTION;
+    const bool i1 = ((action + 1) & 1) != 0;
+    Word<NW> A = wsel<NW>(i1, w1, w0);
+    int nA = i1 ? n1 : n0;
+    if (action < 4) {
+        const Word<NW> J = wsel<NW>(i1, w0, w1);
+        const int nJ = i1 ? n0 : n1;
+        const bool inv = (action == 1) || (action == 2);
+        Word<NW> Bw = J;
+        if (inv) {
+            Bw = wrev<NW>(J, nJ);
+            const Word<NW> m = wmask<NW>(2 * nJ);
+#pragma unroll
+            for (int k = 0; k < NW; ++k) Bw.w[k] ^= (m.w[k] & P55);
+        }
+        const int mn = nA < nJ ? nA : nJ;
+        int acc = wfirst<NW>(wxinv<NW>(wrev<NW>(A, nA), Bw));
+        acc = acc < mn ? acc : mn;
+        const int nn = nA + nJ - 2 * acc;
+        if (nn > L) return ACX_ERR_NONE;       // gated: no-op
+        if (nn == 0) return ACX_ERR_INVALID;   // r_i emptied (utils.py:264-266)
+        A = wor<NW>(wand<NW>(A, wmask<NW>(2 * (nA - acc))), wshl<NW>(wshr<NW>(Bw, 2 * acc), 2 * (nA - acc)));
+        nA = nn;
+        if (cyc) cyclic_reduce<NW>(A, nA);
+    } else {
+        const uint32_t g = (CONJ_G >> (2 * (action - 4))) & 3u;
+        const uint32_t first = A.w[0] & 3u;
+        const uint32_t last = wletter<NW>(A, nA - 1);
+        const bool sc = first == (g ^ 1u);
+        const bool ec = last == g;
+        if (cyc) {
+            if (sc == ec) return ACX_ERR_NONE;  // no cancellation: reduces back to r_i
+            if (sc) {                             // r = g^-1 v  ->  v g^-1 : rotate left
+                A = wor<NW>(wshr<NW>(A, 2), wsingle<NW>(first, nA - 1));
+            } else {                              // r = v g  ->  g v : rotate right
+                Word<NW> t = wand<NW>(wshl<NW>(A, 2), wmask<NW>(2 * nA));
+                t.w[0] |= last;
+                A = t;
+            }
+        } else {
+            const int nn = nA + 2 - 2 * ((int)sc + (int)ec);
+            if (nn > L) return ACX_ERR_NONE;
+            const Word<NW> mid = wand<NW>(wshr<NW>(A, 2 * (int)sc), wmask<NW>(2 * (nA - (int)sc - (int)ec)));
+            Word<NW> nw = wshl<NW>(mid, 2 * (1 - (int)sc));
+            if (!sc) nw.w[0] |= g;
+            if (!ec) nw = wor<NW>(nw, wsingle<NW>(g ^ 1u, nn - 1));
+            A = nw;
+            nA = nn;
+        }
+    }
+    if (i1) { w1 = A; n1 = nA; }
+    else    { w0 = A; n0 = nA; }
+    return ACX_ERR_NONE;
+}
+
 // strict triviality (ac_env.py:99, utils.py:57-87): both relators one letter, one x and one y
 template <int NW>
 __device__ __forceinline__ bool is_trivial(const Word<NW>& w0, int n0, const Word<NW>& w1, int n1) {
@@ -773,7 +856,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         const int act = a.action[env];
         int cnt = a.step_count ? a.step_count[env] + 1 : 0;
         const bool bad = tile.pack(w.lane, p);
-        int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, a.cyclical != 0);
+        const bool cyc = a.cyclical != 0;
+        int e;
+        if (bad) e = ACX_ERR_DOMAIN;
+        else if (is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+        else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         if (e == ACX_ERR_NONE) tile.unpack(w.lane, p);
         const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
         const bool trunc = a.step_count ? (cnt >= a.horizon) : false;
@@ -846,10 +933,14 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
     int cnt = 0;
+    const bool cyc = a.cyclical != 0;
+    bool clean = false, rs_clean = false;
     if (w.active) {
         bad |= tile.pack(w.lane, p);
         cnt = a.step_count[env];
         if (bad) first_err = ACX_ERR_DOMAIN;
+        clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+        rs_clean = is_clean<NW>(rs.w0, rs.n0, rs.w1, rs.n1, cyc);
     }
     const int32_t max_reward = a.horizon * L * 2;
     // Drain the prologue's loads here: otherwise the waitcnt pass carries the pending
@@ -877,7 +968,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         }
         if (w.active) {
             const int act = (int)((acts >> (4 * (t & (ACT_BLOCK - 1)))) & 15u);
-            const int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, a.cyclical != 0);
+            int e;
+            if (bad) e = ACX_ERR_DOMAIN;
+            else if (clean) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+            else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+            clean = clean || e == ACX_ERR_NONE;  // a successful general move leaves it clean
             if (first_err == ACX_ERR_NONE) first_err = e;
             const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
             ++cnt;
@@ -887,6 +982,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             if (a.trunc_traj) a.trunc_traj[ti + env] = trunc;
             if ((triv || trunc) && !bad) {
                 p = rs;
+                clean = rs_clean;
                 cnt = 0;
             }
             if (a.obs_traj && !bad) tile.unpack(w.lane, p);
@@ -967,13 +1063,20 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
 
     tile.load(a.parents + w.r0 * twoL, w.R, w.lane);
     PresRegs<NW> p;
-    bool bad = false;
-    if (w.active) bad = tile.pack(w.lane, p);
+    bool bad = false, clean = false;
+    const bool cyc = a.cyclical != 0;
+    if (w.active) {
+        bad = tile.pack(w.lane, p);
+        clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+    }
     int nerr = 0;
     for (int act = 0; act < 12; ++act) {
         if (w.active) {
             PresRegs<NW> q = p;
-            const int e = bad ? ACX_ERR_DOMAIN : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, a.cyclical != 0);
+            int e;
+            if (bad) e = ACX_ERR_DOMAIN;
+            else if (clean) e = ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            else e = ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
             const int64_t ci = par * 12 + act;
             nerr += e != ACX_ERR_NONE;
             if (a.err) a.err[ci] = (uint8_t)e;
