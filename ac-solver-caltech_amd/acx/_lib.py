@@ -39,6 +39,7 @@ SIGNATURES = {
     "acx_search_feed": ([_P, _P, _I64], ctypes.c_int32),
     "acx_search_status": ([_P, _P, _P, _P], ctypes.c_int32),
     "acx_search_path": ([_P, _P, _P, _I64], ctypes.c_int64),
+    "acx_search_node_keys": ([_P, _P, _I64], ctypes.c_int64),
 }
 
 _lib = None

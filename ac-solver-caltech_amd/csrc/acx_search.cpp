@@ -17,7 +17,6 @@
 #include <cstdint>
 #include <cstring>
 #include <set>
-#include <unordered_map>
 #include <vector>
 
 #include "acx.h"
@@ -25,6 +24,7 @@
 namespace {
 
 constexpr int ACT = 12;
+constexpr size_t PREFETCH = 6;  // parents of lookahead for hash-slot prefetches (BFS)
 
 inline uint64_t mix64(uint64_t x) {
     x ^= x >> 30;
@@ -46,8 +46,9 @@ struct Engine {
     std::vector<int16_t> total;
     std::vector<int32_t> depth;
     std::vector<int8_t> lex;  // greedy only: node * 2L letters + 2 (tuple order)
-    // open-addressing hash set of node ids (-1 empty)
-    std::vector<int64_t> table;
+    // open-addressing hash set; entry = (node id + 1) << 24 | 24-bit hash tag, 0 = empty.
+    // The tag filters almost every non-matching probe without touching the node's key.
+    std::vector<uint64_t> table;
     uint64_t mask = 0;
     int64_t n_set = 0;
     // BFS queue
@@ -66,10 +67,11 @@ struct Engine {
         }
     };
     std::set<int64_t, Cmp>* frontier = nullptr;
-    std::unordered_map<int64_t, size_t> pending;  // requested, children not yet fed
-    // children cache: node -> offset into cache_keys (ACT * kw words)
-    std::unordered_map<int64_t, size_t> cache;
+    // children cache: node -> offset into cache_keys (ACT * kw words), -1 = not cached
+    std::vector<int64_t> cache_pos;
+    bool cached(int64_t id) const { return cache_pos[id] >= 0; }
     std::vector<uint64_t> cache_keys;
+    std::vector<uint64_t> cache_hash;  // ACT hashes per slot (computed once, reused for prefetch)
     std::vector<size_t> free_slots;
     // last request (order of nodes handed to next_batch)
     std::vector<int64_t> batch;
@@ -83,7 +85,7 @@ struct Engine {
     int budget_hit = 0;
 
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
-        table.assign(1 << 12, -1);
+        table.assign(1 << 12, 0);
         mask = table.size() - 1;
         if (mode == 1) frontier = new std::set<int64_t, Cmp>(Cmp{this});
     }
@@ -94,27 +96,39 @@ struct Engine {
         for (int i = 0; i < kw; ++i) h = mix64(h ^ k[i]) + (uint64_t)i;
         return h;
     }
+    static uint64_t entry(int64_t id, uint64_t h) { return ((uint64_t)(id + 1) << 24) | (h >> 40); }
     void grow() {
-        std::vector<int64_t> old;
+        std::vector<uint64_t> old;
         old.swap(table);
-        table.assign(old.size() * 2, -1);
+        table.assign(old.size() * 2, 0);
         mask = table.size() - 1;
-        for (int64_t id : old)
-            if (id >= 0) {
-                uint64_t p = hash_key(&keys[(size_t)id * kw]) & mask;
-                while (table[p] >= 0) p = (p + 1) & mask;
-                table[p] = id;
+        for (uint64_t e : old)
+            if (e) {
+                const int64_t id = (int64_t)(e >> 24) - 1;
+                const uint64_t h = hash_key(&keys[(size_t)id * kw]);
+                uint64_t p = h & mask;
+                while (table[p]) p = (p + 1) & mask;
+                table[p] = entry(id, h);
             }
     }
-    // find key; returns node id or -1; *slot gets the insert position
-    int64_t find(const uint64_t* k, uint64_t* slot) const {
-        uint64_t p = hash_key(k) & mask;
+    // find key with hash h; returns node id or -1; *slot gets the insert position
+    int64_t find(const uint64_t* k, uint64_t h, uint64_t* slot) const {
+        const uint64_t tag = h >> 40;
+        uint64_t p = h & mask;
         while (true) {
-            const int64_t id = table[p];
-            if (id < 0) { *slot = p; return -1; }
-            if (std::memcmp(&keys[(size_t)id * kw], k, sizeof(uint64_t) * kw) == 0) return id;
+            const uint64_t e = table[p];
+            if (!e) { *slot = p; return -1; }
+            if ((e & 0xffffffull) == tag) {
+                const int64_t id = (int64_t)(e >> 24) - 1;
+                if (std::memcmp(&keys[(size_t)id * kw], k, sizeof(uint64_t) * kw) == 0) return id;
+            }
             p = (p + 1) & mask;
         }
+    }
+    void prefetch_children(int64_t id) const {
+        if (!cached(id)) return;
+        const uint64_t* hs = &cache_hash[(size_t)cache_pos[id] / kw];
+        for (int a = 0; a < ACT; ++a) __builtin_prefetch(&table[hs[a] & mask], 0, 1);
     }
     static int key_len(const uint64_t* k, int L) {
         const int bit = 4 * L;
@@ -141,18 +155,19 @@ struct Engine {
                 out[h * L + i] = (int8_t)((i < n[h] ? dec[code] : 0) + 2);
             }
     }
-    int64_t add_node(const uint64_t* k, uint64_t slot, int64_t par, int act, int tot, int dep) {
+    int64_t add_node(const uint64_t* k, uint64_t h, uint64_t slot, int64_t par, int act, int tot, int dep) {
         const int64_t id = (int64_t)parent.size();
         keys.insert(keys.end(), k, k + kw);
         parent.push_back(par);
         action.push_back((int8_t)act);
         total.push_back((int16_t)tot);
         depth.push_back(dep);
+        cache_pos.push_back(-1);
         if (mode == 1) {
             lex.resize(lex.size() + 2 * L);
             decode_lex(k, &lex[(size_t)id * 2 * L]);
         }
-        table[slot] = id;
+        table[slot] = entry(id, h);
         ++n_set;
         if ((uint64_t)n_set * 2 > table.size()) grow();
         return id;
@@ -160,10 +175,11 @@ struct Engine {
 
     void start(const uint64_t* k) {
         uint64_t slot;
-        find(k, &slot);
+        const uint64_t h = hash_key(k);
+        find(k, h, &slot);
         const int tot = key_len(k, L);
         min_length = tot;
-        const int64_t id = add_node(k, slot, -1, -1, tot, 0);
+        const int64_t id = add_node(k, h, slot, -1, -1, tot, 0);
         if (mode == 0) queue.push_back(id);
         else frontier->insert(id);
     }
@@ -178,7 +194,7 @@ struct Engine {
             }
         } else {
             for (auto it = frontier->begin(); it != frontier->end() && (int64_t)batch.size() < cap; ++it) {
-                if (cache.count(*it)) continue;
+                if (cached(*it)) continue;
                 batch.push_back(*it);
             }
         }
@@ -195,15 +211,18 @@ struct Engine {
         } else {
             off = cache_keys.size();
             cache_keys.resize(off + (size_t)ACT * kw);
+            cache_hash.resize(cache_hash.size() + ACT);
         }
         std::memcpy(&cache_keys[off], ck, sizeof(uint64_t) * ACT * kw);
-        cache[id] = off;
+        for (int a = 0; a < ACT; ++a) cache_hash[off / kw + a] = hash_key(ck + (size_t)a * kw);
+        cache_pos[id] = (int64_t)off;
     }
 
     // expand one popped node from its cached children; returns true when the search ends
     bool visit(int64_t id) {
-        const size_t off = cache[id];
+        const size_t off = (size_t)cache_pos[id];
         const uint64_t* ck = &cache_keys[off];
+        const uint64_t* hs = &cache_hash[off / kw];
         last_popped = id;
         bool ended = false;
         for (int a = 0; a < ACT && !ended; ++a) {
@@ -221,13 +240,13 @@ struct Engine {
                 break;
             }
             uint64_t slot;
-            if (find(k, &slot) < 0) {
-                const int64_t nid = add_node(k, slot, id, a, len, depth[id] + 1);
+            if (find(k, hs[a], &slot) < 0) {
+                const int64_t nid = add_node(k, hs[a], slot, id, a, len, depth[id] + 1);
                 if (mode == 0) queue.push_back(nid);
                 else frontier->insert(nid);
             }
         }
-        cache.erase(id);
+        cache_pos[id] = -1;
         free_slots.push_back(off);
         if (!ended && n_set >= max_nodes) {  // greedy.py:241, breadth_first.py:91
             status = 2;
@@ -246,13 +265,14 @@ struct Engine {
             if (mode == 0) {
                 if (head >= queue.size()) { status = 2; break; }
                 const int64_t id = queue[head];
-                if (!cache.count(id)) return 0;
+                if (!cached(id)) return 0;
+                if (head + PREFETCH < queue.size()) prefetch_children(queue[head + PREFETCH]);
                 ++head;
                 if (visit(id)) break;
             } else {
                 if (frontier->empty()) { status = 2; break; }
                 const int64_t id = *frontier->begin();
-                if (!cache.count(id)) return 0;
+                if (!cached(id)) return 0;
                 frontier->erase(frontier->begin());
                 if (visit(id)) break;
             }
@@ -320,6 +340,14 @@ int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap)
     if (e->status == 1) return e->path(e->found_parent, actions, totals, cap, true);
     if (e->last_popped < 0) return 0;
     return e->path(e->last_popped, actions, totals, cap, true);
+}
+
+// copy the packed keys of the first min(cap, n_nodes) discovered nodes (discovery order)
+int64_t acx_search_node_keys(void* h, uint64_t* out, int64_t cap) {
+    Engine* e = static_cast<Engine*>(h);
+    const int64_t n = e->n_set < cap ? e->n_set : cap;
+    if (out && n > 0) std::memcpy(out, e->keys.data(), sizeof(uint64_t) * (size_t)n * e->kw);
+    return e->n_set;
 }
 
 }  // extern "C"

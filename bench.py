@@ -40,6 +40,11 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
 
 
+def nw_for(L: int) -> int:
+    """32-bit words per packed relator in the kernel instantiation (csrc/acx_kernels.hip)."""
+    return 1 if L <= 16 else 2 if L <= 32 else 3 if L <= 48 else 4 if L <= 64 else 8
+
+
 def ms_starts(L: int, B: int, offset: int = 0) -> np.ndarray:
     ms = np.load(os.path.join(PKG_ROOT, "acx", "data", "all_presentations.npy"))
     idx = (np.arange(B) + offset) % len(ms)
@@ -246,9 +251,9 @@ def main():
         "data": "synthetic: Miller-Schupp starting states (all_presentations.txt, env i -> i mod 1190), "
                 "uniform random move ids (torch.Generator seed 0+rank)",
         "config": {
-            "workload": "PPO rollout collection (BASELINE configs[2]): 2^20 envs/GPU, L=36, horizon 200, "
-                        "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
-                        "one acx_rollout launch of K steps",
+            "workload": (f"PPO rollout collection (BASELINE configs[2]): {B} envs/GPU, L={L}, horizon {H}, "
+                         "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
+                         "one acx_rollout launch of K steps"),
             "global_batch": world * B,
             "envs_per_gpu": B,
             "max_relator_length": L,
@@ -262,7 +267,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "acx::rollout_kernel<3,36,4>",
+            "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
             "kernel_ms": kernel_s * 1e3,

@@ -1,0 +1,75 @@
+"""Summarise a rocprofv3 run of bench.py (profile_cmd.sh output) into profiles/<tag>_summary.json.
+
+Reads <dir>/trace/bench_kernel_stats.csv, <dir>/trace/bench_kernel_trace.csv,
+<dir>/pmc_fetch/bench_counter_collection.csv, <dir>/pmc_write/bench_counter_collection.csv
+and <dir>/trace_bench.log (the bench JSON line printed under the profiler).
+
+HBM traffic per dispatch follows MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in
+KiB; FETCH_SIZE reads exactly half of a wide coalesced streaming read on gfx950, so it is
+doubled before comparing with a byte count; WRITE_SIZE is exact for 16-B-per-lane stores."""
+import csv
+import json
+import os
+import shutil
+import sys
+
+d, tag = sys.argv[1], sys.argv[2]
+out_dir = sys.argv[3] if len(sys.argv) > 3 else "profiles"
+os.makedirs(out_dir, exist_ok=True)
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+trace = rows(os.path.join(d, "trace", "bench_kernel_trace.csv"))
+disp = {}
+for r in trace:
+    name = r["Kernel_Name"]
+    if "acx::" not in name:
+        continue
+    dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    disp.setdefault(name, []).append(dur)
+pmc = {}
+for kind in ("fetch", "write"):
+    p = os.path.join(d, f"pmc_{kind}", "bench_counter_collection.csv")
+    if not os.path.exists(p):
+        continue
+    for r in rows(p):
+        if "acx::" not in r["Kernel_Name"]:
+            continue
+        pmc.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+bench = None
+log = os.path.join(d, "trace_bench.log")
+if os.path.exists(log):
+    for line in open(log):
+        if line.startswith("{"):
+            bench = json.loads(line)
+summary = {"tag": tag, "kernels": {}}
+for name, durs in disp.items():
+    k = {"dispatches": len(durs), "durations_ms": durs, "max_ms": max(durs), "mean_ms": sum(durs) / len(durs)}
+    c = pmc.get(name, {})
+    if "FETCH_SIZE" in c:
+        k["fetch_bytes_corrected"] = [2 * v * 1024 for v in c["FETCH_SIZE"]]
+    if "WRITE_SIZE" in c:
+        k["write_bytes"] = [v * 1024 for v in c["WRITE_SIZE"]]
+    summary["kernels"][name] = k
+if bench:
+    summary["bench_line"] = bench
+    rl = bench["roofline"]
+    timed = [v for n, v in summary["kernels"].items() if "rollout_kernel" in n]
+    if timed:
+        k = timed[0]
+        i = k["durations_ms"].index(k["max_ms"])  # the timed K-step dispatch (warmup is W steps)
+        summary["rollout_timed_dispatch"] = {
+            "rocprof_ms": k["max_ms"], "bench_event_ms": rl["kernel_ms"],
+            "agree_pct": 100 * abs(k["max_ms"] - rl["kernel_ms"]) / rl["kernel_ms"],
+            "algorithmic_bytes": rl["launch_bytes"],
+            "pmc_hbm_bytes": (k.get("fetch_bytes_corrected", [None] * (i + 1))[i] or 0) + (k.get("write_bytes", [None] * (i + 1))[i] or 0)
+            if "write_bytes" in k else None,
+        }
+with open(os.path.join(out_dir, f"{tag}_summary.json"), "w") as f:
+    json.dump(summary, f, indent=1)
+shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
+print(json.dumps(summary.get("rollout_timed_dispatch"), indent=1))
