@@ -1040,6 +1040,18 @@ __device__ __forceinline__ void load_key(const uint64_t* src, int kw64, int L, P
     p.n1 = (int)((kl.w[0] >> 8) & 0xffu);
 }
 
+constexpr int KEY_GROUP = 3;  // actions per staged key group in expand12 (12 % KEY_GROUP == 0)
+
+// expand12's per-wave LDS: the tile, or the staged keys of one group, whichever is larger
+template <int NW, int LC, int VEC>
+struct ExpandLaunchSmem {
+    static __host__ __device__ size_t wave_bytes(int L) {
+        const size_t t = TileFor<NW, LC, VEC>::wave_bytes(L);
+        const size_t k = (size_t)WAVE * KEY_GROUP * (size_t)((4 * L + 16 + 63) / 64) * 8;
+        return ((t > k ? t : k) + 15) & ~(size_t)15;
+    }
+};
+
 struct ExpandArgs {
     const int32_t* parents;
     int32_t* children;
@@ -1057,7 +1069,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
     if (!wave_ctx(a.N, w)) return;
-    Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
+    Tile tile(smem + w.wid * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t par = w.r0 + w.lane;
 
@@ -1070,6 +1082,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
         clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
     }
     int nerr = 0;
+    // keys only (the search path): stage each group of KEY_GROUP actions' keys in LDS
+    // (the parents' rows are no longer needed once packed) and write them out as
+    // contiguous KEY_GROUP*kw64*8-byte segments instead of per-lane 8-byte pieces
+    const bool stage_keys = a.child_key != nullptr && a.children == nullptr;
+    uint64_t* kst = reinterpret_cast<uint64_t*>(smem + w.wid * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L));
     for (int act = 0; act < 12; ++act) {
         if (w.active) {
             PresRegs<NW> q = p;
@@ -1084,13 +1101,28 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
                 a.child_len[2 * ci] = q.n0;
                 a.child_len[2 * ci + 1] = q.n1;
             }
-            if (a.child_key) store_key<NW>(a.child_key + ci * a.kw64, a.kw64, L, q);
+            if (a.child_key) {
+                if (stage_keys) store_key<NW>(kst + (w.lane * KEY_GROUP + act % KEY_GROUP) * a.kw64, a.kw64, L, q);
+                else store_key<NW>(a.child_key + ci * a.kw64, a.kw64, L, q);
+            }
             if (a.children && !bad) tile.unpack(w.lane, q);
         }
         if (a.children) {
             wave_sync();
             tile.template store<true>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
                                       a.parents + w.r0 * twoL, twoL, w.lane);
+            wave_sync();
+        }
+        if (stage_keys && act % KEY_GROUP == KEY_GROUP - 1) {
+            wave_sync();
+            const int kw = LC > 0 ? (4 * LC + 16 + 63) / 64 : a.kw64;
+            const int seg = KEY_GROUP * kw;  // u64 words per parent in this group
+            const int n = w.R * seg;
+            uint64_t* gbase = a.child_key + (w.r0 * 12 + (act - (KEY_GROUP - 1))) * kw;
+            for (int i = w.lane; i < n; i += WAVE) {
+                const int pp = i / seg;
+                gbase[(int64_t)pp * 12 * kw + (i - pp * seg)] = kst[i];
+            }
             wave_sync();
         }
     }
@@ -1235,7 +1267,7 @@ struct ExpandLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+        const size_t shm = (size_t)WPB * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L);
         expand12_kernel<NW, LC, VEC><<<dim3(grid_for(a.N)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }

@@ -235,6 +235,21 @@ def main():
         }
         n_err = int(err_count.item())
 
+    # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
+    # used only when that profile's workload matches this run's
+    traffic, traffic_src = None, None
+    prof = os.path.join(REPO, "profiles", "r01", "r01_summary.json")
+    if os.path.exists(prof):
+        with open(prof) as f:
+            ps = json.load(f)
+        pc = ps.get("bench_line", {}).get("config", {})
+        td = ps.get("rollout_timed_dispatch") or {}
+        if (pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and ps["bench_line"].get("steps") == K
+                and td.get("pmc_hbm_bytes")):
+            traffic = td["pmc_hbm_bytes"]
+            traffic_src = "profiles/r01/r01_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE, same command"
+
     value = world * B * K / elapsed
     line = {
         "metric": "env-steps/sec at batch 2^20, max_relator_len 36; 1/2/4/8 MI355X",
@@ -266,7 +281,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
