@@ -341,3 +341,103 @@ def test_search_kat_miller_schupp():
         assert solved == case["solved"], case["search_fn"]
         assert unsolved == case["unsolved"], case["search_fn"]
         assert paths == case["paths"], case["search_fn"]
+
+
+@pytest.mark.parametrize("L", [36, 128])
+@pytest.mark.parametrize("B", [1, 63, 65, 1000, 64 * 7 + 5])
+def test_partial_tiles_fast_path(L, B):
+    """FastTile (L % 4 == 0) with batches that end in a partial 64-env tile: step, rollout,
+    expand12 and canonicalize against the oracle; out-of-place and in-place."""
+    import acx
+    rng = np.random.default_rng(B * 7 + L)
+    s = np.zeros((B, 2 * L), np.int32)
+    for b in range(B):
+        for h in range(2):
+            n = int(rng.integers(1, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    a = rng.integers(0, 12, size=B).astype(np.int32)
+    exp, elen, eerr = O.move_batch(s, a, L, 1)
+    out, lens, err = _gpu_move(s, a, L, 1)
+    assert np.array_equal(out, exp) and np.array_equal(err, eerr)
+    # in place
+    st = torch.as_tensor(s).to(DEV)
+    acx.ops.step(st, torch.as_tensor(a).to(DEV), state_out=st, cyclical=True)
+    assert np.array_equal(st.cpu().numpy(), exp)
+    # rollout over 12 steps with autoreset (horizon 5) vs the oracle env
+    T, H = 12, 5
+    A = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    # starting states must be valid presentations (ACEnvConfig's rule): replace rows whose
+    # unreduced input reduced to an empty relator
+    empty = (exp[:, :L] != 0).sum(1) == 0
+    empty |= (exp[:, L:] != 0).sum(1) == 0
+    exp[empty] = 0
+    exp[empty, 0] = 1
+    exp[empty, L] = 2
+    env = acx.VecACEnv(exp, horizon_length=H, device=DEV)
+    obs = torch.empty((T, B, 2 * L), dtype=torch.int32, device=DEV)
+    rew = torch.empty((T, B), dtype=torch.int32, device=DEV)
+    env.rollout(torch.as_tensor(A).to(DEV), obs, rew)
+    ost = exp.copy()
+    cnt = np.zeros(B, np.int32)
+    for t in range(T):
+        r, d, tr, e, _, _ = O.env_step(ost, A[t], L, H, cnt, reset_state=exp)
+        assert np.array_equal(obs[t].cpu().numpy(), ost), t
+        assert np.array_equal(rew[t].cpu().numpy(), r), t
+    assert np.array_equal(env.state.cpu().numpy(), ost)
+    assert np.array_equal(env.step_count.cpu().numpy(), cnt)
+    # expand12 (keys + children) and canonicalize
+    res = acx.ops.expand12(torch.as_tensor(s).to(DEV), cyclical=False, keys=True)
+    ch, cl, ce = O.expand12(s, L, False)
+    assert np.array_equal(res["children"].cpu().numpy(), ch)
+    back = acx.ops.unpack_keys(res["keys"].reshape(-1, res["keys"].shape[-1]), L)
+    assert np.array_equal(back.cpu().numpy(), ch.reshape(-1, 2 * L))
+    keys_only = acx.ops.expand12(torch.as_tensor(s).to(DEV), cyclical=False, children=False, keys=True)
+    assert torch.equal(keys_only["keys"], res["keys"])
+
+
+def test_api_edge_cases():
+    import acx
+    from acx import _lib
+    L = 36
+    s = torch.zeros((0, 2 * L), dtype=torch.int32, device=DEV)
+    out = acx.ops.step(s, torch.zeros(0, dtype=torch.int32, device=DEV))
+    assert out.shape == (0, 2 * L)
+    lib = _lib.load()
+    base = torch.zeros((8, 2 * L + 1), dtype=torch.int32, device=DEV)
+    bad_ptr = base.data_ptr() + 4  # misaligned
+    rc = lib.acx_step(bad_ptr, bad_ptr, base.data_ptr(), None, None, None, None, None, None, None, None, None,
+                      4, L, 0, 1, torch.cuda.current_stream().cuda_stream)
+    assert rc == _lib.E_ARG
+    rc = lib.acx_step(base.data_ptr(), base.data_ptr(), base.data_ptr(), None, None, None, None, None, None, None,
+                      None, None, 4, 129, 0, 1, torch.cuda.current_stream().cuda_stream)
+    assert rc == _lib.E_ARG
+    with pytest.raises(ValueError):
+        acx.ops.step(torch.zeros((4, 7), dtype=torch.int32, device=DEV), torch.zeros(4, dtype=torch.int32, device=DEV))
+    with pytest.raises(TypeError):
+        acx.ops.step(torch.zeros((4, 8), dtype=torch.int64, device=DEV), torch.zeros(4, dtype=torch.int32, device=DEV))
+
+
+def test_acenv_api_mirrors_reference():
+    """ACEnv: reset(options), step returns, truncation at the horizon, info actions, errors."""
+    from acx import ACEnv, ACEnvConfig
+    env = ACEnv(ACEnvConfig(initial_state=[1, 2, 0, -1, 0, 0], horizon_length=3))
+    s, info = env.reset()
+    assert s.tolist() == [1, 2, 0, -1, 0, 0] and info == {}
+    outs = [env.step(a) for a in (8, 8, 8)]
+    assert [o[3] for o in outs] == [False, False, True]
+    from oracle import oracle as O
+    st = np.array([[1, 2, 0, -1, 0, 0]], np.int32)
+    cnt = np.zeros(1, np.int32)
+    for a, o in zip((8, 8, 8), outs):
+        r, d, tr, e, lens, _ = O.env_step(st, [a], 3, 3, cnt)
+        assert o[0].tolist() == st[0].tolist() and o[1] == int(r[0]) and o[2] == bool(d[0])
+    s, _ = env.reset(options={"starting_state": np.array([1, 0, 0, 2, 0, 0])})
+    assert env.lengths == [1, 1] and env.count_steps == 0
+    with pytest.raises(NotImplementedError):
+        ACEnv(ACEnvConfig(use_supermoves=True))
+    # conjugating an empty relator -> IndexError, emptying a relator -> AssertionError
+    from acx import ACMove
+    with pytest.raises(IndexError):
+        ACMove(7, np.array([0, 0, 1, 0]), 2, None)
+    with pytest.raises(AssertionError):
+        ACMove(0, np.array([1, 0, -1, 0]), 2, None)
