@@ -74,6 +74,18 @@ class ACEnvConfig:
         )
 
 
+def _invalid_rows(states: np.ndarray) -> np.ndarray:
+    """Vectorised is_array_valid_presentation over (B, 2L) rows (utils.py:13-54)."""
+    L = states.shape[1] // 2
+    bad = np.zeros(states.shape[0], bool)
+    idx = np.arange(L)[None, :]
+    for h in range(2):
+        nz = states[:, h * L : (h + 1) * L] != 0
+        n = nz.sum(1)
+        bad |= (n == 0) | (nz & (idx >= n[:, None])).any(1)
+    return bad
+
+
 def _check_domain(state: np.ndarray) -> None:
     if np.any(np.abs(state) > 2):
         raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
@@ -172,9 +184,9 @@ class VecACEnv:
         if init.dim() != 2 or init.shape[1] % 2:
             raise ValueError("initial_states must be (B, 2L)")
         init_np = init.cpu().numpy()
-        for row in init_np[: min(len(init_np), 4096)]:
-            if not is_array_valid_presentation(row):
-                raise ValueError(f"initial state {row} is not a valid presentation")
+        bad = _invalid_rows(init_np)
+        if bad.any():
+            raise ValueError(f"initial state {init_np[np.argmax(bad)]} is not a valid presentation")
         _check_domain(init_np)
         self.num_envs = init.shape[0]
         self.max_relator_length = init.shape[1] // 2

@@ -642,6 +642,162 @@ struct FastTile {
     }
 };
 
+// CodeTile: compile-time L % 8 == 0, large L (128).  LDS holds, per 4-letter chunk, one
+// 16-bit slot = 8-bit code field | 4-bit non-zero mask << 8 (half the bytes of an int8
+// image: 8.5 KB per wave at L = 128, so LDS no longer caps occupancy); the SWAR
+// conversion happens in the cooperative load/store, and a lane's pack/unpack is plain
+// field assembly.  Row stride S dwords, S = 2 mod 4 (conflict-free 8-byte lane accesses).
+template <int NW, int LC>
+struct CodeTile {
+    static_assert(LC > 0 && LC % 8 == 0, "CodeTile needs a compile-time L multiple of 8");
+    static constexpr int L = LC;
+    static constexpr int twoL = 2 * LC;
+    static constexpr int CPR = LC / 2;   // 4-letter chunks per row (16-bit slots)
+    static constexpr int RDW = CPR / 2;  // dwords per row
+    static constexpr int S = (RDW % 4 == 2) ? RDW : RDW + ((6 - RDW % 4) % 4);
+    static constexpr int HALF = CPR / 2;  // chunks per relator
+    static_assert(S % 4 == 2 && RDW % 2 == 0, "row layout");
+    static constexpr int LOAD_BATCH = 8;
+
+    uint32_t* lds;
+    uint8_t* flags;
+    bool tile_bad = false;
+
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    __device__ __forceinline__ CodeTile(char* base, int) {
+        lds = reinterpret_cast<uint32_t*>(base);
+        flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
+    }
+    __device__ __forceinline__ int Lr() const { return L; }
+    __device__ __forceinline__ uint16_t* slots(int r) const { return reinterpret_cast<uint16_t*>(lds + r * S); }
+
+    __device__ __forceinline__ void put(int c, uint32_t slot) const {
+        const int r = c / CPR;
+        slots(r)[c - r * CPR] = (uint16_t)slot;
+    }
+    __device__ __forceinline__ uint32_t get(int c) const {
+        const int r = c / CPR;
+        return slots(r)[c - r * CPR];
+    }
+
+    __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        flags[ln] = 0;
+        wave_sync();
+        const int nc = R * CPR;
+        const int4* src = reinterpret_cast<const int4*>(g) + ln;
+        bool any_bad = false;
+        for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
+            int4 v[LOAD_BATCH];
+#pragma unroll
+            for (int u = 0; u < LOAD_BATCH; ++u)
+                if (ln + (u0 + u) * WAVE < nc) v[u] = src[(u0 + u) * WAVE];
+#pragma unroll
+            for (int u = 0; u < LOAD_BATCH; ++u) {
+                const int c = ln + (u0 + u) * WAVE;
+                if (c < nc) {
+                    bool bad = false;
+                    const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
+                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                    uint32_t c8, nz4;
+                    swar_pack4(d, c8, nz4);
+                    put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+                    if (bad) flags[c / CPR] = 1;
+                    any_bad |= bad;
+                }
+            }
+        }
+        tile_bad = __any(any_bad);
+        wave_sync();
+    }
+
+    template <bool FB>
+    __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
+                                          int64_t fpitch, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (ln + (u0 + u) * WAVE < nc) p[u] = get(ln + (u0 + u) * WAVE);
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                const int c = ln + (u0 + u) * WAVE;
+                if (c >= nc) continue;
+                const int r = c / CPR;
+                const int pos = 4 * (c - r * CPR);
+                int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
+                if (FB && tile_bad && flags[r]) {
+                    *dst = *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos);
+                } else {
+                    const uint32_t nz4 = (p[u] >> 8) & 0xfu;
+                    *dst = widen4(swar_unpack4(p[u] & 0xffu, __builtin_popcount(nz4)));
+                }
+            }
+        }
+    }
+
+    __device__ __forceinline__ bool pack(int lane, PresRegs<NW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t* src = lds + ln * S;
+        bool bad = flags[ln] != 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            Word<NW> w = wzero<NW>();
+            uint64_t mlo = 0, mhi = 0;
+#pragma unroll
+            for (int k = 0; k < HALF; k += 4) {  // 4 slots = one 8-byte LDS read
+                const uint2 x = *reinterpret_cast<const uint2*>(src + (h * HALF + k) / 2);
+                const uint32_t sl[4] = {x.x & 0xffffu, x.x >> 16, x.y & 0xffffu, x.y >> 16};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = k + j;
+                    w.w[kk >> 2] |= (sl[j] & 0xffu) << (8 * (kk & 3));
+                    const uint64_t nz4 = (sl[j] >> 8) & 0xfu;
+                    if (kk < 16) mlo |= nz4 << (4 * kk);
+                    else mhi |= nz4 << (4 * (kk - 16));
+                }
+            }
+            const int n = __builtin_popcountll(mlo) + __builtin_popcountll(mhi);
+            const uint64_t elo = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+            const uint64_t ehi = n <= 64 ? 0ull : (n >= 128 ? ~0ull : ((1ull << (n - 64)) - 1ull));
+            bad |= (mlo != elo) || (mhi != ehi);
+            if (h == 0) { p.w0 = w; p.n0 = n; }
+            else        { p.w1 = w; p.n1 = n; }
+        }
+        return bad;
+    }
+
+    __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const Word<NW>& w = h ? p.w1 : p.w0;
+            const int n = h ? p.n1 : p.n0;
+#pragma unroll
+            for (int k = 0; k < HALF; k += 4) {
+                uint32_t sl[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = k + j;
+                    const int nin = n - 4 * kk;
+                    const uint32_t nz4 = nin >= 4 ? 0xfu : (nin <= 0 ? 0u : ((1u << nin) - 1u));
+                    const uint32_t c8 = (w.w[kk >> 2] >> (8 * (kk & 3))) & 0xffu;
+                    sl[j] = c8 | (nz4 << 8);
+                }
+                *reinterpret_cast<uint2*>(dst + (h * HALF + k) / 2) =
+                    make_uint2(sl[0] | (sl[1] << 16), sl[2] | (sl[3] << 16));
+            }
+        }
+    }
+};
+
 template <int NW, int LC, int VEC>
 struct GenericTile {
     static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
@@ -800,7 +956,43 @@ struct GenericTile {
 };
 
 template <int NW, int LC, int VEC>
-using TileFor = typename std::conditional<(LC > 0 && LC % 4 == 0), FastTile<NW, LC>, GenericTile<NW, LC, VEC>>::type;
+using TileFor = typename std::conditional<
+    (LC >= 64 && LC % 8 == 0), CodeTile<NW, LC>,
+    typename std::conditional<(LC > 0 && LC % 4 == 0), FastTile<NW, LC>, GenericTile<NW, LC, VEC>>::type>::type;
+
+// Per-lane row <-> registers through HBM directly (uncoalesced; used only on the rare
+// same-step-autoreset path of the step kernel).  LMAX = compile-time bound on L.
+template <int NW>
+__device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>& p, int L) {
+    for (int h = 0; h < 2; ++h) {
+        const Word<NW> w = h ? p.w1 : p.w0;
+        const int n = h ? p.n1 : p.n0;
+#pragma unroll 1
+        for (int k = 0; k < L; ++k) {
+            const uint32_t code = wletter<NW>(w, k);
+            const int32_t v = (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu);
+            dst[h * L + k] = k < n ? v : 0;
+        }
+    }
+}
+template <int NW>
+__device__ __forceinline__ void global_to_regs(const int32_t* src, PresRegs<NW>& p, int L) {
+    for (int h = 0; h < 2; ++h) {
+        Word<NW> w = wzero<NW>();
+        int n = 0;
+#pragma unroll 1
+        for (int k = 0; k < L; ++k) {
+            const int32_t b = src[h * L + k];
+            const uint32_t code = ((((uint32_t)~b & 1u) << 1) | (((uint32_t)b >> 31) & 1u));
+            if (b != 0) {
+                w = wor<NW>(w, wsingle<NW>(code, k));
+                ++n;
+            }
+        }
+        if (h == 0) { p.w0 = w; p.n0 = n; }
+        else        { p.w1 = w; p.n1 = n; }
+    }
+}
 
 // common per-wave prologue: tile index, rows in the tile, LDS slice
 struct WaveCtx {
@@ -870,20 +1062,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         int l0 = p.n0, l1 = p.n1;
         if ((triv || trunc) && a.reset_state && e == ACX_ERR_NONE) {
             // same-step autoreset (rare): final_obs <- post-move state, state <- reset row
-            int8_t* row = tile.row(w.lane);
-            if (a.final_obs) {
-                int32_t* fo = a.final_obs + env * twoL;
-                for (int k = 0; k < twoL; ++k) fo[k] = (int32_t)row[k];
-            }
-            const int32_t* rs = a.reset_state + env * twoL;
-            l0 = 0;
-            l1 = 0;
-            for (int k = 0; k < twoL; ++k) {
-                const int32_t v = rs[k];
-                row[k] = (int8_t)v;
-                if (k < L) l0 += v != 0;
-                else l1 += v != 0;
-            }
+            if (a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
+            global_to_regs<NW>(a.reset_state + env * twoL, p, L);
+            tile.unpack(w.lane, p);
+            l0 = p.n0;
+            l1 = p.n1;
             cnt = 0;
         }
         if (a.step_count) a.step_count[env] = cnt;

@@ -177,6 +177,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     roll(actions[W : W + K], K)
+    t_launch = time.perf_counter() - t0
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -287,6 +288,7 @@ def main():
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
             "kernel_ms": kernel_s * 1e3,
+            "host_launch_ms": t_launch * 1e3,
         },
         "cpu_baseline": cpu,
         "cpu_baseline_c_oracle": cpu_c,
