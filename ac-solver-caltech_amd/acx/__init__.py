@@ -9,5 +9,6 @@ from .envs.ac_env import ACEnv, ACEnvConfig, VecACEnv
 from .envs.ac_moves import ACMove
 from .search.breadth_first import bfs
 from .search.greedy import greedy_search
+from . import data  # noqa: F401
 
 __all__ = ["ACEnv", "ACEnvConfig", "VecACEnv", "ACMove", "bfs", "greedy_search"]

@@ -40,6 +40,7 @@ SIGNATURES = {
     "acx_search_status": ([_P, _P, _P, _P], ctypes.c_int32),
     "acx_search_path": ([_P, _P, _P, _I64], ctypes.c_int64),
     "acx_search_node_keys": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_search_stats": ([_P, _P], None),
 }
 
 _lib = None

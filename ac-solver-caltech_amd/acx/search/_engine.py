@@ -13,6 +13,7 @@ from .. import _lib, ops
 from ..envs.utils import is_array_valid_presentation
 
 BFS, GREEDY = 0, 1
+LAST_STATS = {}  # engine statistics of the most recent search (rounds, expanded, pops)
 
 
 def _pack_key(state: np.ndarray, L: int) -> np.ndarray:
@@ -72,6 +73,9 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
                                err=False, out=out)
             pinned_out[:n].copy_(res["keys"][:n], non_blocking=False)
             status = lib.acx_search_feed(h, pinned_out.data_ptr(), n)
+        st = np.zeros(3, np.int64)
+        lib.acx_search_stats(h, st.ctypes.data)
+        LAST_STATS.update(rounds=int(st[0]), expanded=int(st[1]), pops=int(st[2]))
         budget = ctypes.c_int32(0)
         min_len = ctypes.c_int32(0)
         n_nodes = ctypes.c_int64(0)

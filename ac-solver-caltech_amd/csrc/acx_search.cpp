@@ -66,7 +66,8 @@ struct Engine {
             return a < b;
         }
     };
-    std::set<int64_t, Cmp>* frontier = nullptr;
+    std::set<int64_t, Cmp>* frontier = nullptr;    // pop order (all unpopped nodes)
+    std::set<int64_t, Cmp>* unexpanded = nullptr;  // the subset not yet sent to the GPU
     // children cache: node -> offset into cache_keys (ACT * kw words), -1 = not cached
     std::vector<int64_t> cache_pos;
     bool cached(int64_t id) const { return cache_pos[id] >= 0; }
@@ -83,13 +84,21 @@ struct Engine {
     int64_t last_popped = -1;
     int min_length = 0;
     int budget_hit = 0;
+    // statistics: rounds (next_batch calls that returned parents), parents expanded, pops
+    int64_t st_rounds = 0, st_expanded = 0, st_pops = 0;
 
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
         table.assign(1 << 12, 0);
         mask = table.size() - 1;
-        if (mode == 1) frontier = new std::set<int64_t, Cmp>(Cmp{this});
+        if (mode == 1) {
+            frontier = new std::set<int64_t, Cmp>(Cmp{this});
+            unexpanded = new std::set<int64_t, Cmp>(Cmp{this});
+        }
     }
-    ~Engine() { delete frontier; }
+    ~Engine() {
+        delete frontier;
+        delete unexpanded;
+    }
 
     uint64_t hash_key(const uint64_t* k) const {
         uint64_t h = 0x9e3779b97f4a7c15ull;
@@ -181,7 +190,10 @@ struct Engine {
         min_length = tot;
         const int64_t id = add_node(k, h, slot, -1, -1, tot, 0);
         if (mode == 0) queue.push_back(id);
-        else frontier->insert(id);
+        else {
+            frontier->insert(id);
+            unexpanded->insert(id);
+        }
     }
 
     int64_t next_batch(uint64_t* out, int64_t cap) {
@@ -193,13 +205,17 @@ struct Engine {
                 batch.push_back(id);
             }
         } else {
-            for (auto it = frontier->begin(); it != frontier->end() && (int64_t)batch.size() < cap; ++it) {
-                if (cached(*it)) continue;
-                batch.push_back(*it);
+            // the smallest unpopped nodes not expanded yet (speculative: their children are
+            // cached until the node is popped in the reference's order)
+            while ((int64_t)batch.size() < cap && !unexpanded->empty()) {
+                batch.push_back(*unexpanded->begin());
+                unexpanded->erase(unexpanded->begin());
             }
         }
         for (size_t i = 0; i < batch.size(); ++i)
             std::memcpy(out + i * kw, &keys[(size_t)batch[i] * kw], sizeof(uint64_t) * kw);
+        if (!batch.empty()) ++st_rounds;
+        st_expanded += (int64_t)batch.size();
         return (int64_t)batch.size();
     }
 
@@ -224,6 +240,7 @@ struct Engine {
         const uint64_t* ck = &cache_keys[off];
         const uint64_t* hs = &cache_hash[off / kw];
         last_popped = id;
+        ++st_pops;
         bool ended = false;
         for (int a = 0; a < ACT && !ended; ++a) {
             const uint64_t* k = ck + (size_t)a * kw;
@@ -243,7 +260,10 @@ struct Engine {
             if (find(k, hs[a], &slot) < 0) {
                 const int64_t nid = add_node(k, hs[a], slot, id, a, len, depth[id] + 1);
                 if (mode == 0) queue.push_back(nid);
-                else frontier->insert(nid);
+                else {
+                    frontier->insert(nid);
+                    unexpanded->insert(nid);
+                }
             }
         }
         cache_pos[id] = -1;
@@ -340,6 +360,14 @@ int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap)
     if (e->status == 1) return e->path(e->found_parent, actions, totals, cap, true);
     if (e->last_popped < 0) return 0;
     return e->path(e->last_popped, actions, totals, cap, true);
+}
+
+// statistics: out[0] = rounds, out[1] = parents expanded on the GPU, out[2] = parents popped
+void acx_search_stats(void* h, int64_t* out) {
+    Engine* e = static_cast<Engine*>(h);
+    out[0] = e->st_rounds;
+    out[1] = e->st_expanded;
+    out[2] = e->st_pops;
 }
 
 // copy the packed keys of the first min(cap, n_nodes) discovered nodes (discovery order)
