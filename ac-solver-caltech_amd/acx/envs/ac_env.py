@@ -229,13 +229,27 @@ class VecACEnv:
         self.state[i].copy_(t)
         self.step_count[i] = 0
 
+    def _step_args(self):
+        """Pointers of the env's persistent buffers, computed once (the per-call Python
+        overhead of argument checking would otherwise rival a small batch's kernel time)."""
+        if getattr(self, "_args", None) is None:
+            fo = self.final_obs.data_ptr() if self.final_obs is not None else None
+            self._args = (self.state.data_ptr(), self.state.data_ptr(), self.reset_state.data_ptr(),
+                          self.step_count.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
+                          self.truncated.data_ptr(), self.lengths.data_ptr(), fo, self.err.data_ptr(),
+                          self.err_count.data_ptr())
+            self._lib = _lib.load()
+        return self._args
+
     def step(self, actions: torch.Tensor):
-        if actions.dtype != torch.int32 or actions.device != self.device:
-            actions = actions.to(self.device, torch.int32)
-        ops.step(self.state, actions.contiguous(), state_out=self.state, reset_state=self.reset_state,
-                 step_count=self.step_count, horizon=self.horizon_length, cyclical=self.cyclical,
-                 reward=self.reward, done=self.done, truncated=self.truncated, lengths=self.lengths,
-                 final_obs=self.final_obs, err=self.err, err_count=self.err_count)
+        if (actions.dtype != torch.int32 or actions.device != self.device or not actions.is_contiguous()
+                or actions.shape != (self.num_envs,)):
+            actions = actions.to(self.device, torch.int32).contiguous().reshape(self.num_envs)
+        s_in, s_out, rs, cnt, rew, dn, tr, ln, fo, err, ec = self._step_args()
+        st = self._lib.acx_step(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
+                                self.num_envs, self.max_relator_length, self.horizon_length, int(self.cyclical),
+                                torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(st, "acx_step")
         if self.check_errors:
             self.raise_if_errors()
         info = {"final_observation": self.final_obs} if self.final_obs is not None else {}
