@@ -17,6 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ACX_LIB", os.path.join(HERE, "libacx.so"))
 
 OK, E_ARG, E_LAUNCH = 0, -1, -2
+BFS_EXHAUSTED, BFS_FOUND, BFS_BUDGET, BFS_MOVE_ERROR = 0, 1, 2, 3
 ERR_NONE, ERR_INVALID, ERR_EMPTY_CONJ, ERR_DOMAIN, ERR_ACTION = 0, 1, 2, 3, 4
 MAX_L = 128
 
@@ -41,6 +42,11 @@ SIGNATURES = {
     "acx_search_path": ([_P, _P, _P, _I64], ctypes.c_int64),
     "acx_search_node_keys": ([_P, _P, _I64], ctypes.c_int64),
     "acx_search_stats": ([_P, _P], None),
+    # device BFS (ac-solver-caltech_amd/csrc/acx_bfs.hip)
+    "acx_bfs_create": ([_I32, _I64, _I64, _I32], ctypes.c_void_p),
+    "acx_bfs_run": ([_P, _P, _I64, _P, _P, _I64, _P, _P], ctypes.c_int),
+    "acx_bfs_destroy": ([_P], None),
+    "acx_bfs_node_keys": ([_P, _P, _I64], ctypes.c_int64),
 }
 
 _lib = None

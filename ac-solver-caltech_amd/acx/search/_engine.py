@@ -38,7 +38,8 @@ def _pack_key(state: np.ndarray, L: int) -> np.ndarray:
     return words
 
 
-def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, device=None, batch=None):
+def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, device=None, batch=None,
+               keep_node_keys=False):
     p = np.asarray(presentation)
     assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
     L = len(p) // 2
@@ -75,11 +76,19 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
             status = lib.acx_search_feed(h, pinned_out.data_ptr(), n)
         st = np.zeros(3, np.int64)
         lib.acx_search_stats(h, st.ctypes.data)
+        LAST_STATS.clear()
         LAST_STATS.update(rounds=int(st[0]), expanded=int(st[1]), pops=int(st[2]))
         budget = ctypes.c_int32(0)
         min_len = ctypes.c_int32(0)
         n_nodes = ctypes.c_int64(0)
         status = lib.acx_search_status(h, ctypes.byref(budget), ctypes.byref(min_len), ctypes.byref(n_nodes))
+        LAST_STATS.update(nodes=int(n_nodes.value), status=int(status))
+        if keep_node_keys:
+            nk = np.zeros((n_nodes.value, kw), np.uint64)
+            lib.acx_search_node_keys(h, nk.ctypes.data, n_nodes.value)
+            LAST_STATS["node_keys"] = nk
+        if status == 3:
+            raise AssertionError("a move produced an invalid presentation (utils.py:264-266)")
         if verbose:
             print(f"Minimal total length found: {min_len.value}")
         if budget.value:

@@ -1,17 +1,26 @@
 """bfs with the reference's signature and results (ac_solver/search/breadth_first.py:15-97).
 
-FIFO frontier expanded in chunks of parents per GPU launch (acx_expand12); the host engine
-(csrc/acx_search.cpp) scans children in (parent FIFO order, action 0..11) order with the
-reference's success test, dedup and per-parent budget check, so paths are identical."""
+engine="device" (default): the whole search runs on the GPU (csrc/acx_bfs.hip) -- queue,
+  visited hash set in HBM, expansion, dedup, budget -- in chunks of parents.
+engine="host": GPU expansion (acx_expand12) with the host engine (csrc/acx_search.cpp)
+  replaying the FIFO/dedup/budget logic on packed keys (BASELINE config 4's "dedup on host").
+Both scan children in (parent FIFO order, action 0..11) order with the reference's success
+test, dedup and per-parent budget check, so paths are identical."""
 
 from __future__ import annotations
 
+from ._device_bfs import device_bfs
 from ._engine import BFS, run_search
 
 
 def bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False, device=None,
-        batch=None):
+        batch=None, engine="device"):
     """Returns (True, path) or (False, None), as breadth_first.py:15-97."""
+    if engine == "device":
+        return device_bfs(presentation, max_nodes_to_explore, verbose, cyclically_reduce_after_moves, device=device,
+                          chunk=batch or 0)
+    if engine != "host":
+        raise ValueError(f"engine must be 'device' or 'host', not {engine!r}")
     ok, path = run_search(BFS, presentation, max_nodes_to_explore, verbose, cyclically_reduce_after_moves,
                           device=device, batch=batch)
     return (True, path) if ok else (False, None)

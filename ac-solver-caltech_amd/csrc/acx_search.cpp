@@ -77,7 +77,7 @@ struct Engine {
     // last request (order of nodes handed to next_batch)
     std::vector<int64_t> batch;
     // result
-    int status = 0;  // 0 running, 1 success, 2 failed (budget or exhausted)
+    int status = 0;  // 0 running, 1 success, 2 failed (budget or exhausted), 3 move error
     int64_t found_parent = -1;
     int found_action = -1, found_len = -1;
     int last_action = -1, last_len = -1;
@@ -145,6 +145,13 @@ struct Engine {
         const uint64_t hi = (bit & 63) > 48 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
         const uint64_t v = lo | hi;
         return (int)(v & 0xff) + (int)((v >> 8) & 0xff);
+    }
+    // acx_expand12's key for a child whose move failed: both length bytes 0xFF
+    static bool key_is_error(const uint64_t* k, int L) {
+        const int bit = 4 * L;
+        const uint64_t lo = k[bit >> 6] >> (bit & 63);
+        const uint64_t hi = (bit & 63) > 48 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
+        return ((lo | hi) & 0xffffull) == 0xffffull;
     }
     void decode_lex(const uint64_t* k, int8_t* out) const {
         // letters of r0 then r1 (padded), stored as value + 2 (unsigned order == numeric)
@@ -244,6 +251,11 @@ struct Engine {
         bool ended = false;
         for (int a = 0; a < ACT && !ended; ++a) {
             const uint64_t* k = ck + (size_t)a * kw;
+            if (key_is_error(k, L)) {  // ACMove raised (utils.py:264-266) before any test
+                status = 3;
+                ended = true;
+                break;
+            }
             const int len = key_len(k, L);
             last_action = a;
             last_len = len;
@@ -344,7 +356,8 @@ int32_t acx_search_feed(void* h, const uint64_t* child_keys, int64_t count) {
     return static_cast<Engine*>(h)->feed(child_keys, count);
 }
 
-// 0 running, 1 success, 2 failed; *budget_hit = 1 when the node budget ended the search
+// 0 running, 1 success, 2 failed, 3 move error; *budget_hit = 1 when the node budget ended
+// the search
 int32_t acx_search_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {
     Engine* e = static_cast<Engine*>(h);
     if (budget_hit) *budget_hit = e->budget_hit;

@@ -100,6 +100,8 @@ int acx_rollout(int32_t* state, const int32_t* actions, const int32_t* reset_sta
  *   child_len  (N,12,2) int32 or NULL
  *   child_key  (N,12,acx_key_words(L)) uint64 or NULL: packed child state (2 bits per
  *              letter, r0 then r1, then the two lengths) -- equal keys <=> equal states.
+ *              The key of a child whose move failed (err != 0) has both length bytes
+ *              0xFF, which no state has.
  *   err        (N,12) uint8 or NULL
  */
 int acx_expand12(const int32_t* parents, int32_t* children, int32_t* child_len, uint64_t* child_key,
@@ -113,6 +115,56 @@ int acx_canonicalize(const int32_t* state_in, int32_t* state_out, int32_t* lengt
 /* packed keys (M, acx_key_words(L)) -> presentations (M,2L) int32 (+ lengths (M,2), nullable) */
 int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out, int64_t M, int32_t L,
                     void* stream);
+
+/*
+ * Breadth-first search entirely on the GPU (replaces bfs, ac_solver/search/breadth_first.py:15-97,
+ * with identical results): FIFO queue of packed node keys and the visited set (open-addressing
+ * hash table) in HBM; the 12-way expansion, dedup against the visited set and within the chunk
+ * (first occurrence in (parent, action) order wins), the success test and the per-parent node
+ * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^21).
+ *   acx_bfs_create   allocates the device workspace on the current device for searches of
+ *                    up to max_nodes nodes (<= 2^30) at max_relator_length L; NULL on failure.
+ *   acx_bfs_run      searches from `presentation` (HOST pointer, 2L int32, a valid presentation
+ *                    with letters +-1, +-2) with budget max_nodes (<= the create-time value);
+ *                    synchronous on `stream`.  On ACX_BFS_FOUND the reference's path
+ *                    [(-1, initial total), (action, total)...] is written to path_actions /
+ *                    path_totals (first path_cap entries).  stats (int64[5]) = n_nodes
+ *                    (len(tree_nodes) at the end), parents expanded, chunks, min total length
+ *                    seen, path length.  Returns an ACX_BFS_* status or a negative ACX_E_*.
+ */
+#define ACX_BFS_EXHAUSTED 0  /* queue ran empty: (False, None) */
+#define ACX_BFS_FOUND 1      /* (True, path) */
+#define ACX_BFS_BUDGET 2     /* len(tree_nodes) >= max_nodes after a parent: (False, None) */
+#define ACX_BFS_MOVE_ERROR 3 /* an ACMove raised AssertionError (a relator became empty) */
+void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_t cyclical);
+int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t* path_actions,
+                int32_t* path_totals, int64_t path_cap, int64_t* stats, void* stream);
+void acx_bfs_destroy(void* h);
+/* packed keys (acx.h key format) of the first min(cap, n) nodes of the last run in discovery
+   (FIFO) order, n = nodes held (<= max_nodes + 12); returns n */
+int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
+
+/*
+ * Host search engine (csrc/acx_search.cpp) for greedy_search (greedy.py:15-121) and bfs with
+ * host-side dedup: the caller expands the parents the engine asks for with acx_expand12
+ * (packed keys) and feeds the child keys back; the engine replays the reference's pop /
+ * expand / dedup / budget order exactly.  mode 0 = bfs, 1 = greedy.
+ *   acx_search_next_batch  up to cap parent keys to expand next (0: nothing left)
+ *   acx_search_feed        the (count, 12, kw) child keys of the last batch; returns status
+ *   acx_search_status      0 running, 1 success, 2 failed, 3 a child move raised (its key
+ *                          is the acx_expand12 error sentinel): the reference's AssertionError
+ *   acx_search_path        the result path (see acx_search.cpp); returns its length
+ *   acx_search_stats       out[0] rounds, out[1] parents expanded, out[2] parents popped
+ *   acx_search_node_keys   the packed keys of the discovered nodes in discovery order
+ */
+void* acx_search_create(int32_t mode, int32_t L, const uint64_t* start_key, int64_t max_nodes);
+void acx_search_destroy(void* h);
+int64_t acx_search_next_batch(void* h, uint64_t* parent_keys, int64_t cap);
+int32_t acx_search_feed(void* h, const uint64_t* child_keys, int64_t count);
+int32_t acx_search_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes);
+int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap);
+void acx_search_stats(void* h, int64_t* out);
+int64_t acx_search_node_keys(void* h, uint64_t* out, int64_t cap);
 
 /* number of uint64 words in one packed key: ceil((4L + 16) / 64) */
 int32_t acx_key_words(int32_t L);

@@ -353,6 +353,46 @@ def gen_kat_search(ref):
     return out
 
 
+def gen_kat_search_extra(ref, n_cases=240):
+    """Random small presentations through the reference bfs / greedy_search with assorted
+    budgets and both cyclical flags: result, path, the node count the budget message prints
+    (len(tree_nodes), captured from stdout), or the AssertionError a move raises."""
+    import contextlib
+    import io
+    import re
+
+    rng = np.random.default_rng(7)
+    cases = []
+    for i in range(n_cases):
+        L = int(rng.integers(2, 7))
+        kind = i % 4
+        w0 = random_reduced_word(rng, int(rng.integers(1, L + 1)))
+        if kind == 3:  # relators equal or mutually inverse: some move empties a relator
+            w1 = list(w0) if rng.integers(2) else [-x for x in reversed(w0)]
+        else:
+            w1 = random_reduced_word(rng, int(rng.integers(1, L + 1)))
+        pres = np.zeros(2 * L, np.int8)
+        pres[: len(w0)] = w0
+        pres[L : L + len(w1)] = w1
+        budget = int(rng.choice([1, 2, 5, 13, 50, 200, 1000, 5000]))
+        cyc = bool(rng.integers(2))
+        fn = "bfs" if i % 2 == 0 else "greedy_search"
+        search = ref.bfs.bfs if fn == "bfs" else ref.greedy.greedy_search
+        buf = io.StringIO()
+        rec = dict(search_fn=fn, presentation=to_jsonable(pres), budget=budget, cyclical=cyc)
+        try:
+            with contextlib.redirect_stdout(buf):
+                ok, path = search(presentation=pres, max_nodes_to_explore=budget,
+                                  cyclically_reduce_after_moves=cyc)
+            rec.update(raises=False, ok=bool(ok), path=to_jsonable(path))
+        except AssertionError:
+            rec.update(raises=True)
+        m = re.search(r"number of explored nodes = (\d+)", buf.getvalue())
+        rec["budget_nodes"] = int(m.group(1)) if m else None
+        cases.append(rec)
+    return cases
+
+
 def gen_kat_paths(ref, root, ms):
     """Known-answer action sequences: the 17 exact replays of
     tests/test_solution_verification.py:503-577, the notebook AC paths, Stable-AK3."""
@@ -453,4 +493,12 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--search-extra" in sys.argv:  # only (re)generate kat_search_extra.json
+        sys.argv.remove("--search-extra")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--reference", default="/root/reference")
+        ref = load_reference(ap.parse_args().reference)
+        with open(os.path.join(HERE, "kat_search_extra.json"), "w") as f:
+            json.dump(gen_kat_search_extra(ref), f)
+    else:
+        main()

@@ -84,7 +84,18 @@ def _oracle_keys(states, L, cyclical):
     for i in range(states.shape[0]):
         for a in range(12):
             keys[i, a] = E._pack_key(ch[i, a], L)
+            if err[i, a]:  # acx_expand12's error sentinel: both length bytes 0xFF
+                keys[i, a] |= E._pack_key(np.zeros(2 * L, np.int64), L) | _len_bytes_ff(L)
     return keys
+
+
+def _len_bytes_ff(L):
+    kw = _lib.key_words(L)
+    k = np.zeros(kw, np.uint64)
+    for j in range(16):
+        b = 4 * L + j
+        k[b // 64] |= np.uint64(1) << np.uint64(b % 64)
+    return k
 
 
 def _unpack_key_host(k, L):
@@ -101,6 +112,12 @@ def _unpack_key_host(k, L):
 
 def _drive(mode, pres, budget, cyclical=False):
     """The production engine, with the GPU expansion replaced by the oracle (test only)."""
+    status, path, _ = _drive_full(mode, pres, budget, cyclical)
+    return status == 1, path
+
+
+def _drive_full(mode, pres, budget, cyclical=False):
+    """-> (engine status, path, len(tree_nodes) at the end)"""
     import ctypes
     p = np.asarray(pres)
     L = len(p) // 2
@@ -117,11 +134,12 @@ def _drive(mode, pres, budget, cyclical=False):
             parents = np.stack([_unpack_key_host(buf[i], L) for i in range(n)])
             keys = np.ascontiguousarray(_oracle_keys(parents, L, cyclical))
             status = lib.acx_search_feed(h, keys.ctypes.data, n)
-        status = lib.acx_search_status(h, None, None, None)
+        n_nodes = ctypes.c_int64(0)
+        status = lib.acx_search_status(h, None, None, ctypes.byref(n_nodes))
         acts = np.zeros(4096, np.int32)
         tots = np.zeros(4096, np.int32)
         m = lib.acx_search_path(h, acts.ctypes.data, tots.ctypes.data, 4096)
-        return status == 1, [(int(acts[i]), int(tots[i])) for i in range(m)]
+        return status, [(int(acts[i]), int(tots[i])) for i in range(m)], n_nodes.value
     finally:
         lib.acx_search_destroy(h)
 
@@ -164,3 +182,25 @@ def test_engine_miller_schupp_cases_on_oracle_expansions():
             paths.append([list(x) for x in path])
     assert solved == case["solved"]
     assert paths == case["paths"]
+
+
+def test_engine_matches_reference_on_random_searches():
+    """kat_search_extra.json: 240 reference bfs/greedy runs on random small presentations
+    (budgets 1..5000, both cyclical flags), including runs where a move raises
+    AssertionError and the node count the budget message prints."""
+    with open(os.path.join(GOLDEN, "kat_search_extra.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        mode = E.BFS if c["search_fn"] == "bfs" else E.GREEDY
+        status, path, n_nodes = _drive_full(mode, np.array(c["presentation"]), c["budget"], c["cyclical"])
+        if c["raises"]:
+            assert status == 3, c
+            continue
+        assert status in (1, 2), c
+        assert (status == 1) == c["ok"], c
+        if c["search_fn"] == "bfs":
+            assert (path if status == 1 else None) == (None if c["path"] is None else [tuple(x) for x in c["path"]]), c
+        else:
+            assert path == [tuple(x) for x in c["path"]], c
+        if c["budget_nodes"] is not None:
+            assert n_nodes == c["budget_nodes"], c

@@ -390,7 +390,11 @@ def test_partial_tiles_fast_path(L, B):
     ch, cl, ce = O.expand12(s, L, False)
     assert np.array_equal(res["children"].cpu().numpy(), ch)
     back = acx.ops.unpack_keys(res["keys"].reshape(-1, res["keys"].shape[-1]), L)
-    assert np.array_equal(back.cpu().numpy(), ch.reshape(-1, 2 * L))
+    ok = ce.reshape(-1) == 0
+    assert np.array_equal(back.cpu().numpy()[ok], ch.reshape(-1, 2 * L)[ok])
+    # an errored child's key is the sentinel: both length bytes 0xFF (acx.h)
+    _, blen = acx.ops.unpack_keys(res["keys"].reshape(-1, res["keys"].shape[-1]), L, lengths=True)
+    assert (blen.cpu().numpy()[~ok] == 0xFF).all()
     keys_only = acx.ops.expand12(torch.as_tensor(s).to(DEV), cyclical=False, children=False, keys=True)
     assert torch.equal(keys_only["keys"], res["keys"])
 

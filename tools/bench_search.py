@@ -1,10 +1,12 @@
 """Config 4 (BASELINE.json configs[3]): bfs 12-way neighbour expansion on AK(3), L = 36,
-cyclical = False, frontier of 10^7 states, host dedup.
+cyclical = False, frontier of 10^7 states.
 
 Reports (1) end-to-end acx.bfs until 10^7 distinct states are known (GPU acx_expand12 in
 batches of parents + the host engine's exact FIFO/dedup/budget replay), and (2) the
 kernel alone: acx_expand12 over all 10^7 discovered states at once, packed-key output
-(and full int32 children for the first 10^6 parents)."""
+(and full int32 children for the first 10^6 parents), and (3) the device BFS
+(csrc/acx_bfs.hip: dedup on the GPU, the "next" step of SURVEY §8f) to the same 10^7 nodes,
+plus optional larger budgets:  python tools/bench_search.py [NODES] [N2,N3,...]"""
 import ctypes
 import json
 import os
@@ -102,4 +104,21 @@ for _ in range(3):
 b = M * (8 * L + 12 * (8 * L + 8))
 res["expand12_children"] = {"parents": M, "kernel_ms": best * 1e3, "children_per_s": 12 * M / best,
                             "GBps": b / best / 1e9, "bytes_per_parent": 8 * L + 12 * (8 * L + 8)}
+
+# ---- (3) device BFS (csrc/acx_bfs.hip): queue, visited set, dedup, budget all on the GPU ----
+from acx.search import _device_bfs as D  # noqa: E402
+
+for n_nodes_dev in [NODES] + ([int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else []):
+    D.device_bfs(ak3, n_nodes_dev, device=dev)  # allocate the workspace, warm up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok, _ = D.device_bfs(ak3, n_nodes_dev, device=dev)
+    wall = time.perf_counter() - t0
+    st = dict(D.LAST_STATS)
+    res[f"device_bfs_{n_nodes_dev:.0e}".replace("+", "")] = {
+        "nodes": st["nodes"], "parents_expanded": st["parents"], "children": 12 * st["parents"],
+        "chunks": st["chunks"], "wall_s": wall, "children_per_s": 12 * st["parents"] / wall,
+        "nodes_per_s": st["nodes"] / wall, "status": st["status"],
+        "speedup_vs_host_dedup": res["bfs_end_to_end"]["wall_s"] / wall if n_nodes_dev == NODES else None}
+    D.release_workspaces()
 print(json.dumps(res))

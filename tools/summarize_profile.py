@@ -71,5 +71,12 @@ if bench:
         }
 with open(os.path.join(out_dir, f"{tag}_summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
-shutil.copy(os.path.join(d, "trace", "bench_kernel_stats.csv"), os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
+for src, dst in (("trace/bench_kernel_stats.csv", "kernel_stats.csv"), ("trace/bench_kernel_trace.csv", "kernel_trace.csv"),
+                 ("pmc_fetch/bench_counter_collection.csv", "pmc_fetch.csv"),
+                 ("pmc_write/bench_counter_collection.csv", "pmc_write.csv")):
+    if os.path.exists(os.path.join(d, src)):
+        shutil.copy(os.path.join(d, src), os.path.join(out_dir, f"{tag}_{dst}"))
+if bench:
+    with open(os.path.join(out_dir, f"{tag}_bench_under_rocprof.json"), "w") as f:
+        f.write(json.dumps(bench) + "\n")
 print(json.dumps(summary.get("rollout_timed_dispatch"), indent=1))
