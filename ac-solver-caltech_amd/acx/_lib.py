@@ -33,6 +33,8 @@ SIGNATURES = {
     "acx_unpack_keys": ([_P] * 3 + [_I64, _I32, _P], ctypes.c_int),
     "acx_key_words": ([_I32], ctypes.c_int32),
     "acx_version": ([], ctypes.c_char_p),
+    "acx_features": ([_P] * 5 + [_I64, _I32, _P], ctypes.c_int),
+    "acx_token_ids": ([_P] * 3 + [_I64, _I32, _I32, _P], ctypes.c_int),
     # host-side search engine (ac-solver-caltech_amd/csrc/acx_search.cpp)
     "acx_search_create": ([_I32, _I32, _P, _I64], ctypes.c_void_p),
     "acx_search_destroy": ([_P], None),

@@ -219,3 +219,59 @@ def unpack_keys(keys: torch.Tensor, L: int, *, out: Optional[torch.Tensor] = Non
     st = lib.acx_unpack_keys(_ptr(keys), _ptr(out), _ptr(lens), M, int(L), _stream(dev))
     _lib.check(st, "acx_unpack_keys")
     return (out, lens) if lengths else out
+
+
+def _states_or_keys(states, keys, L):
+    if (states is None) == (keys is None):
+        raise ValueError("pass exactly one of states= or keys=")
+    if states is not None:
+        _need_gpu(states, "states")
+        L = _L_of(states)
+        M = states.shape[0]
+        _check(states, "states", _INT32, (M, 2 * L), states.device)
+        return states, None, L, M, states.device
+    if L is None:
+        raise ValueError("keys= needs L")
+    _need_gpu(keys, "keys")
+    kw = _lib.key_words(L)
+    keys = keys.reshape(-1, kw)
+    M = keys.shape[0]
+    _check(keys, "keys", torch.int64, (M, kw), keys.device)
+    return None, keys, int(L), M, keys.device
+
+
+def features(*, states: Optional[torch.Tensor] = None, keys: Optional[torch.Tensor] = None, L: Optional[int] = None,
+             mean: Optional[torch.Tensor] = None, std: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None):
+    """acx_features: the 14 features of value_search/feature_extraction.py:11-91 per presentation
+    ((M,2L) int32 states, or packed keys with L) -> (M,14) float32; normalised (f - mean)/std
+    when mean and std (14 float32 each) are given, as value_guided_search.py:49-66."""
+    lib = _lib.load()
+    states, keys, L, M, dev = _states_or_keys(states, keys, L)
+    if (mean is None) != (std is None):
+        raise ValueError("pass both mean and std, or neither")
+    for name, t in (("mean", mean), ("std", std)):
+        _check(t, name, torch.float32, (14,), dev)
+    if out is None:
+        out = torch.empty((M, 14), dtype=torch.float32, device=dev)
+    _check(out, "out", torch.float32, (M, 14), dev)
+    st = lib.acx_features(_ptr(states), _ptr(keys), _ptr(mean), _ptr(std), _ptr(out), M, L, _stream(dev))
+    _lib.check(st, "acx_features")
+    return out
+
+
+def token_ids(*, states: Optional[torch.Tensor] = None, keys: Optional[torch.Tensor] = None, L: Optional[int] = None,
+              max_state_dim: Optional[int] = None, out: Optional[torch.Tensor] = None):
+    """acx_token_ids: SequenceValueNet input (value_guided_search.py:68-84): letter + 2 as int64,
+    padded with 2 to max_state_dim (default 2L) -> (M, max_state_dim) int64."""
+    lib = _lib.load()
+    states, keys, L, M, dev = _states_or_keys(states, keys, L)
+    D = 2 * L if max_state_dim is None else int(max_state_dim)
+    if D < 2 * L:
+        raise ValueError(f"max_state_dim {D} < 2L = {2 * L}")
+    if out is None:
+        out = torch.empty((M, D), dtype=torch.int64, device=dev)
+    _check(out, "out", torch.int64, (M, D), dev)
+    st = lib.acx_token_ids(_ptr(states), _ptr(keys), _ptr(out), M, L, D, _stream(dev))
+    _lib.check(st, "acx_token_ids")
+    return out

@@ -145,6 +145,20 @@ void acx_bfs_destroy(void* h);
 int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
 
 /*
+ * Scoring inputs for value-guided search (value_search/): exactly one of `states` ((M,2L) int32)
+ * or `keys` ((M, acx_key_words(L)) packed keys, e.g. acx_expand12 output) is non-NULL.
+ *   acx_features   out (M,14) float32 = compute_features (feature_extraction.py:11-91); with
+ *                  mean/std (14 float32 each, both or neither) normalised (f - mean) / std as
+ *                  _score_states_mlp does (value_guided_search.py:49-66).
+ *   acx_token_ids  out (M, max_state_dim) int64 = letter + 2, padded with 2
+ *                  (_score_states_seq, value_guided_search.py:68-84); max_state_dim >= 2L.
+ */
+int acx_features(const int32_t* states, const uint64_t* keys, const float* mean, const float* stdv, float* out,
+                 int64_t M, int32_t L, void* stream);
+int acx_token_ids(const int32_t* states, const uint64_t* keys, int64_t* out, int64_t M, int32_t L,
+                  int32_t max_state_dim, void* stream);
+
+/*
  * Host search engine (csrc/acx_search.cpp) for greedy_search (greedy.py:15-121) and bfs with
  * host-side dedup: the caller expands the parents the engine asks for with acx_expand12
  * (packed keys) and feeds the child keys back; the engine replays the reference's pop /

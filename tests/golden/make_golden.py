@@ -393,6 +393,49 @@ def gen_kat_search_extra(ref, n_cases=240):
     return cases
 
 
+def gen_features(root, ms, rng):
+    """The reference's compute_features (value_search/feature_extraction.py, numpy only) on
+    Miller-Schupp starts (L = 18, its default), random-walk states at L = 36 and L = 7, and
+    hand edge cases; token ids are restated in oracle/features.py (a one-line numpy op)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_feature_extraction",
+                                                  os.path.join(root, "value_search", "feature_extraction.py"))
+    fe = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fe)
+    out = {}
+    ref = load_reference(root)
+    for L, n in ((18, len(ms)), (36, 3000), (7, 2000)):
+        rows = []
+        if L == 18:
+            rows = list(ms)
+        else:
+            for i in range(n):
+                s = np.zeros(2 * L, np.int8)
+                w0 = random_reduced_word(rng, int(rng.integers(1, L + 1)))
+                w1 = random_reduced_word(rng, int(rng.integers(1, L + 1)))
+                s[: len(w0)] = w0
+                s[L : L + len(w1)] = w1
+                for _ in range(int(rng.integers(0, 30))):
+                    s2, _, e = ref_move(ref, s, L, int(rng.integers(12)), True)
+                    if e == ERR_OK:
+                        s = s2.astype(np.int8)
+                rows.append(s)
+            # edge cases: single letters, one relator at full length, balanced halves
+            edge = np.zeros((4, 2 * L), np.int8)
+            edge[0, 0], edge[0, L] = 1, 2
+            edge[1, :L] = 2
+            edge[1, L] = -1
+            edge[2, 0], edge[2, L : 2 * L] = -1, -2
+            edge[3, : L // 2 + 1] = 1
+            edge[3, L : L + L // 2 + 1] = -2
+            rows += list(edge)
+        st = np.stack(rows).astype(np.int8)
+        out[f"L{L}_states"] = st
+        out[f"L{L}_features"] = np.stack([fe.compute_features(x, L) for x in st]).astype(np.float32)
+    return out
+
+
 def gen_kat_paths(ref, root, ms):
     """Known-answer action sequences: the 17 exact replays of
     tests/test_solution_verification.py:503-577, the notebook AC paths, Stable-AK3."""
@@ -493,7 +536,15 @@ def main():
 
 
 if __name__ == "__main__":
-    if "--search-extra" in sys.argv:  # only (re)generate kat_search_extra.json
+    if "--features" in sys.argv:  # only (re)generate features.npz
+        sys.argv.remove("--features")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--reference", default="/root/reference")
+        root = ap.parse_args().reference
+        ms = np.load(os.path.join(PKG_DATA, "all_presentations.npy"))
+        np.savez_compressed(os.path.join(HERE, "features.npz"),
+                            **gen_features(root, ms, np.random.default_rng(11)))
+    elif "--search-extra" in sys.argv:  # only (re)generate kat_search_extra.json
         sys.argv.remove("--search-extra")
         ap = argparse.ArgumentParser()
         ap.add_argument("--reference", default="/root/reference")

@@ -130,3 +130,15 @@ def test_config1():
         assert st[0].tolist() == row["state"]
         assert int(r[0]) == row["reward"] and bool(dn[0]) == row["done"] and bool(tr[0]) == row["truncated"]
         assert lens[0].tolist() == row["lengths"]
+
+
+def test_features_oracle_vs_reference_golden():
+    """oracle/features.py restatement vs the reference's compute_features outputs."""
+    from oracle import features as F
+    d = np.load(os.path.join(GOLDEN, "features.npz"))
+    for L in (18, 36, 7):
+        st, exp = d[f"L{L}_states"], d[f"L{L}_features"]
+        got = F.compute_features_batch(st, L)
+        assert got.dtype == np.float32 and np.array_equal(got.view(np.uint32), exp.view(np.uint32)), L
+    tok = F.token_ids(d["L18_states"], 72)
+    assert tok.dtype == np.int64 and (tok[:, 36:] == 2).all() and np.array_equal(tok[:, :36], d["L18_states"] + 2)
