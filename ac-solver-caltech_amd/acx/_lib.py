@@ -27,6 +27,9 @@ _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
 SIGNATURES = {
     "acx_step": ([_P] * 12 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_step_learner": ([_P] * 11 + [_I32, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_curriculum_workspace": ([_I64], ctypes.c_int64),
+    "acx_curriculum_assign": ([_P, _P, _P, _I64] + [_P] * 7 + [_I64, _I32, _P], ctypes.c_int),
     "acx_rollout": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_expand12": ([_P] * 6 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_canonicalize": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),

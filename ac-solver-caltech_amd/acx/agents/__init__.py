@@ -1,0 +1,4 @@
+"""PPO-side plumbing for the device env (ac_solver/agents/training.py rollout phase)."""
+from .rollout import LearnerEnv
+
+__all__ = ["LearnerEnv"]

@@ -1,0 +1,121 @@
+"""Device-resident env plumbing for the PPO rollout phase (ac_solver/agents/training.py:221-356).
+
+The reference steps a gymnasium SyncVectorEnv on the host each step (`envs.step(action.cpu()
+.numpy())`, training.py:238-240), copies obs/reward/done back to the device (:241, :354-356)
+and runs a Python loop over the envs for episode bookkeeping and the start-state curriculum
+(:262-352).  LearnerEnv keeps all of it on the GPU, one acx_step_learner + one
+acx_curriculum_assign launch per step:
+
+  * the policy's int64 actions go straight in;
+  * the next observation is written as float32 into whatever (B, 2L) buffer the caller names
+    (e.g. obs[t + 1] of the learner's (T, B, 2L) buffer), rewards[t] and next_done likewise;
+  * each env's current episode moves are kept in a (B, hist_cap) byte buffer, so info["actions"]
+    of a solved episode (training.py:275-280) is one row read;
+  * the round-1 curriculum (training.py:319-336, 349-352) runs on the device: finished envs
+    take the next unprocessed initial state in env order.  Once every initial state has been
+    used the reference draws random solved/unsolved states with Python `random` (:337-346);
+    those envs are flagged in `needs_host` and placed by `place()`.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..envs.ac_env import VecACEnv
+
+
+class LearnerEnv:
+    def __init__(self, initial_states, num_envs: int, horizon_length: int = 200, device=None,
+                 cyclical: bool = True, hist_cap: Optional[int] = None):
+        init = np.asarray(initial_states)
+        if init.ndim != 2 or num_envs > init.shape[0]:
+            raise ValueError("initial_states must be (N, 2L) with N >= num_envs (environment.py:82-86)")
+        # env i starts at initial_states[i]; states 0..num_envs-1 are processed (environment.py:96-101)
+        self.vec = VecACEnv(init[:num_envs], horizon_length=horizon_length, device=device, cyclical=cyclical,
+                            track_final_obs=False)
+        dev = self.vec.device
+        self.device = dev
+        self.num_envs = num_envs
+        self.L = self.vec.max_relator_length
+        self.horizon_length = int(horizon_length)
+        self.initial_states = torch.as_tensor(init.astype(np.int32)).to(dev).contiguous()
+        self.n_states = init.shape[0]
+        self.curr_index = torch.arange(num_envs, dtype=torch.int32, device=dev)
+        self.next_index = torch.tensor([num_envs], dtype=torch.int32, device=dev)  # max(states_processed) + 1
+        self.needs_host = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
+        self.hist_cap = int(hist_cap if hist_cap is not None else horizon_length)
+        self.action_hist = torch.zeros((num_envs, self.hist_cap), dtype=torch.uint8, device=dev)
+        self.episode_len = torch.zeros(num_envs, dtype=torch.int32, device=dev)
+        self.done = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
+        self.truncated = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
+        self._ws = torch.zeros(int(_lib.load().acx_curriculum_workspace(num_envs)), dtype=torch.int32, device=dev)
+
+    @property
+    def state(self) -> torch.Tensor:
+        return self.vec.state
+
+    def initial_obs(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """next_obs before the first step (training.py:190-193) as float32."""
+        o = self.vec.state.to(torch.float32)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+
+    def step(self, action: torch.Tensor, obs_out: Optional[torch.Tensor] = None,
+             reward_out: Optional[torch.Tensor] = None, done_out: Optional[torch.Tensor] = None):
+        """One env step for all envs.  action: (B,) int64 (policy samples) or int32 device tensor.
+        obs_out / reward_out / done_out: float32 (B, 2L) / (B,) / (B,) device views to fill
+        (next_obs, rewards[t], next_done).  Returns (done, truncated, episode_len, needs_host)
+        uint8/int32 device tensors; no host synchronisation."""
+        lib = _lib.load()
+        B, L, dev = self.num_envs, self.L, self.device
+        for name, t, shape in (("obs_out", obs_out, (B, 2 * L)), ("reward_out", reward_out, (B,)),
+                               ("done_out", done_out, (B,))):
+            if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != shape or t.device != dev
+                                  or not t.is_contiguous()):
+                raise ValueError(f"{name} must be a contiguous float32 {shape} tensor on {dev}")
+        if action.device != dev or action.shape != (B,) or not action.is_contiguous():
+            action = action.to(dev).contiguous().reshape(B)
+        a32 = action if action.dtype == torch.int32 else None
+        a64 = action if action.dtype == torch.int64 else None
+        if a32 is None and a64 is None:
+            a64 = action.to(torch.int64)
+        v = self.vec
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        st = lib.acx_step_learner(
+            v.state.data_ptr(), ptr(a32), ptr(a64), v.reset_state.data_ptr(), v.step_count.data_ptr(), ptr(obs_out),
+            ptr(reward_out), ptr(done_out), self.done.data_ptr(), self.truncated.data_ptr(),
+            self.action_hist.data_ptr(), self.hist_cap, self.episode_len.data_ptr(), None, v.err.data_ptr(),
+            v.err_count.data_ptr(), B, L, self.horizon_length, int(v.cyclical), stream)
+        _lib.check(st, "acx_step_learner")
+        st = lib.acx_curriculum_assign(
+            self.done.data_ptr(), self.truncated.data_ptr(), self.initial_states.data_ptr(), self.n_states,
+            self.next_index.data_ptr(), self.curr_index.data_ptr(), self.needs_host.data_ptr(), v.state.data_ptr(),
+            v.reset_state.data_ptr(), ptr(obs_out), self._ws.data_ptr(), B, L, stream)
+        _lib.check(st, "acx_curriculum_assign")
+        return self.done, self.truncated, self.episode_len, self.needs_host
+
+    def episode_actions(self, i: int) -> list:
+        """info["actions"] of env i's episode that ended at the last step (training.py:275-280)."""
+        n = int(self.episode_len[i].item())
+        if n > self.hist_cap:
+            raise ValueError(f"episode of {n} moves exceeds hist_cap {self.hist_cap}")
+        return [int(x) for x in self.action_hist[i, :n].cpu().numpy()]
+
+    def place(self, i: int, state_index: int, obs_out: Optional[torch.Tensor] = None) -> None:
+        """Host placement of env i (after round 1, training.py:337-352): start from
+        initial_states[state_index]."""
+        s = self.initial_states[state_index]
+        self.vec.reset_state[i].copy_(s)
+        self.vec.state[i].copy_(s)
+        self.vec.step_count[i] = 0
+        self.curr_index[i] = state_index
+        self.needs_host[i] = 0
+        if obs_out is not None:
+            obs_out[i].copy_(s.to(torch.float32))

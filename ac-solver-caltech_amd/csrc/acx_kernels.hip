@@ -94,6 +94,32 @@ __device__ __forceinline__ void st16(int4* p, const int4& v) {
         *p = v;
     }
 }
+// 16 bytes of a row: int32 letters, or (F32) the same letters as float32 (the PPO learner's
+// observation buffer, training.py:151-153)
+template <bool NT, bool F32>
+__device__ __forceinline__ void out16(int4* p, const int4& v) {
+    if constexpr (F32) {
+        float4 f;
+        f.x = (float)v.x;
+        f.y = (float)v.y;
+        f.z = (float)v.z;
+        f.w = (float)v.w;
+        *reinterpret_cast<float4*>(p) = f;
+    } else {
+        st16<NT>(p, v);
+    }
+}
+template <bool F32>
+__device__ __forceinline__ void out8(int2* p, const int2& v) {
+    if constexpr (F32) {
+        float2 f;
+        f.x = (float)v.x;
+        f.y = (float)v.y;
+        *reinterpret_cast<float2*>(p) = f;
+    } else {
+        *p = v;
+    }
+}
 template <bool NT, class T>
 __device__ __forceinline__ void st_scalar(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -205,7 +231,7 @@ struct FastTile {
     }
 
     // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from fallback
-    template <bool FB, bool NT = false>
+    template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
                                           int64_t fpitch, int lane) const {
         int ln = lane;
@@ -222,7 +248,7 @@ struct FastTile {
                     if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
 #pragma unroll
                 for (int u = 0; u < STAGE_UNROLL; ++u)
-                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) st16<NT>(dst + (u0 + u) * WAVE, widen4(p[u]));
+                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
             }
             return;
         }
@@ -239,8 +265,8 @@ struct FastTile {
                     const int r = c / CPR;
                     const int pos = 4 * (c - r * CPR);
                     int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
-                    if (FB && flags[r]) *dst = *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos);
-                    else *dst = widen4(p[u]);
+                    if (FB && flags[r]) out16<false, F32>(dst, *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos));
+                    else out16<NT, F32>(dst, widen4(p[u]));
                 }
             }
         }
@@ -371,7 +397,7 @@ struct CodeTile {
         wave_sync();
     }
 
-    template <bool FB, bool NT = false>
+    template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
                                           int64_t fpitch, int lane) const {
         int ln = lane;
@@ -390,10 +416,10 @@ struct CodeTile {
                 const int pos = 4 * (c - r * CPR);
                 int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
                 if (FB && tile_bad && flags[r]) {
-                    *dst = *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos);
+                    out16<false, F32>(dst, *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos));
                 } else {
                     const uint32_t nz4 = (p[u] >> 8) & 0xfu;
-                    st16<NT>(dst, widen4(swar_unpack4(p[u] & 0xffu, __builtin_popcount(nz4))));
+                    out16<NT, F32>(dst, widen4(swar_unpack4(p[u] & 0xffu, __builtin_popcount(nz4))));
                 }
             }
         }
@@ -538,7 +564,7 @@ struct GenericTile {
         wave_sync();
     }
 
-    template <bool FB, bool NT = false>
+    template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
                                           int64_t fpitch, int lane) const {
         const int nc = (R * twoL) / VEC;
@@ -565,12 +591,12 @@ struct GenericTile {
                 const bool fb = FB && flags[rows[u]];
                 const int32_t* f = fallback + (int64_t)rows[u] * fpitch + poss[u];
                 if constexpr (VEC == 4) {
-                    *reinterpret_cast<int4*>(dst) = fb ? *reinterpret_cast<const int4*>(f) : widen4(p[u]);
+                    out16<false, F32>(reinterpret_cast<int4*>(dst), fb ? *reinterpret_cast<const int4*>(f) : widen4(p[u]));
                 } else {
                     int2 x;
                     x.x = (int32_t)(int8_t)(p[u] & 0xffu);
                     x.y = (int32_t)(int8_t)((p[u] >> 8) & 0xffu);
-                    *reinterpret_cast<int2*>(dst) = fb ? *reinterpret_cast<const int2*>(f) : x;
+                    out8<F32>(reinterpret_cast<int2*>(dst), fb ? *reinterpret_cast<const int2*>(f) : x);
                 }
             }
         }
@@ -686,8 +712,15 @@ struct StepArgs {
     int32_t* final_obs;
     uint8_t* err;
     int32_t* err_count;
+    // learner-side outputs (acx_step_learner; all NULL for acx_step)
+    const int64_t* action64;
+    float* obs_f32;
+    float* reward_f32;
+    float* done_f32;
+    uint8_t* action_hist;
+    int32_t* episode_len;
     int64_t B;
-    int L, horizon, cyclical;
+    int L, horizon, cyclical, hist_cap;
 };
 
 template <int NW, int LC, int VEC>
@@ -704,8 +737,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 
     if (w.active) {
         PresRegs<NW> p;
-        const int act = a.action[env];
+        int act;
+        if (a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
+            const int64_t v = a.action64[env];
+            act = (v >= 0 && v < 12) ? (int)v : -1;
+        } else {
+            act = a.action[env];
+        }
         int cnt = a.step_count ? a.step_count[env] + 1 : 0;
+        // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each
+        if (a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[env * a.hist_cap + (cnt - 1)] = (uint8_t)act;
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
         int e;
@@ -718,6 +759,9 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
+        if (a.reward_f32) a.reward_f32[env] = (float)(triv ? a.horizon * L * 2 : -(p.n0 + p.n1));
+        if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
+        if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
         int l0 = p.n0, l1 = p.n1;
         if ((triv || trunc) && a.reset_state && e == ACX_ERR_NONE) {
             // same-step autoreset (rare): final_obs <- post-move state, state <- reset row
@@ -738,6 +782,9 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     }
     wave_sync();
     tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
+    if (a.obs_f32)  // the same rows as float32, straight into the learner's buffer
+        tile.template store<true, false, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
+                                               a.state_in + w.r0 * twoL, twoL, w.lane);
 }
 
 struct RolloutArgs {
@@ -1126,7 +1173,24 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
     if (!aligned16(state_in) || !aligned16(state_out)) return ACX_E_ARG;
     if (reset_state && !step_count) return ACX_E_ARG;
     StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated,
-               lengths_out, final_obs, err, err_count, B, L, horizon, cyclical};
+               lengths_out, final_obs, err, err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+               B, L, horizon, cyclical, 0};
+    StepLaunch f{a, (hipStream_t)stream};
+    return dispatch(L, f);
+}
+
+int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* action_i64, const int32_t* reset_state,
+                     int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len,
+                     int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                     int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state || !step_count || (!action == !action_i64) || (action_hist && hist_cap == 0)) return ACX_E_ARG;
+    if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
+    StepArgs a{state, state, action, reset_state, step_count, nullptr, done, truncated, nullptr, final_obs, err,
+               err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
+               cyclical, hist_cap};
     StepLaunch f{a, (hipStream_t)stream};
     return dispatch(L, f);
 }

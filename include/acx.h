@@ -82,6 +82,42 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
              void* stream);
 
 /*
+ * acx_step for the PPO learner (ac_solver/agents/training.py:221-356), state updated in place
+ * with same-step autoreset to reset_state, plus the learner-side writes fused in:
+ *   action / action_i64 : exactly one non-NULL; action_i64 = the policy's int64 samples
+ *                         (training.py:232-236), out of [0,12) -> ACX_ERR_ACTION.
+ *   obs_f32     (B,2L) float32 or NULL: the next observation (post reset), written straight
+ *               into the learner's buffer (e.g. obs[t+1], training.py:151-153,225).
+ *   reward_f32  (B) float32 or NULL (rewards[t], training.py:241-253).
+ *   done_f32    (B) float32 or NULL: done only, as next_done = torch.Tensor(done) (:354-356).
+ *   done, truncated (B) uint8 or NULL.
+ *   action_hist (B, hist_cap) uint8 or NULL: the moves of each env's current episode, move k
+ *               at [env, k] (ACEnv.actions / info["actions"], ac_env.py:96,105; training.py:275-280).
+ *   episode_len (B) int32 or NULL: the length of the episode that ended this step, else 0.
+ *   step_count is required (truncation, history position).
+ */
+int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* action_i64, const int32_t* reset_state,
+                     int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len,
+                     int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                     int32_t cyclical, void* stream);
+
+/*
+ * Start-state curriculum of the PPO trainer, round 1 (training.py:319-352): every env whose
+ * episode ended this step (done | truncated), in env order, starts next from
+ * curriculum_states[k], k = *next_index, *next_index + 1, ... (max(states_processed) + 1);
+ * its state, reset_state (nullable) and obs_f32 (nullable) rows are set to that state and
+ * curr_index[env] = k.  When k reaches n_states round 1 is complete and the env is flagged in
+ * needs_host[env] = 1 (the reference then draws a random solved/unsolved state on the host).
+ * workspace: acx_curriculum_workspace(B) int32 device words.
+ */
+int64_t acx_curriculum_workspace(int64_t B);
+int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
+                          int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
+                          int32_t* state, int32_t* reset_state, float* obs_f32, int32_t* workspace, int64_t B,
+                          int32_t L, void* stream);
+
+/*
  * T fused env steps (PPO rollout collection).  state (B,2L) and step_count (B) are
  * updated in place; actions is (T,B) int32.  Per step t the kernel writes (all optional):
  *   obs_traj[t]    (T,B,2L) int32  observation after step t (post autoreset)

@@ -1,0 +1,104 @@
+"""GPU parity of the PPO rollout plumbing (acx_step_learner + acx_curriculum_assign, via
+acx.agents.LearnerEnv) against oracle/curriculum.py, the restatement of the env side of
+training.py:221-352 (oracle env step, episode action lists, round-1 curriculum)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import curriculum as C
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _ms_states(L, n):
+    import acx
+    ms = np.load(os.path.join(os.path.dirname(acx.__file__), "data", "all_presentations.npy"))
+    out = np.zeros((n, 2 * L), np.int32)
+    for i in range(n):
+        p = ms[i % len(ms)]
+        out[i, :18], out[i, L : L + 18] = p[:18], p[18:]
+    return out
+
+
+@pytest.mark.parametrize("L,B,N,H,T,adtype", [(36, 128, 300, 5, 40, torch.int64), (36, 1000, 1190, 9, 30, torch.int32),
+                                              (18, 77, 200, 3, 60, torch.int64), (128, 64, 150, 4, 25, torch.int64)])
+def test_learner_env_matches_training_loop_restatement(L, B, N, H, T, adtype):
+    from acx.agents import LearnerEnv
+    init = _ms_states(L, N)
+    # a few envs that solve quickly: trivial-adjacent starts ([x],[y x]) so `done` happens too
+    init[1] = 0
+    init[1, 0], init[1, L], init[1, L + 1] = 1, 2, 1
+    ref = C.RolloutEnvs(init, B, H)
+    env = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    obs = torch.empty((T + 1, B, 2 * L), dtype=torch.float32, device=DEV)
+    rew = torch.empty((T, B), dtype=torch.float32, device=DEV)
+    dones = torch.empty((T, B), dtype=torch.float32, device=DEV)
+    env.initial_obs(out=obs[0])
+    rng = np.random.default_rng(L + B)
+    host_pick = lambda i: (7 * i + 3) % N  # noqa: E731  stands in for random.choice (training.py:337-346)
+    n_host = n_done = 0
+    for t in range(T):
+        a = rng.integers(0, 12, size=B)
+        res = ref.step(a, host_pick)
+        done, trunc, ep_len, needs_host = env.step(torch.as_tensor(a).to(DEV, adtype), obs_out=obs[t + 1],
+                                                   reward_out=rew[t], done_out=dones[t])
+        nh = needs_host.cpu().numpy().astype(bool)
+        assert np.array_equal(nh, res["picked_by_host"]), t
+        for i in np.nonzero(nh)[0]:
+            env.place(int(i), host_pick(int(i)), obs_out=obs[t + 1])
+        n_host += int(nh.sum())
+        assert np.array_equal(done.cpu().numpy(), res["done"]) and np.array_equal(trunc.cpu().numpy(), res["truncated"])
+        assert np.array_equal(rew[t].cpu().numpy(), res["reward"].astype(np.float32))
+        assert np.array_equal(dones[t].cpu().numpy(), res["done"].astype(np.float32))
+        assert np.array_equal(ep_len.cpu().numpy(), res["episode_len"])
+        for i, acts in res["info_actions"].items():
+            assert env.episode_actions(i) == acts
+            n_done += 1
+        assert np.array_equal(env.state.cpu().numpy(), ref.state), t
+        assert np.array_equal(obs[t + 1].cpu().numpy(), ref.state.astype(np.float32)), t
+        assert env.curr_index.cpu().tolist() == ref.curr_states
+    assert n_host > 0 or N - B > T * B  # round 1 completed in the long cases
+
+
+def test_step_learner_matches_acx_step():
+    """obs_f32 / reward_f32 / done_f32 are the int outputs of acx_step, converted."""
+    import acx
+    from acx import _lib
+    L, B = 36, 5000
+    init = _ms_states(L, B)
+    st_a = torch.as_tensor(init).to(DEV)
+    st_b = st_a.clone()
+    rs = st_a.clone()
+    ca = torch.zeros(B, dtype=torch.int32, device=DEV)
+    cb = ca.clone()
+    lib = _lib.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1)
+    for t in range(30):
+        a = torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)
+        rew = torch.empty(B, dtype=torch.int32, device=DEV)
+        dn = torch.empty(B, dtype=torch.uint8, device=DEV)
+        acx.ops.step(st_a, a.to(torch.int32), state_out=st_a, reset_state=rs, step_count=ca, horizon=11, reward=rew,
+                     done=dn)
+        obs = torch.empty((B, 2 * L), dtype=torch.float32, device=DEV)
+        rf = torch.empty(B, dtype=torch.float32, device=DEV)
+        df = torch.empty(B, dtype=torch.float32, device=DEV)
+        rc = lib.acx_step_learner(st_b.data_ptr(), None, a.data_ptr(), rs.data_ptr(), cb.data_ptr(), obs.data_ptr(),
+                                  rf.data_ptr(), df.data_ptr(), None, None, None, 0, None, None, None, None, B, L, 11, 1,
+                                  stream)
+        assert rc == 0
+        assert torch.equal(st_a, st_b) and torch.equal(ca, cb)
+        assert torch.equal(obs, st_b.to(torch.float32))
+        assert torch.equal(rf, rew.to(torch.float32)) and torch.equal(df, dn.to(torch.float32))
+    # out-of-range int64 action -> ACX_ERR_ACTION, state kept
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    bad = torch.full((B,), 12, dtype=torch.int64, device=DEV)
+    before = st_b.clone()
+    assert lib.acx_step_learner(st_b.data_ptr(), None, bad.data_ptr(), rs.data_ptr(), cb.data_ptr(), None, None, None,
+                                None, None, None, 0, None, None, err.data_ptr(), None, B, L, 11, 1, stream) == 0
+    assert (err == _lib.ERR_ACTION).all() and torch.equal(before, st_b)
