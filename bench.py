@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-step-api", action="store_true")
+    ap.add_argument("--no-learner", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -235,6 +236,40 @@ def main():
                          "bytes_per_env_step": sb},
         }
         n_err = int(err_count.item())
+
+    if not args.no_learner and world == 1:
+        # PPO plumbing (acx.agents.LearnerEnv): per step one acx_step_learner (int64 policy
+        # actions in, float32 obs straight into the learner's (T+1,B,2L) buffer, float32
+        # reward/done, episode move history) + one acx_curriculum_assign
+        from acx.agents import LearnerEnv
+        KL = min(K, 50)
+        lenv = LearnerEnv(np.concatenate([ms_starts(L, B), ms_starts(L, 4096, offset=B)]), B, horizon_length=H,
+                          device=dev)
+        lobs = torch.empty((KL + 1, B, 2 * L), dtype=torch.float32, device=dev)
+        lrew = torch.empty((KL, B), dtype=torch.float32, device=dev)
+        ldone = torch.empty((KL, B), dtype=torch.float32, device=dev)
+        la = actions[W : W + KL].to(torch.int64)
+        lobs.zero_()
+        lenv.step(la[0], obs_out=lobs[1], reward_out=lrew[0], done_out=ldone[0])
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for t in range(KL):
+            lenv.step(la[t], obs_out=lobs[t + 1], reward_out=lrew[t], done_out=ldone[t])
+        e1.record()
+        torch.cuda.synchronize()
+        s_l = e0.elapsed_time(e1) / 1e3
+        # per env-step: state in/out 16L + action 8 + count in/out 8 + obs f32 8L + reward f32 4
+        # + done f32 4 + done/trunc u8 2 + history 1 + episode_len 4 + err 1 + curriculum
+        # (done/trunc re-read 2, needs_host 1)
+        lb = 24 * L + 35
+        variants["learner_step"] = {
+            "value": B * KL / s_l, "unit": "env-steps/s", "steps": KL, "ms_per_step": s_l / KL * 1e3,
+            "roofline": {"bound": "hbm", "achieved": B * lb / (s_l / KL) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb},
+        }
+        del lobs, lrew, ldone, lenv
 
     # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
