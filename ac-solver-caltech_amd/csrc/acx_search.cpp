@@ -9,14 +9,12 @@
 //     (breadth_first.py:61-95).  Parents are expanded ahead in FIFO order, which cannot
 //     change the result because expansion is a pure function of the state.
 //   * greedy: priority order (total length, path length, state tuple) -- a total order,
-//     so heapq's pop sequence equals walking an ordered set from its minimum
-//     (greedy.py:181-239).  The smallest not-yet-expanded nodes are expanded
+//     so heapq's pop sequence equals popping a min-heap on that order (greedy.py:181-239).  The smallest not-yet-expanded nodes are expanded
 //     speculatively in one launch; children are cached until their parent is popped.
 // Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
 // acx_key_words(L) uint64 words.
 #include <cstdint>
 #include <cstring>
-#include <set>
 #include <vector>
 
 #include "acx.h"
@@ -45,7 +43,6 @@ struct Engine {
     std::vector<int8_t> action;
     std::vector<int16_t> total;
     std::vector<int32_t> depth;
-    std::vector<int8_t> lex;  // greedy only: node * 2L letters + 2 (tuple order)
     // open-addressing hash set; entry = (node id + 1) << 24 | 24-bit hash tag, 0 = empty.
     // The tag filters almost every non-matching probe without touching the node's key.
     std::vector<uint64_t> table;
@@ -54,20 +51,71 @@ struct Engine {
     // BFS queue
     std::vector<int64_t> queue;
     size_t head = 0, requested = 0;
-    // greedy ordered frontier
-    struct Cmp {
-        const Engine* e;
-        bool operator()(int64_t a, int64_t b) const {
-            if (e->total[a] != e->total[b]) return e->total[a] < e->total[b];
-            if (e->depth[a] != e->depth[b]) return e->depth[a] < e->depth[b];
-            const int n = 2 * e->L;
-            const int c = std::memcmp(&e->lex[(size_t)a * n], &e->lex[(size_t)b * n], (size_t)n);
-            if (c != 0) return c < 0;
-            return a < b;
+    // greedy ordered frontier: the heap tuple (total, path length, state tuple) of
+    // greedy.py:161-167,231-239 packed MSB-first into pk words per node -- total (8 bits),
+    // depth (24 bits), then every letter + 2 (3 bits, r0 then r1 incl. padding) -- so
+    // comparing the words as unsigned integers is Python's tuple order.  Two 4-ary min-heaps
+    // with the keys inline (no pointer chasing per comparison): all unpopped nodes (pop
+    // order) and the subset not yet sent to the GPU (speculative expansion order).
+    int pk = 0;
+    struct Heap {
+        int pk = 0;
+        std::vector<uint64_t> k;  // size() * pk key words
+        std::vector<int64_t> id;
+        bool empty() const { return id.empty(); }
+        int64_t top() const { return id[0]; }
+        bool less(const uint64_t* a, const uint64_t* b) const {
+            for (int i = 0; i < pk; ++i)
+                if (a[i] != b[i]) return a[i] < b[i];
+            return false;
+        }
+        void push(const uint64_t* key, int64_t v) {
+            size_t i = id.size();
+            id.push_back(v);
+            k.resize(k.size() + pk);
+            uint64_t tmp[32];
+            std::memcpy(tmp, key, sizeof(uint64_t) * pk);
+            while (i > 0) {
+                const size_t par = (i - 1) / 4;
+                if (!less(tmp, &k[par * pk])) break;
+                std::memcpy(&k[i * pk], &k[par * pk], sizeof(uint64_t) * pk);
+                id[i] = id[par];
+                i = par;
+            }
+            std::memcpy(&k[i * pk], tmp, sizeof(uint64_t) * pk);
+            id[i] = v;
+        }
+        void pop() {
+            const size_t n = id.size() - 1;
+            if (n == 0) {
+                id.clear();
+                k.clear();
+                return;
+            }
+            uint64_t tmp[32];
+            std::memcpy(tmp, &k[n * pk], sizeof(uint64_t) * pk);
+            const int64_t v = id[n];
+            id.pop_back();
+            k.resize(n * pk);
+            size_t i = 0;
+            while (true) {
+                const size_t c0 = 4 * i + 1;
+                if (c0 >= n) break;
+                size_t best = c0;
+                const size_t ce = c0 + 4 < n ? c0 + 4 : n;
+                for (size_t c = c0 + 1; c < ce; ++c)
+                    if (less(&k[c * pk], &k[best * pk])) best = c;
+                if (!less(&k[best * pk], tmp)) break;
+                std::memcpy(&k[i * pk], &k[best * pk], sizeof(uint64_t) * pk);
+                id[i] = id[best];
+                i = best;
+            }
+            std::memcpy(&k[i * pk], tmp, sizeof(uint64_t) * pk);
+            id[i] = v;
         }
     };
-    std::set<int64_t, Cmp>* frontier = nullptr;    // pop order (all unpopped nodes)
-    std::set<int64_t, Cmp>* unexpanded = nullptr;  // the subset not yet sent to the GPU
+    Heap frontier;    // pop order (all unpopped nodes)
+    Heap unexpanded;  // the subset not yet sent to the GPU
     // children cache: node -> offset into cache_keys (ACT * kw words), -1 = not cached
     std::vector<int64_t> cache_pos;
     bool cached(int64_t id) const { return cache_pos[id] >= 0; }
@@ -90,14 +138,8 @@ struct Engine {
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
         table.assign(1 << 12, 0);
         mask = table.size() - 1;
-        if (mode == 1) {
-            frontier = new std::set<int64_t, Cmp>(Cmp{this});
-            unexpanded = new std::set<int64_t, Cmp>(Cmp{this});
-        }
-    }
-    ~Engine() {
-        delete frontier;
-        delete unexpanded;
+        pk = (32 + 6 * L + 63) / 64;
+        frontier.pk = unexpanded.pk = pk;
     }
 
     uint64_t hash_key(const uint64_t* k) const {
@@ -153,8 +195,8 @@ struct Engine {
         const uint64_t hi = (bit & 63) > 48 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
         return ((lo | hi) & 0xffffull) == 0xffffull;
     }
-    void decode_lex(const uint64_t* k, int8_t* out) const {
-        // letters of r0 then r1 (padded), stored as value + 2 (unsigned order == numeric)
+    // the packed priority key of a node (see Heap)
+    void prio_key(const uint64_t* k, int tot, int dep, uint64_t* out) const {
         int n[2];
         {
             const int bit = 4 * L;
@@ -163,12 +205,23 @@ struct Engine {
             n[0] = (int)((lo | hi) & 0xff);
             n[1] = (int)(((lo | hi) >> 8) & 0xff);
         }
-        static const int8_t dec[4] = {1, -1, 2, -2};
+        for (int i = 0; i < pk; ++i) out[i] = 0;
+        out[0] = ((uint64_t)tot << 56) | ((uint64_t)(dep & 0xffffff) << 32);
+        static const uint64_t val[4] = {3, 1, 4, 0};  // letter + 2 for codes x, x^-1, y, y^-1
+        int pos = 32;  // next free bit, counted from the MSB of word 0
         for (int h = 0; h < 2; ++h)
-            for (int i = 0; i < L; ++i) {
+            for (int i = 0; i < L; ++i, pos += 3) {
                 const int bit = 2 * (h * L + i);
                 const int code = (int)((k[bit >> 6] >> (bit & 63)) & 3u);
-                out[h * L + i] = (int8_t)((i < n[h] ? dec[code] : 0) + 2);
+                const uint64_t v = i < n[h] ? val[code] : 2;  // padding 0 -> 2
+                // 3 bits at MSB-first position pos (may straddle two words)
+                const int w = pos >> 6, o = pos & 63;
+                if (o <= 61) {
+                    out[w] |= v << (61 - o);
+                } else {
+                    out[w] |= v >> (o - 61);
+                    out[w + 1] |= v << (64 - (o - 61));
+                }
             }
     }
     int64_t add_node(const uint64_t* k, uint64_t h, uint64_t slot, int64_t par, int act, int tot, int dep) {
@@ -179,18 +232,21 @@ struct Engine {
         total.push_back((int16_t)tot);
         depth.push_back(dep);
         cache_pos.push_back(-1);
-        if (mode == 1) {
-            lex.resize(lex.size() + 2 * L);
-            decode_lex(k, &lex[(size_t)id * 2 * L]);
-        }
         table[slot] = entry(id, h);
         ++n_set;
         if ((uint64_t)n_set * 2 > table.size()) grow();
         return id;
     }
 
+    void push_frontier(int64_t id, const uint64_t* k) {
+        uint64_t key[32];
+        prio_key(k, total[id], depth[id], key);
+        frontier.push(key, id);
+        unexpanded.push(key, id);
+    }
+
     void start(const uint64_t* k) {
-        uint64_t slot;
+        uint64_t slot = 0;
         const uint64_t h = hash_key(k);
         find(k, h, &slot);
         const int tot = key_len(k, L);
@@ -198,8 +254,7 @@ struct Engine {
         const int64_t id = add_node(k, h, slot, -1, -1, tot, 0);
         if (mode == 0) queue.push_back(id);
         else {
-            frontier->insert(id);
-            unexpanded->insert(id);
+            push_frontier(id, k);
         }
     }
 
@@ -214,9 +269,9 @@ struct Engine {
         } else {
             // the smallest unpopped nodes not expanded yet (speculative: their children are
             // cached until the node is popped in the reference's order)
-            while ((int64_t)batch.size() < cap && !unexpanded->empty()) {
-                batch.push_back(*unexpanded->begin());
-                unexpanded->erase(unexpanded->begin());
+            while ((int64_t)batch.size() < cap && !unexpanded.empty()) {
+                batch.push_back(unexpanded.top());
+                unexpanded.pop();
             }
         }
         for (size_t i = 0; i < batch.size(); ++i)
@@ -268,13 +323,12 @@ struct Engine {
                 ended = true;
                 break;
             }
-            uint64_t slot;
+            uint64_t slot = 0;
             if (find(k, hs[a], &slot) < 0) {
                 const int64_t nid = add_node(k, hs[a], slot, id, a, len, depth[id] + 1);
                 if (mode == 0) queue.push_back(nid);
                 else {
-                    frontier->insert(nid);
-                    unexpanded->insert(nid);
+                    push_frontier(nid, k);
                 }
             }
         }
@@ -302,10 +356,10 @@ struct Engine {
                 ++head;
                 if (visit(id)) break;
             } else {
-                if (frontier->empty()) { status = 2; break; }
-                const int64_t id = *frontier->begin();
+                if (frontier.empty()) { status = 2; break; }
+                const int64_t id = frontier.top();
                 if (!cached(id)) return 0;
-                frontier->erase(frontier->begin());
+                frontier.pop();
                 if (visit(id)) break;
             }
         }

@@ -27,8 +27,9 @@ for name, p in cases.items():
         t0 = time.perf_counter()
         ok, path = fn(presentation=p, max_nodes_to_explore=budget)
         dt = time.perf_counter() - t0
-        from acx.search import _engine
+        from acx.search import _device_bfs, _engine
+        stats = _device_bfs.LAST_STATS if fn is acx.bfs else _engine.LAST_STATS
         out[f"{fn.__name__}_{name}"] = {"solved": bool(ok), "path_len": len(path) if path else None,
                                        "budget": budget, "wall_s": dt, "nodes_per_s": budget / dt,
-                                       **_engine.LAST_STATS}
+                                       **{k: v for k, v in stats.items() if k != "node_keys"}}
 print(json.dumps(out, indent=1))
