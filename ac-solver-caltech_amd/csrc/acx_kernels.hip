@@ -723,7 +723,8 @@ struct StepArgs {
     int L, horizon, cyclical, hist_cap;
 };
 
-template <int NW, int LC, int VEC>
+// LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path)
+template <int NW, int LC, int VEC, bool LEARN>
 __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
     using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -738,7 +739,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     if (w.active) {
         PresRegs<NW> p;
         int act;
-        if (a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
+        if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
             const int64_t v = a.action64[env];
             act = (v >= 0 && v < 12) ? (int)v : -1;
         } else {
@@ -746,7 +747,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         }
         int cnt = a.step_count ? a.step_count[env] + 1 : 0;
         // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each
-        if (a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[env * a.hist_cap + (cnt - 1)] = (uint8_t)act;
+        if (LEARN && a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[env * a.hist_cap + (cnt - 1)] = (uint8_t)act;
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
         int e;
@@ -759,9 +760,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
-        if (a.reward_f32) a.reward_f32[env] = (float)(triv ? a.horizon * L * 2 : -(p.n0 + p.n1));
-        if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
-        if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
+        if constexpr (LEARN) {
+            if (a.reward_f32) a.reward_f32[env] = (float)(triv ? a.horizon * L * 2 : -(p.n0 + p.n1));
+            if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
+            if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
+        }
         int l0 = p.n0, l1 = p.n1;
         if ((triv || trunc) && a.reset_state && e == ACX_ERR_NONE) {
             // same-step autoreset (rare): final_obs <- post-move state, state <- reset row
@@ -782,7 +785,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     }
     wave_sync();
     tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
-    if (a.obs_f32)  // the same rows as float32, straight into the learner's buffer
+    if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, false, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane);
 }
@@ -1105,10 +1108,12 @@ static inline unsigned grid_for(int64_t rows) {
 struct StepLaunch {
     StepArgs a;
     hipStream_t s;
+    bool learn;
     template <int NW, int LC, int VEC>
     int go() {
         const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        step_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        if (learn) step_kernel<NW, LC, VEC, true><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        else step_kernel<NW, LC, VEC, false><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
 };
@@ -1175,7 +1180,7 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
     StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated,
                lengths_out, final_obs, err, err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                B, L, horizon, cyclical, 0};
-    StepLaunch f{a, (hipStream_t)stream};
+    StepLaunch f{a, (hipStream_t)stream, false};
     return dispatch(L, f);
 }
 
@@ -1191,7 +1196,7 @@ int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* actio
     StepArgs a{state, state, action, reset_state, step_count, nullptr, done, truncated, nullptr, final_obs, err,
                err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
                cyclical, hist_cap};
-    StepLaunch f{a, (hipStream_t)stream};
+    StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
 }
 

@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-step-api", action="store_true")
     ap.add_argument("--no-learner", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -236,6 +237,33 @@ def main():
                          "bytes_per_env_step": sb},
         }
         n_err = int(err_count.item())
+
+        # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
+        # the ctypes launches on the capture stream) and replayed: no per-launch host cost
+        if not args.no_graph:
+            gs = torch.cuda.Stream(device=dev)
+            gs.wait_stream(torch.cuda.current_stream(dev))
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(gs):
+                with torch.cuda.graph(graph, stream=gs):
+                    for t in range(K):
+                        step(actions[W + t])
+            torch.cuda.synchronize()
+            graph.replay()  # warm
+            torch.cuda.synchronize()
+            e0.record()
+            graph.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            s_g = e0.elapsed_time(e1) / 1e3
+            variants["step_api_hipgraph"] = {
+                "value": B * K / s_g if world == 1 else None, "unit": "env-steps/s", "ms_per_step": s_g / K * 1e3,
+                "roofline": {"bound": "hbm", "achieved": B * sb / (s_g / K) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": B * sb / (s_g / K) / 1e9 / HBM_PEAK_GBS,
+                             "bytes_per_env_step": sb},
+            }
+            del graph
+            n_err = int(err_count.item())
 
     if not args.no_learner and world == 1:
         # PPO plumbing (acx.agents.LearnerEnv): per step one acx_step_learner (int64 policy

@@ -445,3 +445,40 @@ def test_acenv_api_mirrors_reference():
         ACMove(7, np.array([0, 0, 1, 0]), 2, None)
     with pytest.raises(AssertionError):
         ACMove(0, np.array([1, 0, -1, 0]), 2, None)
+
+
+def test_step_api_under_hipgraph_capture():
+    """acx_step launches captured into a hipGraph (torch.cuda.CUDAGraph) replay to the same
+    states as eager launches: the C-ABI never allocates or synchronises."""
+    import acx
+    L, B, K = 36, 3000, 12
+    rng = np.random.default_rng(5)
+    ms = np.load(os.path.join(os.path.dirname(acx.__file__), "data", "all_presentations.npy"))
+    init = np.zeros((B, 2 * L), np.int32)
+    for i in range(B):
+        p = ms[i % len(ms)]
+        init[i, :18], init[i, L : L + 18] = p[:18], p[18:]
+    acts = torch.as_tensor(rng.integers(0, 12, size=(K, B)).astype(np.int32)).to(DEV)
+    rs = torch.as_tensor(init).to(DEV)
+
+    def run(st, cnt, rew):
+        for t in range(K):
+            acx.ops.step(st, acts[t], state_out=st, reset_state=rs, step_count=cnt, horizon=5, reward=rew[t])
+
+    st_e, cnt_e = rs.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)
+    rew_e = torch.zeros((K, B), dtype=torch.int32, device=DEV)
+    run(st_e, cnt_e, rew_e)
+    st_g, cnt_g = rs.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)
+    rew_g = torch.zeros((K, B), dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            run(st_g, cnt_g, rew_g)
+    # capture does not execute: reset and replay
+    st_g.copy_(rs)
+    cnt_g.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(st_g, st_e) and torch.equal(cnt_g, cnt_e) and torch.equal(rew_g, rew_e)
