@@ -31,6 +31,9 @@ SIGNATURES = {
     "acx_curriculum_workspace": ([_I64], ctypes.c_int64),
     "acx_curriculum_assign": ([_P, _P, _P, _I64] + [_P] * 7 + [_I64, _I32, _P], ctypes.c_int),
     "acx_rollout": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_packed_actions_words": ([_I32, _I64], ctypes.c_int64),
+    "acx_pack_actions": ([_P, _P, _I32, _I64, _P], ctypes.c_int),
+    "acx_rollout_packed": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_expand12": ([_P] * 6 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_canonicalize": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_unpack_keys": ([_P] * 3 + [_I64, _I32, _P], ctypes.c_int),

@@ -111,8 +111,15 @@ def rollout(
     trunc_traj: Optional[torch.Tensor] = None,
     err: Optional[torch.Tensor] = None,
     err_count: Optional[torch.Tensor] = None,
+    pack_actions: bool = True,
+    packed_workspace: Optional[torch.Tensor] = None,
 ) -> None:
-    """acx_rollout: T = actions.shape[0] fused env steps; state/step_count updated in place."""
+    """acx_rollout: T = actions.shape[0] fused env steps; state/step_count updated in place.
+
+    pack_actions (default): acx_pack_actions + acx_rollout_packed -- one streaming pass packs
+    the (T, B) int32 move ids 8 per word (0.5 B per env-step) into `packed_workspace`
+    ((ceil(T/8), B) int32, allocated if not given), then the rollout reads those; identical
+    results to acx_rollout (pack_actions=False)."""
     lib = _lib.load()
     _need_gpu(state, "state")
     L = _L_of(state)
@@ -129,6 +136,22 @@ def rollout(
     _check(trunc_traj, "trunc_traj", _UINT8, (T, B), dev)
     _check(err, "err", _UINT8, (B,), dev)
     _check(err_count, "err_count", _INT32, (1,), dev)
+    if pack_actions and T > 0 and B > 0:
+        words = (T + 7) // 8
+        if packed_workspace is None:
+            packed_workspace = torch.empty((words, B), dtype=_INT32, device=dev)
+        elif (packed_workspace.dtype != _INT32 or packed_workspace.device != dev or not packed_workspace.is_contiguous()
+              or packed_workspace.numel() < words * B):
+            raise ValueError(f"packed_workspace must be a contiguous int32 tensor of >= {words * B} elements on {dev}")
+        st = lib.acx_pack_actions(_ptr(actions), _ptr(packed_workspace), T, B, _stream(dev))
+        _lib.check(st, "acx_pack_actions")
+        st = lib.acx_rollout_packed(
+            _ptr(state), _ptr(packed_workspace), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj),
+            _ptr(reward_traj), _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon),
+            int(bool(cyclical)), _stream(dev),
+        )
+        _lib.check(st, "acx_rollout_packed")
+        return
     st = lib.acx_rollout(
         _ptr(state), _ptr(actions), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj),
         _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon),

@@ -70,10 +70,6 @@ __device__ __forceinline__ int4 widen4(uint32_t p) {
 
 
 constexpr int STAGE_UNROLL = 8;
-#ifndef ACX_ACT_BLOCK
-#define ACX_ACT_BLOCK 8
-#endif
-constexpr int ACT_BLOCK = ACX_ACT_BLOCK;  // steps per packed action register (4 bits each)
 // Non-temporal (streaming) stores for the rollout's write-once trajectory outputs: the
 // obs trajectory with them is 1.4 % faster (B = 2^20, L = 36, T = 200: 10.08 vs 10.22 ms,
 // tools/ab_libs.py); for reward/done/truncated they cost 0.4 %, so those stay plain.
@@ -139,16 +135,17 @@ __device__ __forceinline__ void swar_pack4(uint32_t d, uint32_t& c8, uint32_t& n
     nz4 = (u & 3u) | ((u >> 14) & 0xcu);
 }
 
-// SWAR: 8-bit code field -> 4 int8 letters, letters at index >= n_in (0..4) zeroed
-__device__ __forceinline__ uint32_t swar_unpack4(uint32_t c8, int n_in) {
-    const uint32_t b = (c8 & 3u) | ((c8 & 0xcu) << 6) | ((c8 & 0x30u) << 12) | ((c8 & 0xc0u) << 18);
-    const uint32_t b0 = b & 0x01010101u;
-    const uint32_t b1 = (b >> 1) & 0x01010101u;
-    const uint32_t m0 = b0 * 0xffu;  // 0xff in bytes of negative letters
-    const uint32_t v = (m0 & ~b1) | (~m0 & (0x01010101u + b1));
-    const uint32_t keep = n_in >= 4 ? 0xffffffffu : (n_in <= 0 ? 0u : ((1u << (8 * n_in)) - 1u));
-    return v & keep;
+// 8-bit code field -> 4 int8 letters, the first s/8 kept (s = 8m, m = 0..4), the rest zero.
+// The four 2-bit codes are spread to one per byte (two shift-or-mask rounds); a byte past m
+// gets selector bit 2 set, so one v_perm_b32 reads either the letter table {1,-1,2,-2}
+// (src1 bytes 0..3) or zero (src0 bytes 4..7).  ~7 full-rate VALU ops per 4 letters.
+__device__ __forceinline__ uint32_t codes_to_i8x4(uint32_t c8, uint32_t s) {
+    uint32_t x = (c8 | (c8 << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    const uint32_t z = (uint32_t)(0x04040404ull << s);  // 0x04 in bytes >= m (s = 32 -> none)
+    return __builtin_amdgcn_perm(0u, 0xFE02FF01u, x | z);
 }
+__device__ __forceinline__ uint32_t clamp_bits(int s) { return (uint32_t)(s < 0 ? 0 : (s > 32 ? 32 : s)); }
 
 template <int NW, int LC>
 struct FastTile {
@@ -166,6 +163,13 @@ struct FastTile {
     bool tile_bad = false;  // wave-uniform: some row of the last load was flagged
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    // per-row out-of-domain flags as of the tile's FIRST load (a later load of other rows
+    // replaced them); the fallback rows of store<true> follow these
+    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
+        flags[lane] = flagged;
+        tile_bad = __any(flagged);
+        wave_sync();
+    }
     __device__ __forceinline__ FastTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
@@ -230,6 +234,53 @@ struct FastTile {
         wave_sync();
     }
 
+    template <bool NT, bool F32, bool FULL>
+    __device__ __forceinline__ void store_flat(int4* dst, int ln, int nc) const {
+#pragma unroll
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (u0 + u < CPR && (FULL || ln + (u0 + u) * WAVE < nc)) p[u] = lds[lds_index(ln, u0 + u)];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (u0 + u < CPR && (FULL || ln + (u0 + u) * WAVE < nc))
+                    out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
+        }
+    }
+
+    // LDS -> R contiguous global rows, EXACTLY CPR store instructions on every path (a partial
+    // tile's spare lanes re-store its last chunk, same data to the same address), so the
+    // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load)
+    template <bool NT>
+    __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        int4* dst = reinterpret_cast<int4*>(g);
+        const int nc = R * CPR;
+        if (R == WAVE) {
+            store_flat<NT, false, true>(dst + ln, ln, nc);
+            return;
+        }
+#pragma unroll
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+            int cc[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                if (u0 + u >= CPR) continue;
+                const int c0 = ln + (u0 + u) * WAVE;
+                const int c = c0 < nc ? c0 : nc - 1;
+                const int r = c / CPR;
+                cc[u] = c;
+                p[u] = lds[r * S + (c - r * CPR)];
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (u0 + u < CPR) out16<NT, false>(dst + cc[u], widen4(p[u]));
+        }
+    }
+
     // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from fallback
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
@@ -238,18 +289,11 @@ struct FastTile {
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
         if (gpitch == twoL && !(FB && tile_bad)) {
-            // contiguous rows, nothing flagged: chunk c goes to g + 4c (immediate offsets)
+            // contiguous rows, nothing flagged: chunk c goes to g + 4c (immediate offsets); a
+            // full tile (wave-uniform) needs no per-chunk guards
             int4* dst = reinterpret_cast<int4*>(g) + ln;
-#pragma unroll
-            for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
-                uint32_t p[STAGE_UNROLL];
-#pragma unroll
-                for (int u = 0; u < STAGE_UNROLL; ++u)
-                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
-#pragma unroll
-                for (int u = 0; u < STAGE_UNROLL; ++u)
-                    if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
-            }
+            if (R == WAVE) store_flat<NT, F32, true>(dst, ln, nc);
+            else store_flat<NT, F32, false>(dst, ln, nc);
             return;
         }
 #pragma unroll
@@ -318,9 +362,10 @@ struct FastTile {
         for (int h = 0; h < 2; ++h) {
             const Word<NW>& w = h ? p.w1 : p.w0;
             const int n = h ? p.n1 : p.n0;
+            const int n8 = 8 * n;
 #pragma unroll
             for (int k = 0; k < HALF; ++k)
-                d[h * HALF + k] = swar_unpack4((w.w[k >> 2] >> (8 * (k & 3))) & 0xffu, n - 4 * k);
+                d[h * HALF + k] = codes_to_i8x4((w.w[k >> 2] >> (8 * (k & 3))) & 0xffu, clamp_bits(n8 - 32 * k));
         }
 #pragma unroll
         for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
@@ -349,6 +394,11 @@ struct CodeTile {
     bool tile_bad = false;
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
+        flags[lane] = flagged;
+        tile_bad = __any(flagged);
+        wave_sync();
+    }
     __device__ __forceinline__ CodeTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
@@ -397,6 +447,31 @@ struct CodeTile {
         wave_sync();
     }
 
+    // LDS -> R contiguous global rows, exactly CPR store instructions on every path (see
+    // FastTile::store_rows)
+    template <bool NT>
+    __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        int4* dst = reinterpret_cast<int4*>(g);
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+            int cc[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                const int c0 = ln + (u0 + u) * WAVE;
+                cc[u] = c0 < nc ? c0 : nc - 1;
+                p[u] = get(cc[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                const uint32_t nz4 = (p[u] >> 8) & 0xfu;
+                out16<NT, false>(dst + cc[u], widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
+            }
+        }
+    }
+
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
                                           int64_t fpitch, int lane) const {
@@ -419,7 +494,7 @@ struct CodeTile {
                     out16<false, F32>(dst, *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos));
                 } else {
                     const uint32_t nz4 = (p[u] >> 8) & 0xfu;
-                    out16<NT, F32>(dst, widen4(swar_unpack4(p[u] & 0xffu, __builtin_popcount(nz4))));
+                    out16<NT, F32>(dst, widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
                 }
             }
         }
@@ -503,6 +578,15 @@ struct GenericTile {
         flags = reinterpret_cast<uint8_t*>(b + WAVE * rowb);
     }
     __device__ __forceinline__ int Lr() const { return L; }
+    // contiguous rows
+    template <bool NT>
+    __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
+        store<false, NT>(g, 2 * L, R, nullptr, 0, lane);
+    }
+    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
+        flags[lane] = flagged;
+        wave_sync();
+    }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(base + r * rowb); }
 
     // (row, pos) of a chunk of VEC int32; chunks never straddle rows (2L % VEC == 0)
@@ -688,7 +772,8 @@ struct WaveCtx {
 };
 __device__ __forceinline__ bool wave_ctx(int64_t rows, WaveCtx& w) {
     w.lane = threadIdx.x & (WAVE - 1);
-    w.wid = threadIdx.x / WAVE;
+    // wave-uniform (SGPR): the tile base, its row count and the addresses derived from them
+    w.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     w.r0 = ((int64_t)blockIdx.x * WPB + w.wid) * WAVE;
     if (w.r0 >= rows) return false;
     w.R = (int)((rows - w.r0) < WAVE ? (rows - w.r0) : WAVE);
@@ -793,6 +878,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 struct RolloutArgs {
     int32_t* state;
     const int32_t* actions;
+    const uint32_t* packed;  // or: move ids pre-packed by pack_actions_kernel (actions unused)
     const int32_t* reset_state;
     int32_t* step_count;
     int32_t* obs_traj;
@@ -805,7 +891,7 @@ struct RolloutArgs {
     int T, L, horizon, cyclical;
 };
 
-template <int NW, int LC, int VEC>
+template <int NW, int LC, int VEC, bool OBS>
 __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_kernel(RolloutArgs a) {
     using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -815,51 +901,45 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
 
-    // the reset (starting) state stays packed in registers for the whole rollout
-    PresRegs<NW> rs;
+    // starting states: validated here, re-read (coalesced, through the tile) only when an
+    // episode of the tile ends -- not kept in registers, which are the rollout's occupancy
+    // limit (one reload per horizon per tile)
     bool bad = false;
-    tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
-    if (w.active) bad = tile.pack(w.lane, rs);
-    wave_sync();
+    {
+        PresRegs<NW> rs;
+        tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+        if (w.active) bad = tile.pack(w.lane, rs);
+        wave_sync();
+    }
     PresRegs<NW> p;
     tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
     int cnt = 0;
     const bool cyc = a.cyclical != 0;
-    bool clean = false, rs_clean = false;
+    bool clean = false;
     if (w.active) {
         bad |= tile.pack(w.lane, p);
         cnt = a.step_count[env];
         if (bad) first_err = ACX_ERR_DOMAIN;
         clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
-        rs_clean = is_clean<NW>(rs.w0, rs.n0, rs.w1, rs.n1, cyc);
     }
     const int32_t max_reward = a.horizon * L * 2;
     // Drain the prologue's loads here: otherwise the waitcnt pass carries the pending
     // step_count load around the loop back-edge and waits vmcnt(0) (= for every store of
     // the previous step) at each use of `cnt`.
     __builtin_amdgcn_s_waitcnt(0);
-    // move ids of ACT_BLOCK consecutive steps packed 4 bits each into one register: one
-    // vector-memory wait per ACT_BLOCK steps instead of one per step (a wait for a load
-    // also waits for every store issued before it, i.e. the previous step's trajectory)
-    uint32_t acts = 0;
-    for (int t = 0; t < a.T; ++t) {
+    const int32_t* act_tile = a.actions + w.r0;  // wave-uniform
+
+    // One env step of the wave: move, reward/done/truncated, autoreset, obs rows.
+    auto step = [&](int t, uint32_t id) {
         const int64_t ti = (int64_t)t * a.B;
-        if ((t & (ACT_BLOCK - 1)) == 0 && w.active) {
-            int32_t v[ACT_BLOCK];
-#pragma unroll
-            for (int k = 0; k < ACT_BLOCK; ++k)
-                v[k] = (t + k < a.T) ? a.actions[(int64_t)(t + k) * a.B + env] : 0;
-            acts = 0;
-#pragma unroll
-            for (int k = 0; k < ACT_BLOCK; ++k) {
-                // ids outside [0,12) -> 15 (ACX_ERR_ACTION in ac_move)
-                const uint32_t id = (uint32_t)v[k] < 12u ? (uint32_t)v[k] : 15u;
-                acts |= id << (4 * k);
-            }
-        }
+        // opaque per step: keeps uniform-base + lane addressing in the loop (hoisted 64-bit
+        // per-lane pointers are what the register allocator spills)
+        int ln = w.lane;
+        asm volatile("" : "+v"(ln));
+        bool reset = false;
         if (w.active) {
-            const int act = (int)((acts >> (4 * (t & (ACT_BLOCK - 1)))) & 15u);
+            const int act = (int)id;
             int e;
             if (bad) e = ACX_ERR_DOMAIN;
             else if (clean) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
@@ -869,21 +949,71 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
             ++cnt;
             const bool trunc = cnt >= a.horizon;
-            if (a.reward_traj) st_scalar<ACX_NT_SCALARS != 0, int32_t>(a.reward_traj + ti + env, triv ? max_reward : -(p.n0 + p.n1));
-            if (a.done_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.done_traj + ti + env, (uint8_t)triv);
-            if (a.trunc_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.trunc_traj + ti + env, (uint8_t)trunc);
-            if ((triv || trunc) && !bad) {
-                p = rs;
-                clean = rs_clean;
-                cnt = 0;
+            if (a.reward_traj) st_scalar<ACX_NT_SCALARS != 0, int32_t>(a.reward_traj + ti + w.r0 + ln, triv ? max_reward : -(p.n0 + p.n1));
+            if (a.done_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.done_traj + ti + w.r0 + ln, (uint8_t)triv);
+            if (a.trunc_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.trunc_traj + ti + w.r0 + ln, (uint8_t)trunc);
+            reset = (triv || trunc) && !bad;
+            if (reset) cnt = 0;
+        }
+        if (__any(reset)) {  // same-step autoreset: the tile's starting states, coalesced
+            tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+            if (reset) {
+                tile.pack(w.lane, p);
+                clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
             }
-            if (a.obs_traj && !bad) tile.unpack(w.lane, p);
-        }
-        if (a.obs_traj) {
-            wave_sync();
-            tile.template store<false, ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, twoL, w.R, nullptr, 0, w.lane);
             wave_sync();
         }
+        if constexpr (OBS) {
+            if (w.active && !bad) tile.unpack(w.lane, p);
+            wave_sync();
+            tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
+            wave_sync();
+        }
+    };
+    // ids outside [0,12) -> 15 (ACX_ERR_ACTION in ac_move)
+    auto decode = [](int32_t v) { return (uint32_t)v < 12u ? (uint32_t)v : 15u; };
+
+    // Move ids are loaded ACT_BLOCK steps at a time and kept packed, 4 bits each, in
+    // ACT_BLOCK/8 registers.  The wait for a load issued after trajectory stores covers those
+    // stores too (loads and stores pending on vmcnt may complete out of order, so the
+    // compiler waits vmcnt(0)): a drain of the wave's write queue.  8-step batches cost 8 %
+    // of the rollout in drains (tools/store_pattern.py, ACT8 vs none); with obs stores the
+    // batch is 32 steps, loaded as four groups of 8 (only the first wait finds stores).
+    constexpr int ACT_BLOCK = OBS ? 32 : 8;
+    constexpr int ACT_GROUP = 8;
+    constexpr int QW = ACT_BLOCK / 8;
+    uint32_t q[QW];
+#pragma unroll
+    for (int k = 0; k < QW; ++k) q[k] = 0;
+    for (int t = 0; t < a.T; ++t) {
+        if ((t & (ACT_BLOCK - 1)) == 0) {
+            // recomputed (v_mbcnt), not kept live across the loop
+            int lc = (int)__lane_id();
+            lc = lc < w.R ? lc : 0;
+            if (a.packed) {  // one uint32 per 8 steps (acx_pack_actions)
+                const uint32_t* pk = a.packed + (int64_t)(t >> 3) * a.B + w.r0;
+#pragma unroll
+                for (int g = 0; g < QW; ++g) q[g] = t + 8 * g < a.T ? (pk + (int64_t)g * a.B)[lc] : 0u;
+            } else {
+#pragma unroll
+            for (int g = 0; g < ACT_BLOCK / ACT_GROUP; ++g) {
+                int32_t v[ACT_GROUP];
+#pragma unroll
+                for (int k = 0; k < ACT_GROUP; ++k) {
+                    const int tk = t + g * ACT_GROUP + k;
+                    v[k] = tk < a.T ? (act_tile + (int64_t)tk * a.B)[lc] : 0;
+                }
+                uint32_t qg = 0;
+#pragma unroll
+                for (int k = 0; k < ACT_GROUP; ++k) qg |= decode(v[k]) << (4 * k);
+                q[g] = qg;
+            }
+            }
+        }
+        const uint32_t id = q[0] & 15u;
+#pragma unroll
+        for (int k = 0; k < QW; ++k) q[k] = (q[k] >> 4) | (k + 1 < QW ? q[k + 1] << 28 : 0u);
+        step(t, id);
     }
     if (w.active) {
         if (!bad) tile.unpack(w.lane, p);
@@ -891,9 +1021,28 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         if (a.err) a.err[env] = (uint8_t)first_err;
         if (first_err != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
-    wave_sync();
     // rows flagged out-of-domain keep their (untouched) global contents
+    tile.restore_flags(w.lane, w.active && bad);
     tile.template store<true>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL, w.lane);
+}
+
+// Move ids (T, B) int32 -> (ceil(T/8), B) uint32, 8 consecutive steps of one env per word,
+// 4 bits each (ids outside [0,12) -> 15, ACX_ERR_ACTION).  The rollout then reads 0.5 B per
+// env-step instead of 4: its action reads are small scattered requests between trajectory
+// write bursts, and at 4 B they cost 7 % of the rollout (tools/store_pattern.py ACT8 vs
+// PACK8); this pass streams them once.
+__global__ __launch_bounds__(256) void pack_actions_kernel(const int32_t* __restrict__ actions,
+                                                           uint32_t* __restrict__ packed, int T, int64_t B) {
+    const int64_t env = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int t0 = (int)blockIdx.y * 8;
+    if (env >= B) return;
+    int32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = t0 + k < T ? actions[(int64_t)(t0 + k) * B + env] : 0;
+    uint32_t q = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q |= (t0 + k < T ? ((uint32_t)v[k] < 12u ? (uint32_t)v[k] : 15u) : 0u) << (4 * k);
+    packed[(int64_t)blockIdx.y * B + env] = q;
 }
 
 
@@ -1123,7 +1272,8 @@ struct RolloutLaunch {
     template <int NW, int LC, int VEC>
     int go() {
         const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        rollout_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        if (a.obs_traj) rollout_kernel<NW, LC, VEC, true><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        else rollout_kernel<NW, LC, VEC, false><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
 };
@@ -1208,8 +1358,33 @@ int acx_rollout(int32_t* state, const int32_t* actions, const int32_t* reset_sta
     if (B == 0 || T == 0) return ACX_OK;
     if (!state || !actions || !reset_state || !step_count) return ACX_E_ARG;
     if (!aligned16(state) || !aligned16(reset_state) || (obs_traj && !aligned16(obs_traj))) return ACX_E_ARG;
-    RolloutArgs a{state, actions, reset_state, step_count, obs_traj, reward_traj, done_traj, trunc_traj,
+    RolloutArgs a{state, actions, nullptr, reset_state, step_count, obs_traj, reward_traj, done_traj, trunc_traj,
                   err, err_count, B, T, L, horizon, cyclical};
+    RolloutLaunch f{a, (hipStream_t)stream};
+    return dispatch(L, f);
+}
+
+int64_t acx_packed_actions_words(int32_t T, int64_t B) { return T <= 0 || B <= 0 ? 0 : (int64_t)((T + 7) / 8) * B; }
+
+int acx_pack_actions(const int32_t* actions, uint32_t* packed, int32_t T, int64_t B, void* stream) {
+    if (B < 0 || T < 0) return ACX_E_ARG;
+    if (B == 0 || T == 0) return ACX_OK;
+    if (!actions || !packed || (T + 7) / 8 > 65535) return ACX_E_ARG;
+    const dim3 grid((unsigned)((B + 255) / 256), (unsigned)((T + 7) / 8));
+    pack_actions_kernel<<<grid, dim3(256), 0, (hipStream_t)stream>>>(actions, packed, T, B);
+    return finish_launch();
+}
+
+int acx_rollout_packed(int32_t* state, const uint32_t* packed_actions, const int32_t* reset_state,
+                       int32_t* step_count, int32_t* obs_traj, int32_t* reward_traj, uint8_t* done_traj,
+                       uint8_t* trunc_traj, uint8_t* err, int32_t* err_count, int32_t T, int64_t B, int32_t L,
+                       int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || T < 0 || L < 1 || L > ACX_MAX_L) return ACX_E_ARG;
+    if (B == 0 || T == 0) return ACX_OK;
+    if (!state || !packed_actions || !reset_state || !step_count) return ACX_E_ARG;
+    if (!aligned16(state) || !aligned16(reset_state) || (obs_traj && !aligned16(obs_traj))) return ACX_E_ARG;
+    RolloutArgs a{state, nullptr, packed_actions, reset_state, step_count, obs_traj, reward_traj, done_traj,
+                  trunc_traj, err, err_count, B, T, L, horizon, cyclical};
     RolloutLaunch f{a, (hipStream_t)stream};
     return dispatch(L, f);
 }

@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[2]): PPO rollout collection -- 2^20 envs per GPU
 L = 36, env horizon 200, Miller-Schupp starting states (env i starts at presentation
 i mod 1190 of all_presentations.txt), uniform random move ids pre-generated on the device
 (torch.Generator, seed 0 + rank), same-step autoreset.  One bench "step" = one env step of
-the whole batch; the K timed steps are ONE acx_rollout launch that writes the full
+the whole batch; the K timed steps are acx_rollout launches of <= 200 steps (one for the
+default K = 200; a larger K reuses the same buffers, as a PPO loop does) that write the full
 (K, B, 2L) int32 observation trajectory plus reward/done/truncated per step.  Inputs are
 resident in HBM before the timed region.
 
@@ -150,7 +151,11 @@ def main():
     count = torch.zeros(B, dtype=torch.int32, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(0 + rank)
-    T_buf = max(K, W)
+    # one launch's obs trajectory is T*B*8L bytes (60.4 GB at T = 200, L = 36); a K beyond
+    # the PPO horizon chunk runs as consecutive launches of <= T_CHUNK steps that reuse the
+    # same buffers (a PPO loop reuses its rollout storage the same way)
+    T_CHUNK = max(1, min(200, (160 << 30) // max(1, B * (8 * L + 10))))
+    T_buf = min(max(K, W), T_CHUNK)
     actions = torch.randint(0, 12, (W + K, B), dtype=torch.int32, device=dev, generator=g)
     obs = torch.empty((T_buf, B, 2 * L), dtype=torch.int32, device=dev)
     rew = torch.empty((T_buf, B), dtype=torch.int32, device=dev)
@@ -164,8 +169,11 @@ def main():
         buf.zero_()
 
     def roll(a, T):
-        ops.rollout(state, a, starts, count, horizon=H, cyclical=True, obs_traj=obs[:T], reward_traj=rew[:T],
-                    done_traj=done[:T], trunc_traj=trunc[:T], err=err, err_count=err_count)
+        for t0 in range(0, T, T_buf):
+            t1 = min(T, t0 + T_buf)
+            ops.rollout(state, a[t0:t1], starts, count, horizon=H, cyclical=True, obs_traj=obs[: t1 - t0],
+                        reward_traj=rew[: t1 - t0], done_traj=done[: t1 - t0], trunc_traj=trunc[: t1 - t0],
+                        err=err, err_count=err_count)
 
     # warmup (W env steps, untimed)
     if W > 0:
@@ -197,7 +205,8 @@ def main():
     # + obs 8L B + reward 4 + done 1 + truncated 1; per env per launch state in/out 2*8L,
     # reset state 8L, step count in/out 8, err 1
     step_bytes = 4 + 8 * L + 4 + 1 + 1
-    launch_bytes = K * B * step_bytes + B * (24 * L + 8 + 1)
+    n_launch = -(-K // T_buf)
+    launch_bytes = K * B * step_bytes + n_launch * B * (24 * L + 8 + 1)
     achieved = launch_bytes / kernel_s / 1e9
 
     variants = {}
@@ -332,7 +341,7 @@ def main():
         "config": {
             "workload": (f"PPO rollout collection (BASELINE configs[2]): {B} envs/GPU, L={L}, horizon {H}, "
                          "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
-                         "one acx_rollout launch of K steps"),
+                         f"acx_rollout launches of <= {T_buf} steps ({n_launch} for K={K})"),
             "global_batch": world * B,
             "envs_per_gpu": B,
             "max_relator_length": L,
@@ -350,6 +359,7 @@ def main():
             "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
+            "launches": n_launch,
             "kernel_ms": kernel_s * 1e3,
             "host_launch_ms": t_launch * 1e3,
         },

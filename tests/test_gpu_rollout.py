@@ -1,0 +1,103 @@
+"""GPU: the rollout's two action paths (int32 ids read in the kernel, acx_rollout; ids
+pre-packed 8 per word, acx_pack_actions + acx_rollout_packed) give identical trajectories,
+states, step counts and error flags -- including ids outside [0,12), T not a multiple of 8,
+partial 64-env tiles and every tile type (L = 36 FastTile, 128 CodeTile, 17 generic) -- and
+both equal the oracle env replay."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _starts(L, B, seed=0):
+    import acx
+    import os
+    ms = np.load(os.path.join(os.path.dirname(acx.__file__), "data", "all_presentations.npy"))
+    rng = np.random.default_rng(seed)
+    out = np.zeros((B, 2 * L), np.int32)
+    for i in range(B):
+        p = ms[rng.integers(len(ms))]
+        a, b = p[:18][p[:18] != 0], p[18:][p[18:] != 0]
+        a, b = a[:L], b[:L]
+        out[i, : len(a)] = a
+        out[i, L : L + len(b)] = b
+    return out
+
+
+def _roll(starts, acts, L, H, cyc, pack):
+    from acx import ops
+    T, B = acts.shape
+    st = torch.as_tensor(starts).to(DEV)
+    rs = st.clone()
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    obs = torch.full((T, B, 2 * L), -7, dtype=torch.int32, device=DEV)
+    rew = torch.zeros((T, B), dtype=torch.int32, device=DEV)
+    dn = torch.zeros((T, B), dtype=torch.uint8, device=DEV)
+    tr = torch.zeros((T, B), dtype=torch.uint8, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    ec = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.rollout(st, torch.as_tensor(acts).to(DEV), rs, cnt, horizon=H, cyclical=cyc, obs_traj=obs, reward_traj=rew,
+                done_traj=dn, trunc_traj=tr, err=err, err_count=ec, pack_actions=pack)
+    return [x.cpu().numpy() for x in (st, cnt, obs, rew, dn, tr, err, ec)]
+
+
+@pytest.mark.parametrize("L,B,T", [(36, 1000, 13), (36, 4096, 40), (128, 200, 21), (17, 333, 9), (36, 64, 1)])
+@pytest.mark.parametrize("cyc", [True, False])
+def test_packed_equals_unpacked_and_oracle(L, B, T, cyc):
+    rng = np.random.default_rng(L * 1000 + T)
+    starts = _starts(L, B, seed=T)
+    acts = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    a = _roll(starts, acts, L, 5, cyc, pack=False)
+    b = _roll(starts, acts, L, 5, cyc, pack=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    # oracle replay of the same episode stream (same-step autoreset to the starting state)
+    st = starts.copy()
+    cnt = np.zeros(B, np.int32)
+    for t in range(T):
+        r, d, tr, e, _, _ = O.env_step(st, acts[t], L, 5, cnt, reset_state=starts, cyclical=cyc)
+        assert np.array_equal(a[2][t], st), t
+        assert np.array_equal(a[3][t], r) and np.array_equal(a[4][t], d) and np.array_equal(a[5][t], tr)
+    assert int(a[7][0]) == 0
+
+
+@pytest.mark.parametrize("L", [36, 128])
+def test_invalid_ids_same_on_both_paths(L):
+    B, T = 300, 19
+    rng = np.random.default_rng(5)
+    starts = _starts(L, B, seed=1)
+    acts = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    bad = rng.random((T, B)) < 0.02
+    acts[bad] = rng.choice(np.array([12, 15, 16, -1, 1 << 20, -(1 << 31), 255], np.int32), size=int(bad.sum()))
+    a = _roll(starts, acts, L, 7, True, pack=False)
+    b = _roll(starts, acts, L, 7, True, pack=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    hit = bad.any(0)
+    assert (a[6][hit] == 4).all() and (a[6][~hit] == 0).all()
+    assert int(a[7][0]) == int(hit.sum())
+
+
+def test_pack_actions_layout():
+    from acx import _lib
+    lib = _lib.load()
+    T, B = 21, 777
+    rng = np.random.default_rng(2)
+    acts = rng.integers(-3, 20, size=(T, B)).astype(np.int32)
+    words = (T + 7) // 8
+    assert lib.acx_packed_actions_words(T, B) == words * B
+    packed = torch.zeros((words, B), dtype=torch.int32, device=DEV)
+    a = torch.as_tensor(acts).to(DEV)
+    st = lib.acx_pack_actions(a.data_ptr(), packed.data_ptr(), T, B, torch.cuda.current_stream().cuda_stream)
+    assert st == 0
+    got = packed.cpu().numpy().view(np.uint32)
+    ids = np.where((acts >= 0) & (acts < 12), acts, 15).astype(np.uint32)
+    want = np.zeros((words, B), np.uint32)
+    for t in range(T):
+        want[t // 8] |= ids[t] << np.uint32(4 * (t % 8))
+    assert np.array_equal(got, want)

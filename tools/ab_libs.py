@@ -24,6 +24,7 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--mode", default="rollout")
 ap.add_argument("--T", type=int, default=200)
+ap.add_argument("--rounds", type=int, default=1, help="fresh output allocations (the speed depends on the mapping)")
 args = ap.parse_args()
 
 libs = []
@@ -41,10 +42,6 @@ starts = torch.as_tensor(ms_starts(L, B)).to(dev)
 g = torch.Generator(device=dev)
 g.manual_seed(0)
 acts = torch.randint(0, 12, (T, B), dtype=torch.int32, device=dev, generator=g)
-obs = torch.zeros((T, B, 2 * L), dtype=torch.int32, device=dev)
-rew = torch.zeros((T, B), dtype=torch.int32, device=dev)
-dn = torch.zeros((T, B), dtype=torch.uint8, device=dev)
-tr = torch.zeros((T, B), dtype=torch.uint8, device=dev)
 lens = torch.zeros((B, 2), dtype=torch.int32, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 
@@ -70,11 +67,18 @@ def run(lib):
     return e0.elapsed_time(e1)
 
 
-for lib in libs:  # warm up each build
-    run(lib)
 times = [[] for _ in libs]
-for r in range(args.reps):
-    for i, lib in enumerate(libs):
-        times[i].append(run(lib))
-out = {os.path.basename(p): {"ms_min": min(t), "ms_median": statistics.median(t)} for p, t in zip(args.libs, times)}
+for rnd in range(args.rounds):
+    obs = torch.zeros((T, B, 2 * L), dtype=torch.int32, device=dev)
+    rew = torch.zeros((T, B), dtype=torch.int32, device=dev)
+    dn = torch.zeros((T, B), dtype=torch.uint8, device=dev)
+    tr = torch.zeros((T, B), dtype=torch.uint8, device=dev)
+    for lib in libs:  # warm up each build
+        run(lib)
+    for r in range(args.reps):
+        for i, lib in enumerate(libs):
+            times[i].append(run(lib))
+    del obs, rew, dn, tr
+    torch.cuda.empty_cache()
+out = {os.path.basename(p): {"ms_min": min(t), "ms_median": statistics.median(t), "all": [round(x, 2) for x in t]} for p, t in zip(args.libs, times)}
 print(json.dumps(out))

@@ -1,29 +1,92 @@
-// Store-pattern microbenchmark: how fast can the rollout's obs-trajectory write pattern go
-// with no compute?  Each wave owns a 64-row tile (18 KB at L=36) and, per step t, writes it
-// to obs[t] as 18 coalesced 1 KB wave-stores -- exactly the acx_rollout pattern.  Compared
-// with the same bytes written linearly (grid-stride, like a fill).
+// Store-pattern microbenchmark: how fast can the rollout's HBM access pattern go with no
+// move compute?  Each wave owns a 64-row tile (18 KB at L=36) and, per step t, writes it to
+// obs[t] as 18 coalesced 1 KB wave-stores -- exactly the acx_rollout obs pattern.  Feature
+// bits add the rollout's other traffic one at a time, to find what costs bandwidth:
+//   F_NT      non-temporal obs stores
+//   F_SCAL    per-step reward (int32) / done / truncated (u8) stores
+//   F_ACT8    per-lane int32 action loads, ACT_BLOCK = 8 steps per load batch (waits vmcnt)
+//   F_ACTPF   the same loads, issued one batch ahead (prefetch; consumed 8 steps later)
+//   F_LDS     obs rows staged through LDS (write 18 dwords per lane, read back per chunk)
+//   F_ACT32   action loads in 32-step batches (4 groups of 8; one drain per 32 steps)
+//   F_PACK8   pre-packed actions: one uint32 (8 ids x 4 bits) per lane per 8 steps
+// Compared with the same bytes written linearly (grid-stride, like a fill).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-template <bool NT>
-__global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int64_t B, int T, int row_chunks) {
+enum { F_NT = 1, F_SCAL = 2, F_ACT8 = 4, F_ACTPF = 8, F_LDS = 16, F_ACT32 = 32, F_PACK8 = 64 };
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+template <int F>
+__global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, uint8_t* dn, uint8_t* tr,
+                                                       const int32_t* act, int64_t B, int T, int row_chunks) {
+    __shared__ uint32_t lds[4][64 * 18];
     const int lane = threadIdx.x & 63;
-    const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wid = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * 4 + wid;
     if (tile * 64 >= B) return;
     const int64_t chunks_per_step = B * row_chunks;
+    const int64_t env = tile * 64 + lane;
     int4 v = make_int4(lane, 1, 2, 3);
+    uint32_t acc = 0, acts = 0;
+    int32_t nv[8];  // prefetched raw action loads of the next batch (consumed 8 steps later)
+    if (F & F_ACTPF) {
+        for (int k = 0; k < 8; ++k) nv[k] = act[(int64_t)k * B + env];
+    }
     for (int t = 0; t < T; ++t) {
-        int4* dst = obs + t * chunks_per_step + tile * 64 * row_chunks + lane;
-        for (int u = 0; u < row_chunks; ++u) {
-            if (NT) {
-                typedef int v4i __attribute__((ext_vector_type(4)));
-                v4i x = {v.x, v.y, v.z, v.w};
-                __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(dst + u * 64));
+        if ((F & (F_ACT8 | F_ACTPF)) && (t & 7) == 0) {
+            if (F & F_ACTPF) {
+                acts = 0;
+                for (int k = 0; k < 8; ++k) acts |= (uint32_t)nv[k] << (4 * k);
+                for (int k = 0; k < 8; ++k) {
+                    const int tt = t + 8 + k < T ? t + 8 + k : T - 1;
+                    nv[k] = act[(int64_t)tt * B + env];
+                }
             } else {
-                dst[u * 64] = v;
+                acts = 0;
+                for (int k = 0; k < 8; ++k)
+                    acts |= (t + k < T) ? (uint32_t)act[(int64_t)(t + k) * B + env] << (4 * k) : 0u;
             }
         }
-        v.y += 1;
+        if ((F & F_ACT32) && (t & 31) == 0) {
+            for (int g = 0; g < 4; ++g) {
+                int32_t v8[8];
+                for (int k = 0; k < 8; ++k) v8[k] = (t + 8 * g + k < T) ? act[(int64_t)(t + 8 * g + k) * B + env] : 0;
+                uint32_t qg = 0;
+                for (int k = 0; k < 8; ++k) qg |= (uint32_t)v8[k] << (4 * k);
+                acc += qg;
+            }
+        }
+        if ((F & F_PACK8) && (t & 7) == 0) acts = (uint32_t)act[(int64_t)(t >> 3) * B + env];
+        if (F & (F_ACT8 | F_ACTPF | F_PACK8)) acc += (acts >> (4 * (t & 7))) & 15u;
+        v.y += 1 + (int)acc;
+        if (F & F_SCAL) {
+            rew[(int64_t)t * B + env] = v.y;
+            dn[(int64_t)t * B + env] = (uint8_t)v.y;
+            tr[(int64_t)t * B + env] = (uint8_t)(v.y >> 8);
+        }
+        int4* dst = obs + t * chunks_per_step + tile * 64 * row_chunks + lane;
+        if (F & F_LDS) {
+            uint32_t* row = &lds[wid][lane * 18];
+            for (int k = 0; k < 18; k += 2) *reinterpret_cast<uint2*>(row + k) = make_uint2(v.y + k, v.x + k);
+            __builtin_amdgcn_wave_barrier();
+            for (int u = 0; u < row_chunks; ++u) {
+                const uint32_t p = lds[wid][lane + 64 * u];
+                const v4i x = {(int)(p & 0xff), (int)((p >> 8) & 0xff), (int)((p >> 16) & 0xff), (int)(p >> 24)};
+                if (F & F_NT) __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(dst + u * 64));
+                else *reinterpret_cast<v4i*>(dst + u * 64) = x;
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            for (int u = 0; u < row_chunks; ++u) {
+                if (F & F_NT) {
+                    v4i x = {v.x, v.y, v.z, v.w};
+                    __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(dst + u * 64));
+                } else {
+                    dst[u * 64] = v;
+                }
+            }
+        }
     }
 }
 
@@ -32,10 +95,19 @@ __global__ __launch_bounds__(256) void linear_fill(int4* p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
 }
 
-extern "C" int sp_tile(void* obs, int64_t B, int T, int row_chunks, int nt, void* stream) {
+#define CASE(f)                                                                                    \
+    case f:                                                                                        \
+        tile_pattern<f><<<grid, 256, 0, (hipStream_t)stream>>>((int4*)obs, (int32_t*)rew, (uint8_t*)dn, \
+                                                              (uint8_t*)tr, (const int32_t*)act, B, T, row_chunks); \
+        break;
+
+extern "C" int sp_tile(void* obs, void* rew, void* dn, void* tr, const void* act, int64_t B, int T, int row_chunks,
+                       int flags, void* stream) {
     dim3 grid((unsigned)((B + 255) / 256));
-    if (nt) tile_pattern<true><<<grid, 256, 0, (hipStream_t)stream>>>((int4*)obs, B, T, row_chunks);
-    else tile_pattern<false><<<grid, 256, 0, (hipStream_t)stream>>>((int4*)obs, B, T, row_chunks);
+    switch (flags) {
+        CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83)
+        default: return -1;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 extern "C" int sp_linear(void* p, int64_t n16, int blocks, void* stream) {
