@@ -3,14 +3,14 @@
 The reference steps a gymnasium SyncVectorEnv on the host each step (`envs.step(action.cpu()
 .numpy())`, training.py:238-240), copies obs/reward/done back to the device (:241, :354-356)
 and runs a Python loop over the envs for episode bookkeeping and the start-state curriculum
-(:262-352).  LearnerEnv keeps all of it on the GPU, one acx_step_learner + one
-acx_curriculum_assign launch per step:
+(:262-352).  LearnerEnv keeps all of it on the GPU, one acx_learner_step call (a step kernel
+and one curriculum pass) per step:
 
   * the policy's int64 actions go straight in;
   * the next observation is written as float32 into whatever (B, 2L) buffer the caller names
     (e.g. obs[t + 1] of the learner's (T, B, 2L) buffer), rewards[t] and next_done likewise;
-  * each env's current episode moves are kept in a (B, hist_cap) byte buffer, so info["actions"]
-    of a solved episode (training.py:275-280) is one row read;
+  * each env's current episode moves are kept in a (hist_cap, B) byte buffer, so info["actions"]
+    of a solved episode (training.py:275-280) is one column read;
   * the round-1 curriculum (training.py:319-336, 349-352) runs on the device: finished envs
     take the next unprocessed initial state in env order.  Once every initial state has been
     used the reference draws random solved/unsolved states with Python `random` (:337-346);
@@ -48,7 +48,8 @@ class LearnerEnv:
         self.next_index = torch.tensor([num_envs], dtype=torch.int32, device=dev)  # max(states_processed) + 1
         self.needs_host = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self.hist_cap = int(hist_cap if hist_cap is not None else horizon_length)
-        self.action_hist = torch.zeros((num_envs, self.hist_cap), dtype=torch.uint8, device=dev)
+        # move k of env i at [k, i] (step-major: coalesced writes, acx.h)
+        self.action_hist = torch.zeros((self.hist_cap, num_envs), dtype=torch.uint8, device=dev)
         self.episode_len = torch.zeros(num_envs, dtype=torch.int32, device=dev)
         self.done = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
@@ -67,16 +68,18 @@ class LearnerEnv:
         return o
 
     def step(self, action: torch.Tensor, obs_out: Optional[torch.Tensor] = None,
-             reward_out: Optional[torch.Tensor] = None, done_out: Optional[torch.Tensor] = None):
+             reward_out: Optional[torch.Tensor] = None, done_out: Optional[torch.Tensor] = None,
+             fused: bool = True):
         """One env step for all envs.  action: (B,) int64 (policy samples) or int32 device tensor.
         obs_out / reward_out / done_out: float32 (B, 2L) / (B,) / (B,) device views to fill
         (next_obs, rewards[t], next_done).  Returns (done, truncated, episode_len, needs_host)
-        uint8/int32 device tensors; no host synchronisation."""
+        uint8/int32 device tensors; no host synchronisation.  fused (default): one
+        acx_learner_step call (2 launches); else acx_step_learner + acx_curriculum_assign."""
         lib = _lib.load()
         B, L, dev = self.num_envs, self.L, self.device
         for name, t, shape in (("obs_out", obs_out, (B, 2 * L)), ("reward_out", reward_out, (B,)),
                                ("done_out", done_out, (B,))):
-            if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != shape or t.device != dev
+            if t is not None and (t.dtype != torch.float32 or t.shape != shape or t.device != dev
                                   or not t.is_contiguous()):
                 raise ValueError(f"{name} must be a contiguous float32 {shape} tensor on {dev}")
         if action.device != dev or action.shape != (B,) or not action.is_contiguous():
@@ -88,6 +91,16 @@ class LearnerEnv:
         v = self.vec
         stream = torch.cuda.current_stream(dev).cuda_stream
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        if fused:
+            st = lib.acx_learner_step(
+                v.state.data_ptr(), ptr(a32), ptr(a64), v.reset_state.data_ptr(), v.step_count.data_ptr(),
+                ptr(obs_out), ptr(reward_out), ptr(done_out), self.done.data_ptr(), self.truncated.data_ptr(),
+                self.action_hist.data_ptr(), self.hist_cap, self.episode_len.data_ptr(), v.err.data_ptr(),
+                v.err_count.data_ptr(), self.initial_states.data_ptr(), self.n_states, self.next_index.data_ptr(),
+                self.curr_index.data_ptr(), self.needs_host.data_ptr(), self._ws.data_ptr(), B, L,
+                self.horizon_length, int(v.cyclical), stream)
+            _lib.check(st, "acx_learner_step")
+            return self.done, self.truncated, self.episode_len, self.needs_host
         st = lib.acx_step_learner(
             v.state.data_ptr(), ptr(a32), ptr(a64), v.reset_state.data_ptr(), v.step_count.data_ptr(), ptr(obs_out),
             ptr(reward_out), ptr(done_out), self.done.data_ptr(), self.truncated.data_ptr(),
@@ -106,7 +119,7 @@ class LearnerEnv:
         n = int(self.episode_len[i].item())
         if n > self.hist_cap:
             raise ValueError(f"episode of {n} moves exceeds hist_cap {self.hist_cap}")
-        return [int(x) for x in self.action_hist[i, :n].cpu().numpy()]
+        return [int(x) for x in self.action_hist[:n, i].cpu().numpy()]
 
     def place(self, i: int, state_index: int, obs_out: Optional[torch.Tensor] = None) -> None:
         """Host placement of env i (after round 1, training.py:337-352): start from

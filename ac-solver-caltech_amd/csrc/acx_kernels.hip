@@ -95,12 +95,10 @@ __device__ __forceinline__ void st16(int4* p, const int4& v) {
 template <bool NT, bool F32>
 __device__ __forceinline__ void out16(int4* p, const int4& v) {
     if constexpr (F32) {
-        float4 f;
-        f.x = (float)v.x;
-        f.y = (float)v.y;
-        f.z = (float)v.z;
-        f.w = (float)v.w;
-        *reinterpret_cast<float4*>(p) = f;
+        typedef float v4f_t __attribute__((ext_vector_type(4)));
+        const v4f_t f = {(float)v.x, (float)v.y, (float)v.z, (float)v.w};
+        if constexpr (NT) __builtin_nontemporal_store(f, reinterpret_cast<v4f_t*>(p));
+        else *reinterpret_cast<v4f_t*>(p) = f;
     } else {
         st16<NT>(p, v);
     }
@@ -806,6 +804,11 @@ struct StepArgs {
     int32_t* episode_len;
     int64_t B;
     int L, horizon, cyclical, hist_cap;
+    // acx_learner_step: finished-env count per 64-env wave (bytes) for the fused curriculum
+    // pass, and the curriculum's next_index copied to next_base before that pass advances it
+    uint8_t* fin_wave;
+    const int32_t* next_index;
+    int32_t* next_base;
 };
 
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path)
@@ -821,6 +824,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 
     tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
 
+    bool fin = false;  // done | truncated (the curriculum's "finished")
     if (w.active) {
         PresRegs<NW> p;
         int act;
@@ -831,8 +835,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             act = a.action[env];
         }
         int cnt = a.step_count ? a.step_count[env] + 1 : 0;
-        // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each
-        if (LEARN && a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[env * a.hist_cap + (cnt - 1)] = (uint8_t)act;
+        // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
+        // at [k][i] -- envs at the same episode position write one coalesced row segment (an
+        // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
+        if (LEARN && a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
         int e;
@@ -845,6 +851,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
+        fin = triv || trunc;
         if constexpr (LEARN) {
             if (a.reward_f32) a.reward_f32[env] = (float)(triv ? a.horizon * L * 2 : -(p.n0 + p.n1));
             if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
@@ -868,10 +875,17 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         if (a.err) a.err[env] = (uint8_t)e;
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
+    if constexpr (LEARN) {
+        if (a.fin_wave) {
+            const uint64_t m = __ballot(fin);
+            if (w.lane == 0) a.fin_wave[w.r0 >> 6] = (uint8_t)__popcll(m);
+            if (w.r0 == 0 && w.lane == 0) *a.next_base = *a.next_index;
+        }
+    }
     wave_sync();
     tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
-        tile.template store<true, false, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
+        tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane);
 }
 
@@ -1348,6 +1362,37 @@ int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* actio
                cyclical, hist_cap};
     StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
+}
+
+// acx_curriculum.hip (not in the public header)
+int acx_internal_curriculum_fused(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
+                                  int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
+                                  int32_t* state, int32_t* reset_state, float* obs_f32, int32_t* workspace, int64_t B,
+                                  int32_t L, void* stream);
+
+int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
+                     int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                     int32_t* err_count, const int32_t* curriculum_states, int64_t n_states, int32_t* next_index,
+                     int32_t* curr_index, uint8_t* needs_host, int32_t* workspace, int64_t B, int32_t L,
+                     int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || n_states < 0 || n_states > INT32_MAX) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state || !step_count || (!action == !action_i64) || (action_hist && hist_cap == 0)) return ACX_E_ARG;
+    if (!done || !truncated || !reset_state || !curriculum_states || !next_index || !curr_index || !needs_host ||
+        !workspace)
+        return ACX_E_ARG;
+    if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
+    // workspace = acx_curriculum_workspace(B) words: [0] next_index before the step, [2..] one
+    // finished-count byte per 64-env wave (4 per 256-env block dword)
+    StepArgs a{state, state, action, reset_state, step_count, nullptr, done, truncated, nullptr, nullptr, err,
+               err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
+               cyclical, hist_cap, reinterpret_cast<uint8_t*>(workspace + 2), next_index, workspace};
+    StepLaunch f{a, (hipStream_t)stream, true};
+    const int st = dispatch(L, f);
+    if (st != ACX_OK) return st;
+    return acx_internal_curriculum_fused(done, truncated, curriculum_states, n_states, next_index, curr_index,
+                                         needs_host, state, reset_state, obs_f32, workspace, B, L, stream);
 }
 
 int acx_rollout(int32_t* state, const int32_t* actions, const int32_t* reset_state, int32_t* step_count,

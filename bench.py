@@ -356,7 +356,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>",
+            "kernel": f"acx::pack_actions_kernel + acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,true>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
             "launches": n_launch,

@@ -91,8 +91,10 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
  *   reward_f32  (B) float32 or NULL (rewards[t], training.py:241-253).
  *   done_f32    (B) float32 or NULL: done only, as next_done = torch.Tensor(done) (:354-356).
  *   done, truncated (B) uint8 or NULL.
- *   action_hist (B, hist_cap) uint8 or NULL: the moves of each env's current episode, move k
- *               at [env, k] (ACEnv.actions / info["actions"], ac_env.py:96,105; training.py:275-280).
+ *   action_hist (hist_cap, B) uint8 or NULL: the moves of each env's current episode, move k
+ *               of env i at [k, i] (ACEnv.actions / info["actions"], ac_env.py:96,105;
+ *               training.py:275-280); step-major so envs at the same episode position write
+ *               one coalesced segment.
  *   episode_len (B) int32 or NULL: the length of the episode that ended this step, else 0.
  *   step_count is required (truncation, history position).
  */
@@ -116,6 +118,20 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
                           int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
                           int32_t* state, int32_t* reset_state, float* obs_f32, int32_t* workspace, int64_t B,
                           int32_t L, void* stream);
+
+/*
+ * One PPO env step = acx_step_learner (final_obs NULL) followed by acx_curriculum_assign, in
+ * two launches instead of four: the step kernel also writes each 64-env wave's finished
+ * count, from which the curriculum pass ranks the finished envs directly.  Same results as
+ * the two calls; done, truncated, reset_state and the curriculum arguments are required;
+ * workspace = acx_curriculum_workspace(B) int32 words.
+ */
+int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
+                     int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                     int32_t* err_count, const int32_t* curriculum_states, int64_t n_states, int32_t* next_index,
+                     int32_t* curr_index, uint8_t* needs_host, int32_t* workspace, int64_t B, int32_t L,
+                     int32_t horizon, int32_t cyclical, void* stream);
 
 /*
  * T fused env steps (PPO rollout collection).  state (B,2L) and step_count (B) are

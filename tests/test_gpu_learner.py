@@ -64,6 +64,44 @@ def test_learner_env_matches_training_loop_restatement(L, B, N, H, T, adtype):
     assert n_host > 0 or N - B > T * B  # round 1 completed in the long cases
 
 
+@pytest.mark.parametrize("L,B,N,H", [(36, 5000, 9000, 6), (36, 4096, 4200, 3), (128, 300, 700, 4), (18, 65, 90, 2)])
+def test_fused_learner_step_equals_two_calls(L, B, N, H):
+    """acx_learner_step (step kernel + one curriculum pass from per-wave counts) gives the same
+    state, outputs, curriculum indices and host flags as acx_step_learner + acx_curriculum_assign,
+    across round-1 completion (full tiles, partial last tile and block, several L)."""
+    from acx.agents import LearnerEnv
+    init = _ms_states(L, N)
+    init[3] = 0
+    init[3, 0], init[3, L], init[3, L + 1] = 1, 2, 1  # solves in one move: done events
+    ea = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    eb = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    T = 3 * H + 2 * (N - B) // max(1, B // H) + 4
+    g = torch.Generator(device=DEV)
+    g.manual_seed(L + B)
+    outs = [[torch.empty((B, 2 * L), dtype=torch.float32, device=DEV), torch.empty(B, dtype=torch.float32, device=DEV),
+             torch.empty(B, dtype=torch.float32, device=DEV)] for _ in range(2)]
+    hosted = 0
+    for t in range(T):
+        a = torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)
+        ra = ea.step(a, *outs[0], fused=True)
+        rb = eb.step(a, *outs[1], fused=False)
+        for x, y in zip(ra, rb):
+            assert torch.equal(x, y), t
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), t
+        assert torch.equal(ea.state, eb.state) and torch.equal(ea.vec.reset_state, eb.vec.reset_state), t
+        assert torch.equal(ea.curr_index, eb.curr_index) and torch.equal(ea.next_index, eb.next_index), t
+        nh = ra[3].cpu().numpy().nonzero()[0]
+        for i in nh[:50]:
+            ea.place(int(i), int(i) % N, obs_out=outs[0][0])
+            eb.place(int(i), int(i) % N, obs_out=outs[1][0])
+        for i in nh[50:]:
+            ea.needs_host[int(i)] = 0
+            eb.needs_host[int(i)] = 0
+        hosted += len(nh)
+    assert int(ea.next_index.item()) == N and hosted > 0
+
+
 def test_step_learner_matches_acx_step():
     """obs_f32 / reward_f32 / done_f32 are the int outputs of acx_step, converted."""
     import acx
