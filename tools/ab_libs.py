@@ -24,6 +24,7 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--mode", default="rollout")
 ap.add_argument("--T", type=int, default=200)
+ap.add_argument("--L", type=int, default=36)
 ap.add_argument("--rounds", type=int, default=1, help="fresh output allocations (the speed depends on the mapping)")
 args = ap.parse_args()
 
@@ -37,7 +38,7 @@ for p in args.libs:
     libs.append(lib)
 
 dev = torch.device("cuda:0")
-L, B, T, H = 36, 1 << 20, args.T, 200
+L, B, T, H = args.L, 1 << 20, args.T, 200
 starts = torch.as_tensor(ms_starts(L, B)).to(dev)
 g = torch.Generator(device=dev)
 g.manual_seed(0)
