@@ -727,8 +727,8 @@ using TileFor = typename std::conditional<
     (LC >= 64 && LC % 8 == 0), CodeTile<NW, LC>,
     typename std::conditional<(LC > 0 && LC % 4 == 0), FastTile<NW, LC>, GenericTile<NW, LC, VEC>>::type>::type;
 
-// Per-lane row <-> registers through HBM directly (uncoalesced; used only on the rare
-// same-step-autoreset path of the step kernel).  LMAX = compile-time bound on L.
+// Per-lane registers -> row in HBM directly (uncoalesced; only for final_obs on the rare
+// same-step-autoreset path of the step kernel).
 template <int NW>
 __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>& p, int L) {
     for (int h = 0; h < 2; ++h) {
@@ -740,24 +740,6 @@ __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>&
             const int32_t v = (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu);
             dst[h * L + k] = k < n ? v : 0;
         }
-    }
-}
-template <int NW>
-__device__ __forceinline__ void global_to_regs(const int32_t* src, PresRegs<NW>& p, int L) {
-    for (int h = 0; h < 2; ++h) {
-        Word<NW> w = wzero<NW>();
-        int n = 0;
-#pragma unroll 1
-        for (int k = 0; k < L; ++k) {
-            const int32_t b = src[h * L + k];
-            const uint32_t code = ((((uint32_t)~b & 1u) << 1) | (((uint32_t)b >> 31) & 1u));
-            if (b != 0) {
-                w = wor<NW>(w, wsingle<NW>(code, k));
-                ++n;
-            }
-        }
-        if (h == 0) { p.w0 = w; p.n0 = n; }
-        else        { p.w1 = w; p.n1 = n; }
     }
 }
 
@@ -824,9 +806,12 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 
     tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
 
-    bool fin = false;  // done | truncated (the curriculum's "finished")
+    bool fin = false;    // done | truncated (the curriculum's "finished")
+    bool reset = false;  // same-step autoreset of this env
+    bool keep = false;   // the env's row is left as loaded (out of domain, or its move failed)
+    PresRegs<NW> p;
+    int cnt = 0, e = ACX_ERR_NONE;
     if (w.active) {
-        PresRegs<NW> p;
         int act;
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
             const int64_t v = a.action64[env];
@@ -834,19 +819,19 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         } else {
             act = a.action[env];
         }
-        int cnt = a.step_count ? a.step_count[env] + 1 : 0;
+        cnt = a.step_count ? a.step_count[env] + 1 : 0;
         // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
         // at [k][i] -- envs at the same episode position write one coalesced row segment (an
         // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
         if (LEARN && a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
-        int e;
         if (bad) e = ACX_ERR_DOMAIN;
         else if (is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
-        if (e == ACX_ERR_NONE) tile.unpack(w.lane, p);
-        const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
+        keep = e != ACX_ERR_NONE;
+        if (!keep) tile.unpack(w.lane, p);
+        const bool triv = !keep && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
         const bool trunc = a.step_count ? (cnt >= a.horizon) : false;
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
@@ -857,20 +842,29 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
             if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
         }
-        int l0 = p.n0, l1 = p.n1;
-        if ((triv || trunc) && a.reset_state && e == ACX_ERR_NONE) {
-            // same-step autoreset (rare): final_obs <- post-move state, state <- reset row
+        reset = fin && a.reset_state && !keep;
+        if (reset) {
+            // final_obs <- post-move state (per lane: rare, and only with final_obs)
             if (a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
-            global_to_regs<NW>(a.reset_state + env * twoL, p, L);
-            tile.unpack(w.lane, p);
-            l0 = p.n0;
-            l1 = p.n1;
             cnt = 0;
         }
+    }
+    if (__any(reset)) {
+        // same-step autoreset: the tile's starting states, one coalesced load (a per-lane row
+        // read cost ~1 ms on the step of a whole-batch truncation); resetting envs pack theirs,
+        // the others re-stage their state, rows left as loaded copy state_in in the store
+        wave_sync();
+        tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+        if (reset) tile.pack(w.lane, p);
+        wave_sync();
+        if (w.active && !keep) tile.unpack(w.lane, p);
+        tile.restore_flags(w.lane, w.active && keep);
+    }
+    if (w.active) {
         if (a.step_count) a.step_count[env] = cnt;
         if (a.lengths_out) {
-            a.lengths_out[2 * env] = l0;
-            a.lengths_out[2 * env + 1] = l1;
+            a.lengths_out[2 * env] = p.n0;
+            a.lengths_out[2 * env + 1] = p.n1;
         }
         if (a.err) a.err[env] = (uint8_t)e;
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
