@@ -1039,18 +1039,41 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
 // env-step instead of 4: its action reads are small scattered requests between trajectory
 // write bursts, and at 4 B they cost 7 % of the rollout (tools/store_pattern.py ACT8 vs
 // PACK8); this pass streams them once.
+__device__ __forceinline__ uint32_t pack_id(int32_t v) { return (uint32_t)v < 12u ? (uint32_t)v : 15u; }
+
+// VEC4: four consecutive envs per thread with 16-byte loads/stores (B % 4 == 0, aligned)
+template <bool VEC4>
 __global__ __launch_bounds__(256) void pack_actions_kernel(const int32_t* __restrict__ actions,
                                                            uint32_t* __restrict__ packed, int T, int64_t B) {
-    const int64_t env = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int t0 = (int)blockIdx.y * 8;
-    if (env >= B) return;
-    int32_t v[8];
+    if constexpr (VEC4) {
+        if (4 * i >= B) return;
+        const int4* src = reinterpret_cast<const int4*>(actions) + i;
+        const int64_t row4 = B / 4;
+        int4 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = t0 + k < T ? actions[(int64_t)(t0 + k) * B + env] : 0;
-    uint32_t q = 0;
+        for (int k = 0; k < 8; ++k) v[k] = t0 + k < T ? src[(int64_t)(t0 + k) * row4] : make_int4(0, 0, 0, 0);
+        uint4 q = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) q |= (t0 + k < T ? ((uint32_t)v[k] < 12u ? (uint32_t)v[k] : 15u) : 0u) << (4 * k);
-    packed[(int64_t)blockIdx.y * B + env] = q;
+        for (int k = 0; k < 8; ++k) {
+            if (t0 + k >= T) continue;
+            q.x |= pack_id(v[k].x) << (4 * k);
+            q.y |= pack_id(v[k].y) << (4 * k);
+            q.z |= pack_id(v[k].z) << (4 * k);
+            q.w |= pack_id(v[k].w) << (4 * k);
+        }
+        reinterpret_cast<uint4*>(packed + (int64_t)blockIdx.y * B)[i] = q;
+    } else {
+        if (i >= B) return;
+        int32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = t0 + k < T ? actions[(int64_t)(t0 + k) * B + i] : 0;
+        uint32_t q = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q |= (t0 + k < T ? pack_id(v[k]) : 0u) << (4 * k);
+        packed[(int64_t)blockIdx.y * B + i] = q;
+    }
 }
 
 
@@ -1409,8 +1432,13 @@ int acx_pack_actions(const int32_t* actions, uint32_t* packed, int32_t T, int64_
     if (B < 0 || T < 0) return ACX_E_ARG;
     if (B == 0 || T == 0) return ACX_OK;
     if (!actions || !packed || (T + 7) / 8 > 65535) return ACX_E_ARG;
-    const dim3 grid((unsigned)((B + 255) / 256), (unsigned)((T + 7) / 8));
-    pack_actions_kernel<<<grid, dim3(256), 0, (hipStream_t)stream>>>(actions, packed, T, B);
+    if (B % 4 == 0 && aligned16(actions) && aligned16(packed)) {
+        const dim3 grid((unsigned)((B / 4 + 255) / 256), (unsigned)((T + 7) / 8));
+        pack_actions_kernel<true><<<grid, dim3(256), 0, (hipStream_t)stream>>>(actions, packed, T, B);
+    } else {
+        const dim3 grid((unsigned)((B + 255) / 256), (unsigned)((T + 7) / 8));
+        pack_actions_kernel<false><<<grid, dim3(256), 0, (hipStream_t)stream>>>(actions, packed, T, B);
+    }
     return finish_launch();
 }
 

@@ -83,10 +83,11 @@ def test_invalid_ids_same_on_both_paths(L):
     assert int(a[7][0]) == int(hit.sum())
 
 
-def test_pack_actions_layout():
+@pytest.mark.parametrize("B", [777, 1024])  # scalar and 16-byte-vector packing paths
+def test_pack_actions_layout(B):
     from acx import _lib
     lib = _lib.load()
-    T, B = 21, 777
+    T = 21
     rng = np.random.default_rng(2)
     acts = rng.integers(-3, 20, size=(T, B)).astype(np.int32)
     words = (T + 7) // 8
