@@ -38,6 +38,17 @@ def _pack_key(state: np.ndarray, L: int) -> np.ndarray:
     return words
 
 
+def _devices(device):
+    """`device` may be one device or a list: the expansion of every parent batch is then
+    sharded by parent index over those GPUs, the keys gathered in order."""
+    if isinstance(device, (list, tuple)):
+        devs = [torch.device(d) for d in device]
+        if not devs:
+            raise ValueError("empty device list")
+        return devs
+    return [torch.device(device if device is not None else "cuda")]
+
+
 def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, device=None, batch=None,
                keep_node_keys=False):
     p = np.asarray(presentation)
@@ -45,7 +56,7 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
     L = len(p) // 2
     if np.any(np.abs(p) > 2):
         raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
-    dev = torch.device(device if device is not None else "cuda")
+    devs = _devices(device)
     lib = _lib.load()
     kw = _lib.key_words(L)
     # the start node is the (unreduced) input itself, as in the reference
@@ -59,20 +70,34 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
         parent_keys = np.zeros((batch, kw), dtype=np.uint64)
         pinned_in = torch.empty((batch, kw), dtype=torch.int64).pin_memory()
         pinned_out = torch.empty((batch, 12, kw), dtype=torch.int64).pin_memory()
-        dev_keys = torch.empty((batch, kw), dtype=torch.int64, device=dev)
-        dev_states = torch.empty((batch, 2 * L), dtype=torch.int32, device=dev)
-        out = {"keys": torch.empty((batch, 12, kw), dtype=torch.int64, device=dev)}
+        G = len(devs)
+        per = -(-batch // G)
+        bufs = []
+        for d in devs:
+            bufs.append((torch.empty((per, kw), dtype=torch.int64, device=d),
+                         torch.empty((per, 2 * L), dtype=torch.int32, device=d),
+                         {"keys": torch.empty((per, 12, kw), dtype=torch.int64, device=d)}))
         status = 0
         while status == 0:
             n = lib.acx_search_next_batch(h, parent_keys.ctypes.data, batch)
             if n == 0:
                 break
             pinned_in[:n].numpy()[:] = parent_keys[:n].view(np.int64)
-            dev_keys[:n].copy_(pinned_in[:n], non_blocking=True)
-            ops.unpack_keys(dev_keys[:n], L, out=dev_states[:n])
-            res = ops.expand12(dev_states[:n], cyclical=cyclical, children=False, lengths=False, keys=True,
-                               err=False, out=out)
-            pinned_out[:n].copy_(res["keys"][:n], non_blocking=False)
+            # contiguous parent slices, one per GPU, launched asynchronously on each GPU's stream
+            bounds = [n * g // G for g in range(G + 1)]
+            for g, d in enumerate(devs):
+                a, b = bounds[g], bounds[g + 1]
+                if a == b:
+                    continue
+                dev_keys, dev_states, out = bufs[g]
+                with torch.cuda.device(d):
+                    dev_keys[: b - a].copy_(pinned_in[a:b], non_blocking=True)
+                    ops.unpack_keys(dev_keys[: b - a], L, out=dev_states[: b - a])
+                    res = ops.expand12(dev_states[: b - a], cyclical=cyclical, children=False, lengths=False,
+                                       keys=True, err=False, out=out)
+                    pinned_out[a:b].copy_(res["keys"][: b - a], non_blocking=True)
+            for d in devs:
+                torch.cuda.synchronize(d)
             status = lib.acx_search_feed(h, pinned_out.data_ptr(), n)
         st = np.zeros(3, np.int64)
         lib.acx_search_stats(h, st.ctypes.data)

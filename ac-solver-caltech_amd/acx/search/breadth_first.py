@@ -3,7 +3,9 @@
 engine="device" (default): the whole search runs on the GPU (csrc/acx_bfs.hip) -- queue,
   visited hash set in HBM, expansion, dedup, budget -- in chunks of parents.
 engine="host": GPU expansion (acx_expand12) with the host engine (csrc/acx_search.cpp)
-  replaying the FIFO/dedup/budget logic on packed keys (BASELINE config 4's "dedup on host").
+  replaying the FIFO/dedup/budget logic on packed keys (BASELINE config 4's "dedup on host");
+  `device` may be a list of GPUs, over which each parent batch is sharded by index
+  (every GPU expands a slice, the keys come back in order for the host dedup).
 Both scan children in (parent FIFO order, action 0..11) order with the reference's success
 test, dedup and per-parent budget check, so paths are identical."""
 
@@ -17,6 +19,8 @@ def bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_redu
         batch=None, engine="device"):
     """Returns (True, path) or (False, None), as breadth_first.py:15-97."""
     if engine == "device":
+        if isinstance(device, (list, tuple)):
+            raise ValueError("the device BFS runs on one GPU; engine='host' shards the expansion over several")
         return device_bfs(presentation, max_nodes_to_explore, verbose, cyclically_reduce_after_moves, device=device,
                           chunk=batch or 0)
     if engine != "host":

@@ -85,3 +85,23 @@ def test_device_bfs_api_edges():
         bfs(np.array([1, 0, 0, 2]), 10)  # not a valid presentation (zero inside r0 ... r1)
     with pytest.raises(ValueError):
         bfs(np.array([3, 0, 2, 0]), 10)
+
+
+@pytest.mark.parametrize("mode,budget,batch,shards", [("bfs", 200_000, 65536, 3), ("bfs", 50_000, 1000, 2),
+                                                      ("greedy", 20_000, 512, 2)])
+def test_host_engine_expansion_sharded_over_devices(mode, budget, batch, shards):
+    """each parent batch split by index over a device list (here the one GPU listed
+    several times, so the slicing/gather path runs) gives the same nodes, order and path."""
+    from acx.search import _engine as E
+    start = _ak3(36)
+    m = E.BFS if mode == "bfs" else E.GREEDY
+    ok1, path1 = E.run_search(m, start, budget, False, False, device=DEV, batch=batch, keep_node_keys=True)
+    one = dict(E.LAST_STATS)
+    okn, pathn = E.run_search(m, start, budget, False, False, device=[DEV] * shards, batch=batch,
+                              keep_node_keys=True)
+    many = dict(E.LAST_STATS)
+    assert ok1 == okn and path1 == pathn
+    assert one["nodes"] == many["nodes"] and np.array_equal(one["node_keys"], many["node_keys"])
+    from acx import bfs
+    with pytest.raises(ValueError):
+        bfs(start, 10, device=[DEV, DEV])
