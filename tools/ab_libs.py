@@ -1,6 +1,6 @@
 """Interleaved A/B of two libacx.so builds in ONE process (cdna_hip_programming.md rule 24).
 
-    python tools/ab_libs.py libA.so libB.so [--reps 7] [--mode rollout|step]
+    python tools/ab_libs.py libA.so libB.so [--reps 7] [--mode rollout|step|expand]
 
 Each build gets its own ctypes handle (RTLD_LOCAL); both time the same acx_rollout
 (B = 2^20, L = 36, T = 200, all outputs) or 200 acx_step launches, alternating."""
@@ -57,6 +57,10 @@ def run(lib):
         rc = lib.acx_rollout(state.data_ptr(), acts.data_ptr(), starts.data_ptr(), cnt.data_ptr(), obs.data_ptr(),
                              rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), None, None, T, B, L, H, 1, stream)
         assert rc == 0
+    elif args.mode == "expand":  # config 4's kernel: 12 packed child keys per parent (search setting)
+        rc = lib.acx_expand12(exp_par.data_ptr(), None, None, exp_keys.data_ptr(), None, None, exp_par.shape[0], L, 0,
+                              stream)
+        assert rc == 0
     else:
         for t in range(T):
             rc = lib.acx_step(state.data_ptr(), state.data_ptr(), acts[t].data_ptr(), starts.data_ptr(),
@@ -68,6 +72,14 @@ def run(lib):
     return e0.elapsed_time(e1)
 
 
+if args.mode == "expand":  # 2^23 parents: random walks off the starting states
+    exp_par = starts.repeat(8, 1).contiguous()
+    for _k in range(16):
+        rc = libs[0].acx_step(exp_par.data_ptr(), exp_par.data_ptr(),
+                              torch.randint(0, 12, (exp_par.shape[0],), dtype=torch.int32, device=dev).data_ptr(),
+                              None, None, None, None, None, None, None, None, None, exp_par.shape[0], L, H, 0, stream)
+        assert rc == 0
+    exp_keys = torch.empty((exp_par.shape[0], 12, _lib.key_words(L)), dtype=torch.int64, device=dev)
 times = [[] for _ in libs]
 for rnd in range(args.rounds):
     obs = torch.zeros((T, B, 2 * L), dtype=torch.int32, device=dev)
