@@ -23,7 +23,7 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-trace = rows(os.path.join(d, "trace", "bench_kernel_trace.csv"))
+trace = sorted(rows(os.path.join(d, "trace", "bench_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
 disp = {}
 for r in trace:
     name = r["Kernel_Name"]
@@ -36,7 +36,7 @@ for kind in ("fetch", "write"):
     p = os.path.join(d, f"pmc_{kind}", "bench_counter_collection.csv")
     if not os.path.exists(p):
         continue
-    for r in rows(p):
+    for r in sorted(rows(p), key=lambda r: int(r["Dispatch_Id"])):
         if "acx::" not in r["Kernel_Name"]:
             continue
         pmc.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
@@ -58,8 +58,9 @@ for name, durs in disp.items():
 if bench:
     summary["bench_line"] = bench
     rl = bench["roofline"]
-    # the timed launch = the longest rollout_kernel dispatch (warmup is W steps) plus, when
-    # ops.rollout packed the move ids first, the longest pack_actions_kernel dispatch
+    # the timed launch = the last (in time) of the longest rollout_kernel dispatches (the warmup
+    # launch comes first) plus, when ops.rollout packed the move ids first, the matching
+    # pack_actions_kernel dispatch
     timed = [v for n, v in summary["kernels"].items() if "rollout_kernel" in n]
     packs = [v for n, v in summary["kernels"].items() if "pack_actions_kernel" in n]
 
@@ -70,16 +71,16 @@ if bench:
 
     if timed:
         k = max(timed, key=lambda v: v["max_ms"])
-        i = k["durations_ms"].index(k["max_ms"])
-        ms, traffic = k["max_ms"], hbm(k, i)
-        rec = {"rollout_kernel_ms": k["max_ms"], "rollout_kernel_hbm_bytes": traffic}
+        i = len(k["durations_ms"]) - 1
+        ms, traffic = k["durations_ms"][i], hbm(k, i)
+        rec = {"rollout_kernel_ms": ms, "rollout_kernel_hbm_bytes": traffic}
         if packs:
             pk = packs[0]
-            j = pk["durations_ms"].index(pk["max_ms"])
-            ms += pk["max_ms"]
+            j = len(pk["durations_ms"]) - 1
+            ms += pk["durations_ms"][j]
             pt = hbm(pk, j)
             traffic = None if traffic is None or pt is None else traffic + pt
-            rec.update({"pack_actions_kernel_ms": pk["max_ms"], "pack_actions_hbm_bytes": pt})
+            rec.update({"pack_actions_kernel_ms": pk["durations_ms"][j], "pack_actions_hbm_bytes": pt})
         rec.update({
             "rocprof_ms": ms, "bench_event_ms": rl["kernel_ms"],
             "agree_pct": 100 * abs(ms - rl["kernel_ms"]) / rl["kernel_ms"],
