@@ -9,11 +9,13 @@
 //   F_LDS     obs rows staged through LDS (write 18 dwords per lane, read back per chunk)
 //   F_ACT32   action loads in 32-step batches (4 groups of 8; one drain per 32 steps)
 //   F_PACK8   pre-packed actions: one uint32 (8 ids x 4 bits) per lane per 8 steps
+//   F_BLK     the block's 4 waves write its 4 tiles interleaved (wave k: every 4th KB) after a
+//             per-step barrier: 4 KB contiguous per store instruction round instead of 1 KB
 // Compared with the same bytes written linearly (grid-stride, like a fill).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-enum { F_NT = 1, F_SCAL = 2, F_ACT8 = 4, F_ACTPF = 8, F_LDS = 16, F_ACT32 = 32, F_PACK8 = 64 };
+enum { F_NT = 1, F_SCAL = 2, F_ACT8 = 4, F_ACTPF = 8, F_LDS = 16, F_ACT32 = 32, F_PACK8 = 64, F_BLK = 128 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -77,6 +79,13 @@ __global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, 
                 else *reinterpret_cast<v4i*>(dst + u * 64) = x;
             }
             __builtin_amdgcn_wave_barrier();
+        } else if (F & F_BLK) {
+            __syncthreads();
+            int4* bdst = obs + t * chunks_per_step + (int64_t)blockIdx.x * 4 * 64 * row_chunks + lane;
+            for (int u = 0; u < row_chunks; ++u) {
+                const v4i x = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(bdst + (u * 4 + wid) * 64));
+            }
         } else {
             for (int u = 0; u < row_chunks; ++u) {
                 if (F & F_NT) {
@@ -105,7 +114,7 @@ extern "C" int sp_tile(void* obs, void* rew, void* dn, void* tr, const void* act
                        int flags, void* stream) {
     dim3 grid((unsigned)((B + 255) / 256));
     switch (flags) {
-        CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83)
+        CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83) CASE(129)
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

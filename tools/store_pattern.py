@@ -37,8 +37,10 @@ def timeit(fn, name, nbytes):
     res[name] = {"ms": round(best, 4), "GBps": round(nbytes / best / 1e6, 1)}
 
 
-NAMES = {1: "NT", 2: "SCAL", 4: "ACT8", 8: "ACTPF", 16: "LDS", 32: "ACT32", 64: "PACK8"}
-for flags in (1, 5, 33, 65, 19, 23, 51, 83, 1, 19):
+NAMES = {1: "NT", 2: "SCAL", 4: "ACT8", 8: "ACTPF", 16: "LDS", 32: "ACT32", 64: "PACK8", 128: "BLK"}
+import sys as _sys
+flag_list = [int(x) for x in _sys.argv[1].split(",")] if len(_sys.argv) > 1 else [1, 5, 33, 65, 19, 23, 51, 83, 1, 19]
+for flags in flag_list:
     nb = obs_bytes + (T * B * 6 if flags & 2 else 0) + (T * B * 4 if flags & 44 else 0) + (T * B // 2 if flags & 64 else 0)
     name = "tile_" + ("+".join(v for k, v in NAMES.items() if flags & k) or "plain")
     name = name if name not in res else name + "_again"
