@@ -108,6 +108,35 @@ def cpu_baseline_c(L: int, horizon: int, seconds: float):
             "sample": f"oracle/acx_oracle.c env_step, 1 core, B=65536, {el:.1f}s"}
 
 
+def cpu_baseline_c_all(L: int, horizon: int, seconds: float, max_procs: int = 16):
+    """C oracle on every host core (one process each, <= 16, 16384 envs each): the strongest
+    CPU number (SURVEY 8d asks for the C++ restatement on one core and on all cores)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs_n = max(1, min(cores, max_procs))
+    code = (
+        "import sys,json,time,numpy as np; sys.path.insert(0,%r); sys.path.insert(0,%r);"
+        "from bench import ms_starts; from oracle import oracle as O;"
+        "r=int(sys.argv[1]); B=16384; s0=ms_starts(%d,B,offset=B*r); st=s0.copy(); c=np.zeros(B,np.int32);"
+        "rng=np.random.default_rng(r); n=0; t0=time.perf_counter()\n"
+        "while time.perf_counter()-t0<%f:\n"
+        "  O.env_step(st,rng.integers(0,12,size=B).astype(np.int32),%d,%d,c,reset_state=s0); n+=B\n"
+        "print(json.dumps([n,time.perf_counter()-t0]))"
+    ) % (REPO, PKG_ROOT, L, seconds, L, horizon)
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, "-c", code, str(r)], stdout=subprocess.PIPE, env=env)
+          for r in range(procs_n)]
+    total = 0.0
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds * 10 + 120)
+        n, el = json.loads(out.decode().strip().splitlines()[-1])
+        total += n / el
+    return {"value": total, "unit": "env-steps/s", "cores": procs_n, "kind": "port",
+            "sample": f"oracle/acx_oracle.c env_step, {procs_n} procs x 16384 envs x {seconds:.0f}s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,10 +159,12 @@ def main():
 
     cpu = None
     cpu_c = None
+    cpu_c_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
         # before anything touches the GPU
         cpu = cpu_baseline(L, H, args.cpu_seconds)
         cpu_c = cpu_baseline_c(L, H, min(5.0, args.cpu_seconds))
+        cpu_c_all = cpu_baseline_c_all(L, H, min(5.0, args.cpu_seconds))
 
     import torch
     import torch.distributed as dist
@@ -365,6 +396,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "cpu_baseline_c_oracle": cpu_c,
+        "cpu_baseline_c_oracle_all_cores": cpu_c_all,
         "variants": variants,
         "env_errors": n_err,
     }
