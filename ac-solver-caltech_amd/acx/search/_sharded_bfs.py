@@ -1,0 +1,240 @@
+"""Breadth-first search over G GPUs, one process per GPU (csrc/acx_sbfs.hip, C-ABI acx_sbfs_* in
+include/acx.h): the node store and the visited set are partitioned by key owner, the FIFO queue
+is global and implicit (node g lives on the rank that owns its key, in ascending g).  Every rank
+calls `sharded_bfs` with the same arguments (SPMD) and gets the same result, equal to
+ac_solver/search/breadth_first.py:15-97 and to the single-GPU device BFS (same path, same
+budget cut, same node order).
+
+Per chunk of global parents [head, head + P) the ranks exchange, through torch.distributed
+(RCCL over xGMI with the "nccl" backend; staged through host memory with "gloo"):
+  1. all_gather of [success seq, move-error seq, min length, children per owner] per rank;
+  2. all_to_all of the child records (packed key + seq) to their owners;
+  3. all_reduce (sum) of the per-parent survivor masks.
+Without an initialised process group (or with world size 1) the same code runs on one GPU with
+the exchanges as local copies.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import _lib
+from ..envs.utils import is_array_valid_presentation
+
+LAST_STATS = {}  # statistics of the most recent sharded search on this rank
+_HANDLES = {}  # (device, L, cyclical, chunk, local_cap, rank, world) -> handle
+NONE = 0xFFFFFFFF
+
+
+class _Comm:
+    """The three exchanges of a chunk over a process group (or none)."""
+
+    def __init__(self, group, dev):
+        self.group = group
+        self.dev = dev
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+            self.device_collectives = dist.get_backend(group) == "nccl"
+        else:
+            self.rank, self.world, self.device_collectives = 0, 1, True
+
+    def all_gather_rows(self, row: np.ndarray) -> np.ndarray:
+        """(world, n) int64: every rank's row."""
+        if self.world == 1:
+            return row[None, :].copy()
+        dev = self.dev if self.device_collectives else torch.device("cpu")
+        t = torch.as_tensor(row, dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return torch.stack(out).cpu().numpy()
+
+    def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits) -> None:
+        if self.world == 1:
+            n = int(send_splits[0])
+            recv[:n].copy_(send[:n])
+            return
+        if self.device_collectives:
+            dist.all_to_all_single(recv, send, list(recv_splits), list(send_splits), group=self.group)
+            return
+        r = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(r, send.cpu(), list(recv_splits), list(send_splits), group=self.group)
+        recv.copy_(r)
+
+    def all_reduce_sum_(self, t: torch.Tensor) -> None:
+        if self.world == 1:
+            return
+        if self.device_collectives:
+            dist.all_reduce(t, group=self.group)
+            return
+        c = t.cpu()
+        dist.all_reduce(c, group=self.group)
+        t.copy_(c)
+
+    def sum_rows(self, row) -> np.ndarray:
+        return self.all_gather_rows(np.asarray(row, dtype=np.int64)).sum(axis=0)
+
+    def min_rows(self, row) -> np.ndarray:
+        return self.all_gather_rows(np.asarray(row, dtype=np.int64)).min(axis=0)
+
+
+def _handle(lib, dev, L, cyc, chunk, lcap, rank, world):
+    key = (dev.index, L, bool(cyc), int(chunk), int(lcap), rank, world)
+    h = _HANDLES.get(key)
+    if h is not None:
+        return h
+    release_workspaces()  # one workspace per process (they hold the largest buffers)
+    with torch.cuda.device(dev):
+        ptr = lib.acx_sbfs_create(L, int(lcap), int(chunk), int(bool(cyc)), rank, world)
+    if not ptr:
+        raise _lib.ACXError(f"acx_sbfs_create(L={L}, local_cap={lcap}, chunk={chunk}) failed (device memory?)")
+    nrec = lib.acx_sbfs_max_records(ptr)
+    kw = _lib.key_words(L)
+    send = torch.empty(nrec * (kw + 1), dtype=torch.int64, device=dev)
+    recv = torch.empty(nrec * (kw + 1), dtype=torch.int64, device=dev)
+    mask = torch.empty(max(int(chunk), 1), dtype=torch.int32, device=dev)
+    h = (ptr, send, recv, mask)
+    _HANDLES[key] = h
+    return h
+
+
+def release_workspaces() -> None:
+    lib = _lib.load()
+    for ptr, *_ in _HANDLES.values():
+        lib.acx_sbfs_destroy(ptr)
+    _HANDLES.clear()
+
+
+def local_capacity(max_nodes: int, world: int) -> int:
+    """Node-store slots per rank: the rank's expected share of the max_nodes + 12 nodes a search
+    can hold, with 25% + 4096 headroom for the hash partition's imbalance (a full store raises)."""
+    n = int(max_nodes) + 12
+    return min(n, (n + world - 1) // world * 5 // 4 + 4096)
+
+
+def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
+                device=None, chunk=0, group=None, keep_node_keys=False):
+    """(True, path) | (False, None), as breadth_first.py:15-97; SPMD over the ranks of `group`
+    (default: the default process group, if initialised).  chunk = parents per round (0: 2^21).
+    keep_node_keys: LAST_STATS["node_keys"] / ["node_ids"] = this rank's nodes (ascending id)."""
+    p = np.asarray(presentation)
+    assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
+    if np.any(np.abs(p) > 2):
+        raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
+    L = len(p) // 2
+    max_nodes = max(int(max_nodes_to_explore), 1)  # the reference still expands the root once
+    if max_nodes > (1 << 30):
+        raise ValueError("sharded bfs supports at most 2^30 nodes")
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    comm = _Comm(group, dev)
+    chunk = int(chunk) if chunk else 1 << 21
+    lcap = local_capacity(max_nodes, comm.world)
+    lib = _lib.load()
+    h, send, recv, gmask = _handle(lib, dev, L, cyclically_reduce_after_moves, chunk, lcap, comm.rank,
+                                   comm.world)
+    kw = _lib.key_words(L)
+    rw = kw + 1
+    pres = np.ascontiguousarray(p, dtype=np.int32)
+    total0 = int(np.count_nonzero(pres))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    W = comm.world
+    exp_out = np.zeros(5 + W, np.int64)
+    com_out = np.zeros(5, np.int64)
+
+    def ok(st, what):
+        if st < 0:
+            _lib.check(st, what)
+
+    with torch.cuda.device(dev):
+        ok(lib.acx_sbfs_reset(h, pres.ctypes.data, stream), "acx_sbfs_reset")
+        n_nodes, head, parents, chunks, min_len = 1, 0, 0, 0, total0
+        status, succ_node, succ_act = _lib.BFS_EXHAUSTED, -1, -1
+        while head < n_nodes:
+            P = min(n_nodes - head, chunk)
+            ok(lib.acx_sbfs_expand(h, head, P, exp_out.ctypes.data, stream), "acx_sbfs_expand")
+            rows = comm.all_gather_rows(exp_out)  # (W, 5 + W)
+            if rows[:, 4].any():
+                raise _lib.ACXError("sharded bfs: hash table overflow")
+            succ_seq, err_seq = int(rows[:, 0].min()), int(rows[:, 1].min())
+            chunk_min = int(rows[:, 2].min())
+            send_counts = rows[comm.rank, 5:]
+            recv_counts = rows[:, 5 + comm.rank]
+            nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
+            ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
+            comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
+                            [int(c) * rw for c in send_counts])
+            end = min(succ_seq, err_seq)
+            ok(lib.acx_sbfs_insert(h, recv.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
+            comm.all_reduce_sum_(gmask[:P])
+            ok(lib.acx_sbfs_commit(h, gmask.data_ptr(), n_nodes, max_nodes - n_nodes, com_out.ctypes.data, stream),
+               "acx_sbfs_commit")
+            chunks += 1
+            if comm.sum_rows([com_out[4]])[0]:
+                raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
+            total_new, cut_p, nodes_at_cut = int(com_out[0]), int(com_out[1]), int(com_out[2])
+            cut = cut_p if cut_p >= 0 else None
+            err_p = err_seq // 12 if err_seq != NONE else None
+            suc_p = succ_seq // 12 if succ_seq != NONE else None
+            err_first = err_p is not None and err_seq < succ_seq and (cut is None or err_p <= cut)
+            succ_first = not err_first and suc_p is not None and (cut is None or suc_p <= cut)
+            if err_first or succ_first or cut is not None:
+                last = err_p if err_first else suc_p if succ_first else cut
+                if succ_first:
+                    min_len = 2
+                else:
+                    m = comm.min_rows([lib.acx_sbfs_min_len(h, last, stream)])[0]
+                    min_len = min(min_len, int(m))
+                parents += last + 1
+                if err_first:
+                    status = _lib.BFS_MOVE_ERROR
+                elif succ_first:
+                    status = _lib.BFS_FOUND
+                    succ_node, succ_act = head + suc_p, succ_seq % 12
+                else:
+                    status = _lib.BFS_BUDGET
+                    n_nodes = nodes_at_cut
+                break
+            min_len = min(min_len, chunk_min)
+            parents += P
+            n_nodes += total_new
+            head += P
+
+        path = None
+        if status == _lib.BFS_FOUND:
+            # walk up the parent ids; the rank that stores a node answers for it
+            look = np.zeros(4, np.int64)
+            edges = [(succ_act, 2)]
+            g = succ_node
+            while g > 0:
+                ok(lib.acx_sbfs_lookup(h, g, look.ctypes.data, stream), "acx_sbfs_lookup")
+                found = comm.sum_rows(look * (look[0] != 0))
+                if found[0] != 1:
+                    raise _lib.ACXError(f"sharded bfs: node {g} stored on {found[0]} ranks")
+                edges.append((int(found[2]), int(found[3])))
+                g = int(found[1])
+            path = [(-1, total0)] + edges[::-1]
+
+    LAST_STATS.clear()
+    LAST_STATS.update(nodes=int(n_nodes), parents=int(parents), chunks=int(chunks), min_length=int(min_len),
+                      status=int(status), rank=comm.rank, world=W)
+    if keep_node_keys:
+        n = lib.acx_sbfs_node_keys(h, None, None, 0)
+        nk = np.zeros((max(n, 0), kw), np.uint64)
+        ng = np.zeros(max(n, 0), np.int64)
+        if n > 0:
+            lib.acx_sbfs_node_keys(h, nk.ctypes.data, ng.ctypes.data, n)
+        LAST_STATS["node_keys"], LAST_STATS["node_ids"] = nk, ng
+    if status == _lib.BFS_MOVE_ERROR:
+        raise AssertionError("bfs: a move produced an invalid presentation (utils.py:264-266)")
+    if verbose and comm.rank == 0:
+        print(f"Minimal total length found: {min_len}")
+    if status == _lib.BFS_BUDGET and comm.rank == 0:
+        print(f"Exiting search as number of explored nodes = {n_nodes} has exceeded the limit "
+              f"{max_nodes_to_explore}")
+    if status == _lib.BFS_FOUND:
+        return True, path
+    return False, None

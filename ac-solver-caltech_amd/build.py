@@ -18,7 +18,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "acx", "libacx.so")
 INCLUDE = os.path.join(REPO, "include")
-SOURCES = ["acx_kernels.hip", "acx_bfs.hip", "acx_features.hip", "acx_curriculum.hip", "acx_search.cpp"]
+SOURCES = ["acx_kernels.hip", "acx_bfs.hip", "acx_sbfs.hip", "acx_features.hip", "acx_curriculum.hip", "acx_search.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ACX_OFFLOAD_ARCH", "gfx950")
 
@@ -38,8 +38,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
     procs = []
+    headers = [os.path.join(INCLUDE, "acx.h")] + [os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                                                   if f.endswith((".h", ".hpp"))]
     for src in SOURCES:
         obj = os.path.join(HERE, "build", src + ".o")
+        objs.append(obj)
+        if not force and os.path.exists(obj):
+            t = os.path.getmtime(obj)
+            if all(os.path.getmtime(d) <= t for d in [os.path.join(CSRC, src), __file__] + headers):
+                continue  # object up to date
         if src.endswith(".hip"):
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE,
                    "-Wno-pass-failed", os.path.join(CSRC, src), "-o", obj]
@@ -48,7 +55,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("libacx build failed")

@@ -35,13 +35,10 @@
 #include "acx.h"
 #include "acx_moves.h"
 
+#include "acx_bfs_common.h"
+
 namespace acx {
 namespace bfs {
-
-constexpr uint64_t CHUNK = 1ull << 63;
-constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t SEEN = 0xffffffffu;  // slot index of a child whose state is already a node
-constexpr int TPB = 256;
 
 struct Ctl {
     uint32_t succ_seq;  // min seq of a child with n0 + n1 == 2
@@ -53,83 +50,6 @@ struct Ctl {
     uint64_t total_new;     // nodes appended by the chunk
     uint64_t nodes_at_cut;  // len(tree_nodes) after parent cut_p
 };
-
-__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdull;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ull;
-    k ^= k >> 33;
-    return k;
-}
-
-template <int KWM>
-struct Key {
-    uint64_t w[KWM];
-};
-
-template <int KWM>
-__device__ __forceinline__ Key<KWM> kload(const uint64_t* p, int kw) {
-    Key<KWM> k;
-#pragma unroll
-    for (int i = 0; i < KWM; ++i) k.w[i] = i < kw ? p[i] : 0ull;
-    return k;
-}
-
-template <int KWM>
-__device__ __forceinline__ bool keq(const uint64_t* p, const Key<KWM>& k, int kw) {
-    bool e = true;
-#pragma unroll
-    for (int i = 0; i < KWM; ++i)
-        if (i < kw) e &= p[i] == k.w[i];
-    return e;
-}
-
-template <int KWM>
-__device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
-    uint64_t h = 0x9e3779b97f4a7c15ull;
-#pragma unroll
-    for (int i = 0; i < KWM; ++i)
-        if (i < kw) h = fmix64(h ^ k.w[i]) + 0x632be59bd9b4e019ull;
-    return fmix64(h);
-}
-
-__device__ __forceinline__ uint64_t tload(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// exclusive prefix sum of v over the block (TPB threads); total in `tot`
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& tot) {
-    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, WAVE);
-        if (lane >= o) x += y;
-    }
-    if (lane == WAVE - 1) sh[wid] = x;
-    __syncthreads();
-    uint32_t off = 0;
-    tot = 0;
-#pragma unroll
-    for (int i = 0; i < TPB / WAVE; ++i) {
-        off += i < wid ? sh[i] : 0u;
-        tot += sh[i];
-    }
-    return off + x - v;
-}
-
-__device__ __forceinline__ uint32_t block_min(uint32_t v, uint32_t* sh) {
-    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, WAVE));
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    uint32_t m = 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < TPB / WAVE; ++i) m = min(m, sh[i]);
-    return m;
-}
 
 struct Args {
     uint64_t* qkeys;     // (qcap, kw) node keys in FIFO order
@@ -362,18 +282,6 @@ __global__ void bfs_path_kernel(Args a, int64_t node, int32_t* out, int64_t cap,
     }
 }
 
-static inline int nw_for(int L) { return L <= 16 ? 1 : L <= 32 ? 2 : L <= 48 ? 3 : L <= 64 ? 4 : 8; }
-
-template <class F>
-static void by_nw(int L, F&& f) {
-    switch (nw_for(L)) {
-        case 1: f.template go<1>(); break;
-        case 2: f.template go<2>(); break;
-        case 3: f.template go<3>(); break;
-        case 4: f.template go<4>(); break;
-        default: f.template go<8>(); break;
-    }
-}
 
 struct Search {
     int dev = 0, L = 0, kw = 0, cyc = 0;
@@ -432,25 +340,6 @@ struct PathLaunch {
     void go() { bfs_path_kernel<NW><<<dim3(1), dim3(64), 0, st>>>(S->a, node, S->path_dev, PATH_CAP, S->path_n_dev); }
 };
 
-// host packing of a presentation into the key format (acx.h)
-static void pack_key(const int32_t* pres, int L, int kw, uint64_t* out) {
-    for (int k = 0; k < kw; ++k) out[k] = 0;
-    int n[2] = {0, 0};
-    for (int h = 0; h < 2; ++h) {
-        for (int i = 0; i < L; ++i) {
-            const int32_t v = pres[h * L + i];
-            if (v == 0) continue;
-            const uint64_t code = v == 1 ? 0 : v == -1 ? 1 : v == 2 ? 2 : 3;
-            const int bit = 2 * (h * L + i);
-            out[bit / 64] |= code << (bit % 64);
-            ++n[h];
-        }
-    }
-    const uint64_t lens = (uint64_t)n[0] | ((uint64_t)n[1] << 8);
-    const int bit = 4 * L;
-    out[bit / 64] |= lens << (bit % 64);
-    if (bit % 64 > 48 && bit / 64 + 1 < kw) out[bit / 64 + 1] |= lens >> (64 - bit % 64);
-}
 
 }  // namespace bfs
 }  // namespace acx

@@ -1,0 +1,677 @@
+// acx_sbfs.hip -- breadth-first search with the node store and the visited set partitioned
+// over G GPUs by key owner (SURVEY §8e "GPU-side dedup", §8f item 1).  One process per GPU;
+// the host (acx/search/_sharded_bfs.py) runs the same chunk loop on every rank and does the
+// three exchanges of a chunk with torch.distributed (RCCL over xGMI on the GPU node):
+//   1. all_gather of a small vector per rank (success / move-error seqs, min length, the
+//      number of children this rank sends to each owner);
+//   2. all_to_all of child records (packed key + chunk seq) to their owners;
+//   3. all_reduce (sum) of the per-parent survivor masks (P x int32; bits are disjoint).
+//
+// Reference: ac_solver/search/breadth_first.py:15-97; results (path, budget cut, node order)
+// equal the single-GPU device BFS (acx_bfs.hip) and the reference.  The FIFO queue is global
+// and implicit: node g (its position in the reference's `to_explore` / `tree_nodes` order)
+// lives on rank owner(key(g)), which stores it in ascending g.  A chunk is the global parent
+// range [head, head + P); each rank expands the parents it owns in that range (a contiguous
+// run of its store), so child seq s = 12 (g - head) + action is the child's position in the
+// reference's sequential order, exactly as on one GPU.
+//
+// Per chunk on rank r:
+//   expand  -- its parents' 12 children (keys action-major), owner per child, per-owner counts;
+//   pack    -- children into the send buffer grouped by owner: record = kw key words + seq;
+//   insert  -- (received records) seq -> record map; probe / claim / join the owner's hash table
+//              with atomicMin on seq (first occurrence wins, as in acx_bfs.hip); mark
+//              survivors as bit (s % 12) of mask[s / 12];
+//   commit  -- after the mask all-reduce every rank knows all survivors: a prefix sum over
+//              parents gives each survivor's global id g and the node-budget cut (identical on
+//              all ranks); a second prefix sum over the survivors this rank owns gives their
+//              slots in its store, where they are appended (ascending g) and their table
+//              entries rewritten as node entries.
+// Owner of a key = (fp * G) >> 32 with fp the high hash bits (table slot = low bits).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+
+#include "acx.h"
+#include "acx_bfs_common.h"
+
+namespace acx {
+namespace sbfs {
+
+using namespace acx::bfs;
+
+constexpr int MAXW = 64;  // max ranks
+
+struct Ctl {
+    uint32_t succ_seq;   // expand: min seq of a local child with n0 + n1 == 2
+    uint32_t err_seq;    // expand: min seq of a local child whose move raised
+    uint32_t min_len;    // expand: min child total over the local parents
+    uint32_t npar;       // expand: local parents in the chunk
+    uint32_t overflow;   // a probe walked the whole table / the node store is full
+    uint32_t cut_p;      // commit: parent after which len(tree_nodes) >= max_nodes (all ranks)
+    uint64_t total_new;  // commit: nodes appended by the chunk over all ranks
+    uint64_t local_new;  // commit: nodes appended to this rank's store
+    uint64_t nodes_at_cut;
+    uint32_t stored;     // commit: nodes stored here (appends before max_nodes + 12)
+    uint32_t pad2;
+    uint32_t cnt[MAXW];  // expand: children sent to each owner
+    uint32_t cur[MAXW];  // pack cursors
+};
+
+struct Args {
+    uint64_t* lkeys;  // (lcap, kw) owned nodes, ascending global id
+    int64_t* lgid;    // (lcap) global node id
+    int64_t* lpar;    // (lcap) global id of the parent, -1 for the root
+    uint8_t* lact;    // (lcap) move id that produced the node
+    uint64_t* ckeys;  // (12, Pr) keys of the local parents' children, action-major
+    uint8_t* cown;    // (12, Pr) owner of each child, 0xff: parent not in the chunk
+    uint8_t* pmin;    // (Pr) min child total per local parent
+    uint32_t* map;    // (12 P) seq -> received record, NONE if not received here
+    uint32_t* rslot;  // (rcap) slot claimed/joined by a received child, SEEN if known
+    uint32_t* bsum;   // (nb) all survivors per block of parents -> exclusive offsets
+    uint32_t* lbsum;  // (nb) own survivors per block -> exclusive offsets
+    uint64_t* table;  // (mask + 1)
+    Ctl* ctl;
+    const uint64_t* recv;  // (nrecv, kw + 1) received records
+    uint64_t* send;        // (nsend, kw + 1) records grouped by owner
+    uint32_t* gmask;       // (P) survivor masks (this rank's, then all-reduced)
+    int64_t* look;         // lookup result
+    uint64_t mask;
+    int64_t head, n_before, need, lcap, nloc, lo, nrecv;
+    int P, Pr, L, kw, cyc, world;
+    uint32_t end;
+};
+
+__device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
+    return (uint32_t)(((h >> 32) * (uint64_t)world) >> 32);
+}
+
+// (1) lane per candidate local parent lo + j (j < Pr = min(P, nloc - lo)); the parents of the
+// chunk are the prefix with gid < head + P
+template <int NW>
+__global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
+    __shared__ uint32_t hist[MAXW];
+    for (int i = threadIdx.x; i < a.world; i += TPB) hist[i] = 0;
+    __syncthreads();
+    const int j = blockIdx.x * TPB + threadIdx.x;
+    const int64_t gid = j < a.Pr ? a.lgid[a.lo + j] : INT64_MAX;
+    if (gid < a.head + a.P) {
+        atomicMax(&a.ctl->npar, (uint32_t)(j + 1));
+        PresRegs<NW> pr;
+        load_key<NW>(a.lkeys + (a.lo + j) * a.kw, a.kw, a.L, pr);
+        const bool cyc = a.cyc != 0;
+        const bool clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, cyc);
+        const uint32_t p = (uint32_t)(gid - a.head);
+        uint32_t succ = NONE, err = NONE;
+        int mn = 255;
+        for (int act = 0; act < 12; ++act) {
+            PresRegs<NW> q = pr;
+            const int e = clean ? ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc)
+                                : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc);
+            const uint32_t s = p * 12u + (uint32_t)act;
+            const int tot = q.n0 + q.n1;
+            if (e != ACX_ERR_NONE) {
+                if (err == NONE) err = s;
+            } else {
+                if (tot == 2 && succ == NONE) succ = s;
+                mn = tot < mn ? tot : mn;
+            }
+            uint64_t* dst = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
+            store_key<NW>(dst, a.kw, a.L, q);
+            const uint32_t o = owner_of(khash<NW + 1>(kload<NW + 1>(dst, a.kw), a.kw), a.world);
+            a.cown[(int64_t)act * a.Pr + j] = (uint8_t)o;
+            atomicAdd(&hist[o], 1u);
+        }
+        a.pmin[j] = (uint8_t)mn;
+        if (succ != NONE) atomicMin(&a.ctl->succ_seq, succ);
+        if (err != NONE) atomicMin(&a.ctl->err_seq, err);
+        atomicMin(&a.ctl->min_len, (uint32_t)mn);
+    } else if (j < a.Pr) {
+        for (int act = 0; act < 12; ++act) a.cown[(int64_t)act * a.Pr + j] = 0xff;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.world; i += TPB)
+        if (hist[i]) atomicAdd(&a.ctl->cnt[i], hist[i]);
+}
+
+// (2) records into the send buffer, grouped by owner (order within a group is arbitrary:
+// the owner indexes records by seq)
+__global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
+    __shared__ uint32_t hist[MAXW], base[MAXW], off[MAXW];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int i = 0; i < a.world; ++i) {
+            off[i] = run;
+            run += a.ctl->cnt[i];
+        }
+    }
+    for (int i = threadIdx.x; i < a.world; i += TPB) hist[i] = 0;
+    __syncthreads();
+    const int j = blockIdx.x * TPB + threadIdx.x;
+    uint32_t loc[12];
+    uint8_t own[12];
+#pragma unroll
+    for (int act = 0; act < 12; ++act) {
+        own[act] = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : (uint8_t)0xff;
+        loc[act] = own[act] != 0xff ? atomicAdd(&hist[own[act]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.world; i += TPB) base[i] = hist[i] ? atomicAdd(&a.ctl->cur[i], hist[i]) : 0u;
+    __syncthreads();
+    if (j >= a.Pr || own[0] == 0xff) return;
+    const uint32_t p = (uint32_t)(a.lgid[a.lo + j] - a.head);
+    const int rw = a.kw + 1;
+#pragma unroll
+    for (int act = 0; act < 12; ++act) {
+        const int o = own[act];
+        const int64_t pos = (int64_t)off[o] + base[o] + loc[act];
+        const uint64_t* src = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
+        uint64_t* dst = a.send + pos * rw;
+        for (int k = 0; k < a.kw; ++k) dst[k] = src[k];
+        dst[a.kw] = (uint64_t)(p * 12u + (uint32_t)act);
+    }
+}
+
+// (3a) seq -> received record
+__global__ __launch_bounds__(TPB) void sbfs_map_kernel(Args a) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= a.nrecv) return;
+    a.map[(uint32_t)a.recv[i * (a.kw + 1) + a.kw]] = (uint32_t)i;
+}
+
+// (3b) probe / claim / join, one lane per received child (acx_bfs.hip bfs_insert_kernel)
+template <int KWM>
+__global__ __launch_bounds__(TPB) void sbfs_insert_kernel(Args a) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= a.nrecv) return;
+    const int rw = a.kw + 1;
+    const uint64_t* rec = a.recv + i * rw;
+    const uint32_t s = (uint32_t)rec[a.kw];
+    if (s > a.end) {  // after the search's last child
+        a.rslot[i] = SEEN;
+        return;
+    }
+    const Key<KWM> key = kload<KWM>(rec, a.kw);
+    const uint64_t h = khash<KWM>(key, a.kw);
+    const uint32_t fp = (uint32_t)(h >> 32);
+    uint64_t idx = h & a.mask;
+    const uint64_t my = CHUNK | ((uint64_t)s << 32) | fp;
+    uint32_t res = SEEN;
+    for (uint64_t it = 0;; ++it) {
+        if (it > a.mask) {
+            atomicOr(&a.ctl->overflow, 1u);
+            break;
+        }
+        uint64_t v = tload(a.table + idx);
+        if (v == 0) {
+            const uint64_t old = atomicCAS((unsigned long long*)(a.table + idx), 0ull, (unsigned long long)my);
+            if (old == 0) {
+                res = (uint32_t)idx;
+                break;
+            }
+            v = old;
+        }
+        if ((uint32_t)v == fp) {
+            const uint32_t hi = (uint32_t)(v >> 32);
+            if (v & CHUNK) {
+                const uint32_t i2 = a.map[hi & 0x7fffffffu];
+                if (keq<KWM>(a.recv + (int64_t)i2 * rw, key, a.kw)) {
+                    atomicMin((unsigned long long*)(a.table + idx), (unsigned long long)my);
+                    res = (uint32_t)idx;
+                    break;
+                }
+            } else if (keq<KWM>(a.lkeys + (int64_t)(hi - 1) * a.kw, key, a.kw)) {
+                break;  // already a node
+            }
+        }
+        idx = (idx + 1) & a.mask;
+    }
+    a.rslot[i] = res;
+}
+
+// (3c) survivors (the slot still holds their own seq) -> mask bits
+__global__ __launch_bounds__(TPB) void sbfs_mark_kernel(Args a) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= a.nrecv) return;
+    const uint32_t si = a.rslot[i];
+    if (si == SEEN) return;
+    const uint32_t s = (uint32_t)a.recv[i * (a.kw + 1) + a.kw];
+    if ((a.table[si] >> 32) == ((CHUNK >> 32) | s)) atomicOr(&a.gmask[s / 12u], 1u << (s % 12u));
+}
+
+// bits of m whose child this rank received (hence owns, if it survived)
+__device__ __forceinline__ uint32_t own_bits(const Args& a, uint32_t p, uint32_t m) {
+    uint32_t r = 0, mm = m;
+    while (mm) {
+        const int act = __builtin_ctz(mm);
+        mm &= mm - 1;
+        if (a.map[p * 12u + act] != NONE) r |= 1u << act;
+    }
+    return r;
+}
+
+// (4a) per-block counts of all survivors and of this rank's
+__global__ __launch_bounds__(TPB) void sbfs_count_kernel(Args a) {
+    __shared__ uint32_t sh[TPB / WAVE];
+    const int p = blockIdx.x * TPB + threadIdx.x;
+    const uint32_t m = p < a.P ? a.gmask[p] : 0u;
+    const uint32_t mine = p < a.P ? own_bits(a, (uint32_t)p, m) : 0u;
+    uint32_t tot, ltot;
+    block_excl_scan(__popc(m), sh, tot);
+    __syncthreads();
+    block_excl_scan(__popc(mine), sh, ltot);
+    if (threadIdx.x == 0) {
+        a.bsum[blockIdx.x] = tot;
+        a.lbsum[blockIdx.x] = ltot;
+    }
+}
+
+// (4b) exclusive scan of x[0..nb) in place, one block of 1024; the total into *total
+__global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, int nb, uint64_t* total) {
+    __shared__ uint32_t sh[1024 / WAVE];
+    const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
+    const int per = (nb + 1023) / 1024;
+    const int b0 = t * per, b1 = min(nb, b0 + per);
+    uint32_t loc = 0;
+    for (int i = b0; i < b1; ++i) loc += x[i];
+    uint32_t v = loc;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, WAVE);
+        if (lane >= o) v += y;
+    }
+    if (lane == WAVE - 1) sh[wid] = v;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < 1024 / WAVE; ++i) {
+        off += i < wid ? sh[i] : 0u;
+        tot += sh[i];
+    }
+    uint32_t run = off + v - loc;
+    for (int i = b0; i < b1; ++i) {
+        const uint32_t c = x[i];
+        x[i] = run;
+        run += c;
+    }
+    if (t == 0) *total = tot;
+}
+
+// (4c) global ids, the budget cut, and the appends to this rank's store
+__global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
+    __shared__ uint32_t sh[TPB / WAVE];
+    const int p = blockIdx.x * TPB + threadIdx.x;
+    const uint32_t m = p < a.P ? a.gmask[p] : 0u;
+    const uint32_t mine = p < a.P ? own_bits(a, (uint32_t)p, m) : 0u;
+    uint32_t tot;
+    const int64_t base = (int64_t)a.bsum[blockIdx.x] + block_excl_scan(__popc(m), sh, tot);
+    __syncthreads();
+    const int64_t lbase = (int64_t)a.lbsum[blockIdx.x] + block_excl_scan(__popc(mine), sh, tot);
+    if (p >= a.P) return;
+    const int64_t incl = base + __popc(m);
+    if (incl >= a.need && (base < a.need || p == 0)) {
+        a.ctl->cut_p = (uint32_t)p;
+        a.ctl->nodes_at_cut = (uint64_t)(a.n_before + incl);
+    }
+    uint32_t mm = mine, stored = 0;
+    while (mm) {
+        const int act = __builtin_ctz(mm);
+        mm &= mm - 1;
+        const uint32_t below = (1u << act) - 1u;
+        const int64_t gid = a.n_before + base + __popc(m & below);
+        // a node at or past max_nodes + 12 comes after the budget cut and is never used (the
+        // single-GPU queue drops it too); the ones kept are a prefix of this rank's appends
+        if (gid >= a.n_before + a.need + 12) continue;
+        const int64_t li = a.nloc + lbase + __popc(mine & below);
+        if (li >= a.lcap) {
+            atomicOr(&a.ctl->overflow, 2u);
+            continue;
+        }
+        ++stored;
+        const uint32_t i = a.map[(uint32_t)p * 12u + act];
+        const uint64_t* rec = a.recv + (int64_t)i * (a.kw + 1);
+        for (int k = 0; k < a.kw; ++k) a.lkeys[li * a.kw + k] = rec[k];
+        a.lgid[li] = gid;
+        a.lpar[li] = a.head + p;
+        a.lact[li] = (uint8_t)act;
+        const uint32_t si = a.rslot[i];
+        a.table[si] = ((uint64_t)(li + 1) << 32) | (uint32_t)a.table[si];
+    }
+    if (stored) atomicAdd(&a.ctl->stored, stored);
+}
+
+// min child total over the local parents of the chunk with p <= last
+__global__ __launch_bounds__(TPB) void sbfs_minlen_kernel(Args a, int64_t last) {
+    const int j = blockIdx.x * TPB + threadIdx.x;
+    if (j >= (int)a.ctl->npar) return;
+    if (a.lgid[a.lo + j] - a.head <= last) atomicMin(&a.ctl->min_len, (uint32_t)a.pmin[j]);
+}
+
+// the stored node with global id g: found, parent id, action, total length
+template <int NW>
+__global__ void sbfs_lookup_kernel(Args a, int64_t g) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t lo = 0, hi = a.nloc;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (a.lgid[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    a.look[0] = 0;
+    if (lo < a.nloc && a.lgid[lo] == g) {
+        PresRegs<NW> pr;
+        load_key<NW>(a.lkeys + lo * a.kw, a.kw, a.L, pr);
+        a.look[0] = 1;
+        a.look[1] = a.lpar[lo];
+        a.look[2] = a.lact[lo];
+        a.look[3] = pr.n0 + pr.n1;
+    }
+}
+
+template <int KWM>
+__global__ void sbfs_root_kernel(Args a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const Key<KWM> key = kload<KWM>(a.lkeys, a.kw);
+    const uint64_t h = khash<KWM>(key, a.kw);
+    a.table[h & a.mask] = (1ull << 32) | (uint32_t)(h >> 32);
+    a.lgid[0] = 0;
+    a.lpar[0] = -1;
+    a.lact[0] = 0xff;
+}
+
+struct Shard {
+    int dev = 0, L = 0, kw = 0, cyc = 0, rank = 0, world = 1;
+    int64_t lcap = 0, pmax = 0, rcap = 0, nloc = 0, lo = 0;
+    int P = 0, Pr = 0;
+    int64_t head = 0, nrecv = 0;
+    uint64_t tsize = 0;
+    Args a{};
+    Ctl* ctl_host = nullptr;
+    int64_t* look_host = nullptr;
+
+    ~Shard() {
+        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.map,
+                        a.rslot, a.bsum, a.lbsum, a.table, a.ctl, a.look};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        if (ctl_host) (void)hipHostFree(ctl_host);
+        if (look_host) (void)hipHostFree(look_host);
+    }
+};
+
+template <class T>
+static bool dalloc(T*& p, size_t n) {
+    return hipMalloc((void**)&p, n * sizeof(T) + 16) == hipSuccess;
+}
+
+static inline int nblocks(int64_t n) { return (int)((n + TPB - 1) / TPB); }
+
+struct ExpandLaunch {
+    Shard* S;
+    hipStream_t st;
+    template <int NW>
+    void go() { sbfs_expand_kernel<NW><<<dim3(nblocks(S->Pr)), dim3(TPB), 0, st>>>(S->a); }
+};
+struct InsertLaunch {
+    Shard* S;
+    hipStream_t st;
+    template <int NW>
+    void go() { sbfs_insert_kernel<NW + 1><<<dim3(nblocks(S->nrecv)), dim3(TPB), 0, st>>>(S->a); }
+};
+struct RootLaunch {
+    Shard* S;
+    hipStream_t st;
+    template <int NW>
+    void go() { sbfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a); }
+};
+struct LookupLaunch {
+    Shard* S;
+    hipStream_t st;
+    int64_t g;
+    template <int NW>
+    void go() { sbfs_lookup_kernel<NW><<<dim3(1), dim3(64), 0, st>>>(S->a, g); }
+};
+
+static int sync_ctl(Shard* S, hipStream_t st) {
+    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMemcpyAsync(S->ctl_host, S->a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess)
+        return ACX_E_LAUNCH;
+    if (hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+    return ACX_OK;
+}
+
+}  // namespace sbfs
+}  // namespace acx
+
+using namespace acx::sbfs;
+
+extern "C" {
+
+void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32_t cyclical, int32_t rank,
+                      int32_t world) {
+    if (L < 1 || L > ACX_MAX_L || local_cap < 1 || local_cap > (1ll << 30)) return nullptr;
+    if (world < 1 || world > MAXW || rank < 0 || rank >= world) return nullptr;
+    Shard* S = new (std::nothrow) Shard();
+    if (!S) return nullptr;
+    if (hipGetDevice(&S->dev) != hipSuccess) { delete S; return nullptr; }
+    S->L = L;
+    S->kw = acx_key_words(L);
+    S->cyc = cyclical != 0;
+    S->rank = rank;
+    S->world = world;
+    S->lcap = local_cap;
+    if (chunk_parents <= 0) chunk_parents = 1 << 21;
+    if (chunk_parents > (1 << 24)) { delete S; return nullptr; }
+    S->pmax = chunk_parents;
+    S->rcap = 12 * S->pmax;  // every child of a chunk may have this owner
+    uint64_t ts = 1024;
+    while (ts < 2 * (uint64_t)(S->lcap + S->rcap)) ts <<= 1;
+    if (ts > (1ull << 31)) { delete S; return nullptr; }
+    S->tsize = ts;
+    Args& a = S->a;
+    const int64_t nb = nblocks(S->pmax);
+    const int64_t pl = S->pmax < S->lcap ? S->pmax : S->lcap;  // local parents per chunk
+    bool ok = dalloc(a.lkeys, (size_t)(S->lcap * S->kw)) && dalloc(a.lgid, (size_t)S->lcap) &&
+              dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
+              dalloc(a.ckeys, (size_t)(12 * pl * S->kw)) && dalloc(a.cown, (size_t)(12 * pl)) &&
+              dalloc(a.pmin, (size_t)pl) && dalloc(a.map, (size_t)S->rcap) && dalloc(a.rslot, (size_t)S->rcap) &&
+              dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
+              dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
+              hipHostMalloc((void**)&S->ctl_host, sizeof(Ctl), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&S->look_host, 4 * sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        delete S;
+        return nullptr;
+    }
+    a.mask = ts - 1;
+    a.lcap = S->lcap;
+    a.L = L;
+    a.kw = S->kw;
+    a.cyc = S->cyc;
+    a.world = world;
+    return S;
+}
+
+void acx_sbfs_destroy(void* h) { delete static_cast<Shard*>(h); }
+
+int64_t acx_sbfs_max_records(void* h) {
+    Shard* S = static_cast<Shard*>(h);
+    return S ? S->rcap : ACX_E_ARG;
+}
+
+int32_t acx_sbfs_owner(const int32_t* presentation, int32_t L, int32_t world) {
+    if (!presentation || L < 1 || L > ACX_MAX_L || world < 1 || world > MAXW) return ACX_E_ARG;
+    constexpr int KM = ACX_MAX_L / 16 + 2;
+    const int kw = acx_key_words(L);
+    Key<KM> k{};
+    pack_key(presentation, L, kw, k.w);
+    const uint64_t hv = khash<KM>(k, kw);
+    return (int32_t)(((hv >> 32) * (uint64_t)world) >> 32);
+}
+
+int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !presentation) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int own = acx_sbfs_owner(presentation, S->L, S->world);
+    if (own < 0) return own;
+    S->nloc = 0;
+    S->lo = 0;
+    S->a.nloc = 0;
+    if (hipMemsetAsync(S->a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (own == S->rank) {
+        uint64_t root[ACX_MAX_L / 16 + 2];
+        pack_key(presentation, S->L, S->kw, root);
+        if (hipMemcpyAsync(S->a.lkeys, root, (size_t)S->kw * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return ACX_E_LAUNCH;
+        RootLaunch rl{S, st};
+        by_nw(S->L, rl);
+        S->nloc = 1;
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+    return own;
+}
+
+// out (int64[5 + world]): succ_seq, err_seq, min_len, local parents, overflow, send counts
+int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !out || P < 1 || P > S->pmax || head < 0) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    Args& a = S->a;
+    S->head = head;
+    S->P = P;
+    const int64_t avail = S->nloc - S->lo;
+    S->Pr = (int)(avail < P ? avail : P);
+    a.head = head;
+    a.P = P;
+    a.Pr = S->Pr;
+    a.lo = S->lo;
+    a.nloc = S->nloc;
+    Ctl init;
+    memset(&init, 0, sizeof(init));
+    init.succ_seq = init.err_seq = init.min_len = init.cut_p = NONE;
+    *S->ctl_host = init;
+    if (hipMemcpyAsync(a.ctl, S->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (S->Pr > 0) {
+        ExpandLaunch el{S, st};
+        by_nw(S->L, el);
+    }
+    const int r = sync_ctl(S, st);
+    if (r != ACX_OK) return r;
+    const Ctl& c = *S->ctl_host;
+    out[0] = c.succ_seq;
+    out[1] = c.err_seq;
+    out[2] = c.min_len;
+    out[3] = c.npar;
+    out[4] = c.overflow;
+    for (int i = 0; i < S->world; ++i) out[5 + i] = c.cnt[i];
+    return ACX_OK;
+}
+
+// the expanded children into `send` ((sum of counts, kw + 1) uint64), grouped by owner rank
+int acx_sbfs_pack(void* h, uint64_t* send, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !send) return ACX_E_ARG;
+    if (S->Pr == 0) return ACX_OK;
+    S->a.send = send;
+    sbfs_pack_kernel<<<dim3(nblocks(S->Pr)), dim3(TPB), 0, (hipStream_t)stream>>>(S->a);
+    return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+}
+
+// received records ((nrecv, kw + 1) uint64) -> probe / insert; this rank's survivors as bits
+// of gmask ((P) int32, zeroed here).  end = min(success seq, move-error seq) over all ranks.
+int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, uint32_t* gmask, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !gmask || nrecv < 0 || nrecv > S->rcap || (nrecv > 0 && !recv)) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    Args& a = S->a;
+    a.recv = recv;
+    a.nrecv = nrecv;
+    a.gmask = gmask;
+    a.end = end < 0 || end > (int64_t)NONE ? NONE : (uint32_t)end;
+    S->nrecv = nrecv;
+    if (hipMemsetAsync(a.map, 0xff, (size_t)12 * S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMemsetAsync(gmask, 0, (size_t)S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (nrecv > 0) {
+        sbfs_map_kernel<<<dim3(nblocks(nrecv)), dim3(TPB), 0, st>>>(a);
+        InsertLaunch il{S, st};
+        by_nw(S->L, il);
+        sbfs_mark_kernel<<<dim3(nblocks(nrecv)), dim3(TPB), 0, st>>>(a);
+    }
+    return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+}
+
+// gmask = the all-reduced survivor masks.  out (int64[5]): nodes appended by the chunk (all
+// ranks), cut parent (-1: none), len(tree_nodes) after the cut parent, nodes appended here,
+// overflow flags
+int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t need, int64_t* out, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !gmask || !out) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    Args& a = S->a;
+    a.gmask = (uint32_t*)gmask;
+    a.n_before = n_before;
+    a.need = need;
+    a.nloc = S->nloc;
+    const int nb = nblocks(S->P);
+    sbfs_count_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
+    sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.bsum, nb, &a.ctl->total_new);
+    sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.lbsum, nb, &a.ctl->local_new);
+    sbfs_commit_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
+    const int r = sync_ctl(S, st);
+    if (r != ACX_OK) return r;
+    const Ctl& c = *S->ctl_host;
+    out[0] = (int64_t)c.total_new;
+    out[1] = c.cut_p == NONE ? -1 : (int64_t)c.cut_p;
+    out[2] = (int64_t)c.nodes_at_cut;
+    out[3] = (int64_t)c.local_new;
+    out[4] = c.overflow;
+    S->nloc += c.stored;
+    S->lo += c.npar;
+    return ACX_OK;
+}
+
+// min child total over this rank's parents of the last chunk with chunk index <= last (255: none)
+int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t init = NONE;
+    if (hipMemcpyAsync(&S->a.ctl->min_len, &init, 4, hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+    // npar is read on the device; lo was advanced by commit
+    Args a = S->a;
+    a.lo = S->lo - S->ctl_host->npar;
+    if (S->Pr > 0) sbfs_minlen_kernel<<<dim3(nblocks(S->Pr)), dim3(TPB), 0, st>>>(a, last);
+    const int r = sync_ctl(S, st);
+    if (r != ACX_OK) return r;
+    return S->ctl_host->min_len == NONE ? 255 : (int64_t)S->ctl_host->min_len;
+}
+
+// node with global id g if this rank stores it: out (int64[4]) = found, parent id, action, total
+int acx_sbfs_lookup(void* h, int64_t g, int64_t* out, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !out) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    S->a.nloc = S->nloc;
+    LookupLaunch ll{S, st, g};
+    by_nw(S->L, ll);
+    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMemcpyAsync(S->look_host, S->a.look, 32, hipMemcpyDeviceToHost, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+    for (int i = 0; i < 4; ++i) out[i] = S->look_host[i];
+    return ACX_OK;
+}
+
+// this rank's stored nodes: keys (cap, kw) and global ids (cap), ascending id; returns the count
+int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S) return ACX_E_ARG;
+    const int64_t n = S->nloc < cap ? S->nloc : cap;
+    if (n > 0 && keys && hipMemcpy(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return ACX_E_LAUNCH;
+    if (n > 0 && gids && hipMemcpy(gids, S->a.lgid, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return ACX_E_LAUNCH;
+    return S->nloc;
+}
+
+}  // extern "C"

@@ -212,6 +212,47 @@ void acx_bfs_destroy(void* h);
 int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
 
 /*
+ * Breadth-first search with the node store and the visited set partitioned over G GPUs by key
+ * owner (one process per GPU).  Same results as acx_bfs_run / the
+ * reference bfs (breadth_first.py:15-97).  The caller runs the same chunk loop on every rank
+ * (acx/search/_sharded_bfs.py) and does the exchanges between the calls:
+ *   acx_sbfs_create    workspace on the current device: this rank's node store (local_cap
+ *                      nodes), chunks of <= chunk_parents parents (<= 0: 2^21); NULL on failure
+ *   acx_sbfs_owner     owner rank of a presentation's key (HOST pointer)
+ *   acx_sbfs_reset     new search from `presentation` (HOST); returns the root's owner rank
+ *   acx_sbfs_expand    expands this rank's parents among global ids [head, head + P);
+ *                      out int64[5 + world] = success seq, move-error seq (0xffffffff: none),
+ *                      min child total, local parents, overflow, children per owner
+ *   acx_sbfs_pack      those children into `send` ((n, kw + 1) uint64: key words, chunk seq),
+ *                      grouped by owner in rank order
+ *   -- all_to_all of the records: recv holds the records every rank sent to this one --
+ *   acx_sbfs_insert    probe / claim the visited set with the received records up to seq
+ *                      `end`; survivors as bits of gmask ((P) uint32, zeroed by the call)
+ *   -- all_reduce (sum) of gmask over the ranks --
+ *   acx_sbfs_commit    global ids, the node-budget cut and the appends; out int64[5] = nodes
+ *                      appended (all ranks), cut parent (-1: none), nodes after the cut
+ *                      parent, nodes appended here, overflow flags
+ *   acx_sbfs_min_len   min child total over this rank's parents of the last chunk up to `last`
+ *   acx_sbfs_lookup    out int64[4] = found, parent id, action, total of the node with id g
+ *   acx_sbfs_node_keys this rank's nodes (keys, global ids; ascending id); returns the count
+ *   acx_sbfs_max_records  capacity of send / recv in records (12 * chunk_parents)
+ * All calls are on `stream`; expand, commit, min_len, lookup and reset synchronise it.
+ */
+void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32_t cyclical, int32_t rank,
+                      int32_t world);
+void acx_sbfs_destroy(void* h);
+int64_t acx_sbfs_max_records(void* h);
+int32_t acx_sbfs_owner(const int32_t* presentation, int32_t L, int32_t world);
+int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream);
+int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream);
+int acx_sbfs_pack(void* h, uint64_t* send, void* stream);
+int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, uint32_t* gmask, void* stream);
+int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t need, int64_t* out, void* stream);
+int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream);
+int acx_sbfs_lookup(void* h, int64_t g, int64_t* out, void* stream);
+int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap);
+
+/*
  * Scoring inputs for value-guided search (value_search/): exactly one of `states` ((M,2L) int32)
  * or `keys` ((M, acx_key_words(L)) packed keys, e.g. acx_expand12 output) is non-NULL.
  *   acx_features   out (M,14) float32 = compute_features (feature_extraction.py:11-91); with
