@@ -93,7 +93,7 @@ def _handle(lib, dev, L, cyc, chunk, lcap, rank, world):
     nrec = lib.acx_sbfs_max_records(ptr)
     kw = _lib.key_words(L)
     send = torch.empty(nrec * (kw + 1), dtype=torch.int64, device=dev)
-    recv = torch.empty(nrec * (kw + 1), dtype=torch.int64, device=dev)
+    recv = torch.empty(nrec * (kw + 1) if world > 1 else 0, dtype=torch.int64, device=dev)
     mask = torch.empty(max(int(chunk), 1), dtype=torch.int32, device=dev)
     h = (ptr, send, recv, mask)
     _HANDLES[key] = h
@@ -165,10 +165,12 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
             recv_counts = rows[:, 5 + comm.rank]
             nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
             ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
-            comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
-                            [int(c) * rw for c in send_counts])
+            if W > 1:
+                comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
+                                [int(c) * rw for c in send_counts])
+            src = recv if W > 1 else send  # one rank: the records it sent are the ones it owns
             end = min(succ_seq, err_seq)
-            ok(lib.acx_sbfs_insert(h, recv.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
+            ok(lib.acx_sbfs_insert(h, src.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
             comm.all_reduce_sum_(gmask[:P])
             ok(lib.acx_sbfs_commit(h, gmask.data_ptr(), n_nodes, max_nodes - n_nodes, com_out.ctypes.data, stream),
                "acx_sbfs_commit")

@@ -382,8 +382,9 @@ struct PresRegs {
 };
 
 // packed key: r0 letters, r1 letters, n0 (8 bits), n1 (8 bits); KW64 uint64 words
+// the packed key in registers: out[k] for k < NW + 1 (words >= kw64 are zero)
 template <int NW>
-__device__ __forceinline__ void store_key(uint64_t* dst, int kw64, int L, const PresRegs<NW>& p) {
+__device__ __forceinline__ void make_key(int L, const PresRegs<NW>& p, uint64_t (&out)[NW + 1]) {
     constexpr int KN = 2 * NW + 2;
     Word<KN> k0 = wzero<KN>(), k1 = wzero<KN>(), kl = wzero<KN>();
 #pragma unroll
@@ -391,8 +392,16 @@ __device__ __forceinline__ void store_key(uint64_t* dst, int kw64, int L, const 
     kl.w[0] = (uint32_t)p.n0 | ((uint32_t)p.n1 << 8);
     const Word<KN> key = wor<KN>(wor<KN>(k0, wshl<KN>(k1, 2 * L)), wshl<KN>(kl, 4 * L));
 #pragma unroll
-    for (int k = 0; k < KN / 2; ++k)
-        if (k < kw64) dst[k] = (uint64_t)key.w[2 * k] | ((uint64_t)key.w[2 * k + 1] << 32);
+    for (int k = 0; k < KN / 2; ++k) out[k] = (uint64_t)key.w[2 * k] | ((uint64_t)key.w[2 * k + 1] << 32);
+}
+
+template <int NW>
+__device__ __forceinline__ void store_key(uint64_t* dst, int kw64, int L, const PresRegs<NW>& p) {
+    uint64_t key[NW + 1];
+    make_key<NW>(L, p, key);
+#pragma unroll
+    for (int k = 0; k < NW + 1; ++k)
+        if (k < kw64) dst[k] = key[k];
 }
 
 template <int NW>

@@ -96,8 +96,12 @@ __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
     __syncthreads();
     const int j = blockIdx.x * TPB + threadIdx.x;
     const int64_t gid = j < a.Pr ? a.lgid[a.lo + j] : INT64_MAX;
-    if (gid < a.head + a.P) {
-        atomicMax(&a.ctl->npar, (uint32_t)(j + 1));
+    const bool live = gid < a.head + a.P;
+    uint8_t own[12];
+#pragma unroll
+    for (int act = 0; act < 12; ++act) own[act] = 0xff;
+    uint32_t mn_lane = NONE;
+    if (live) {
         PresRegs<NW> pr;
         load_key<NW>(a.lkeys + (a.lo + j) * a.kw, a.kw, a.L, pr);
         const bool cyc = a.cyc != 0;
@@ -117,26 +121,48 @@ __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
                 if (tot == 2 && succ == NONE) succ = s;
                 mn = tot < mn ? tot : mn;
             }
+            Key<NW + 1> key;
+            make_key<NW>(a.L, q, key.w);
             uint64_t* dst = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
-            store_key<NW>(dst, a.kw, a.L, q);
-            const uint32_t o = owner_of(khash<NW + 1>(kload<NW + 1>(dst, a.kw), a.kw), a.world);
-            a.cown[(int64_t)act * a.Pr + j] = (uint8_t)o;
-            atomicAdd(&hist[o], 1u);
+#pragma unroll
+            for (int k = 0; k < NW + 1; ++k)
+                if (k < a.kw) dst[k] = key.w[k];
+            own[act] = (uint8_t)owner_of(khash<NW + 1>(key, a.kw), a.world);
+            a.cown[(int64_t)act * a.Pr + j] = own[act];
         }
         a.pmin[j] = (uint8_t)mn;
+        mn_lane = (uint32_t)mn;
         if (succ != NONE) atomicMin(&a.ctl->succ_seq, succ);
         if (err != NONE) atomicMin(&a.ctl->err_seq, err);
-        atomicMin(&a.ctl->min_len, (uint32_t)mn);
     } else if (j < a.Pr) {
         for (int act = 0; act < 12; ++act) a.cown[(int64_t)act * a.Pr + j] = 0xff;
     }
+    // per-owner counts: one ballot per (action, owner) and one LDS add per wave, instead of a
+    // same-address LDS atomic per child
+    const int lane = threadIdx.x & (WAVE - 1);
+    for (int o = 0; o < a.world; ++o) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int act = 0; act < 12; ++act) c += __popcll(__ballot(own[act] == o));
+        if (lane == 0 && c) atomicAdd(&hist[o], c);
+    }
+    // chunk min length and local parent count: one atomic per block (a same-address atomic per
+    // lane serialises in L2)
+    __shared__ uint32_t sh[TPB / WAVE];
+    const uint32_t bmin = block_min(mn_lane, sh);
     __syncthreads();
+    const uint32_t bpar = block_min(live ? NONE - (uint32_t)(j + 1) : NONE, sh);
+    if (threadIdx.x == 0) {
+        if (bmin != NONE) atomicMin(&a.ctl->min_len, bmin);
+        if (bpar != NONE) atomicMax(&a.ctl->npar, NONE - bpar);
+    }
     for (int i = threadIdx.x; i < a.world; i += TPB)
         if (hist[i]) atomicAdd(&a.ctl->cnt[i], hist[i]);
 }
 
 // (2) records into the send buffer, grouped by owner (order within a group is arbitrary:
-// the owner indexes records by seq)
+// the owner indexes records by seq).  Positions are wave-aggregated: per (action, owner) a
+// ballot ranks the lanes and lane 0 reserves the wave's run with one LDS add (broadcast by shfl).
 __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
     __shared__ uint32_t hist[MAXW], base[MAXW], off[MAXW];
     if (threadIdx.x == 0) {
@@ -149,12 +175,25 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
     for (int i = threadIdx.x; i < a.world; i += TPB) hist[i] = 0;
     __syncthreads();
     const int j = blockIdx.x * TPB + threadIdx.x;
-    uint32_t loc[12];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const uint64_t below = (1ull << lane) - 1ull;
     uint8_t own[12];
+    uint32_t loc[12];
 #pragma unroll
     for (int act = 0; act < 12; ++act) {
         own[act] = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : (uint8_t)0xff;
-        loc[act] = own[act] != 0xff ? atomicAdd(&hist[own[act]], 1u) : 0u;
+        loc[act] = 0;
+    }
+    // each (action, owner) run of the wave gets a block-local offset in hist[owner]
+    for (int o = 0; o < a.world; ++o) {
+#pragma unroll
+        for (int act = 0; act < 12; ++act) {
+            const uint64_t m = __ballot(own[act] == o);
+            if (!m) continue;
+            uint32_t b = lane == 0 ? atomicAdd(&hist[o], (uint32_t)__popcll(m)) : 0u;
+            b = (uint32_t)__shfl((int)b, 0, WAVE);
+            if (own[act] == o) loc[act] = b + (uint32_t)__popcll(m & below);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.world; i += TPB) base[i] = hist[i] ? atomicAdd(&a.ctl->cur[i], hist[i]) : 0u;
@@ -342,9 +381,12 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
 
 // min child total over the local parents of the chunk with p <= last
 __global__ __launch_bounds__(TPB) void sbfs_minlen_kernel(Args a, int64_t last) {
+    __shared__ uint32_t sh[TPB / WAVE];
     const int j = blockIdx.x * TPB + threadIdx.x;
-    if (j >= (int)a.ctl->npar) return;
-    if (a.lgid[a.lo + j] - a.head <= last) atomicMin(&a.ctl->min_len, (uint32_t)a.pmin[j]);
+    uint32_t v = NONE;
+    if (j < (int)a.ctl->npar && a.lgid[a.lo + j] - a.head <= last) v = a.pmin[j];
+    v = block_min(v, sh);
+    if (threadIdx.x == 0 && v != NONE) atomicMin(&a.ctl->min_len, v);
 }
 
 // the stored node with global id g: found, parent id, action, total length

@@ -25,6 +25,8 @@ per-env ACEnv.step call pattern -- one process per host core (bounded at 16), 64
 from __future__ import annotations
 
 import argparse
+import contextlib
+import io
 import json
 import os
 import subprocess
@@ -150,6 +152,7 @@ def main():
     ap.add_argument("--no-step-api", action="store_true")
     ap.add_argument("--no-learner", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-bfs", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -338,6 +341,38 @@ def main():
                          "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb},
         }
         del lobs, lrew, ldone, lenv
+
+    if not args.no_bfs:
+        # BASELINE configs[3] on the owner-partitioned BFS (csrc/acx_sbfs.hip): AK(3), L = 36, to
+        # 10^7 nodes; node store + visited set sharded over the ranks by key owner, per-chunk RCCL
+        # all_gather / all_to_all / all_reduce (world 1: the exchanges are local copies)
+        from acx.envs.utils import convert_relators_to_presentation
+        from acx.search import _sharded_bfs as SB
+        ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
+        nb = 10 ** 7
+        with contextlib.redirect_stdout(io.StringIO()):
+            SB.sharded_bfs(ak3, nb, device=dev)  # warmup: workspace allocation
+        best = None
+        for _ in range(3):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(io.StringIO()):
+                res = SB.sharded_bfs(ak3, nb, device=dev)
+            torch.cuda.synchronize()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            best = el.item() if best is None else min(best, el.item())
+        st = SB.LAST_STATS
+        variants["sharded_bfs"] = {
+            "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],
+            "parents_expanded": st["parents"], "chunks": st["chunks"], "result": list(res) if res[0] else [False, None],
+            "workload": "BASELINE configs[3]: bfs from AK(3), L=36, cyclical=False, to 10^7 nodes; node store and "
+                        f"visited set partitioned by key owner over {world} rank(s), RCCL exchanges per chunk",
+        }
+        SB.release_workspaces()
 
     # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
