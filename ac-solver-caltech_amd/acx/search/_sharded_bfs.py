@@ -117,7 +117,7 @@ def local_capacity(max_nodes: int, world: int) -> int:
 def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
                 device=None, chunk=0, group=None, keep_node_keys=False):
     """(True, path) | (False, None), as breadth_first.py:15-97; SPMD over the ranks of `group`
-    (default: the default process group, if initialised).  chunk = parents per round (0: 2^21).
+    (default: the default process group, if initialised).  chunk = parents per round (0: 2^19).
     keep_node_keys: LAST_STATS["node_keys"] / ["node_ids"] = this rank's nodes (ascending id)."""
     p = np.asarray(presentation)
     assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
@@ -131,7 +131,7 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     comm = _Comm(group, dev)
-    chunk = int(chunk) if chunk else 1 << 21
+    chunk = int(chunk) if chunk else 1 << 19
     lcap = local_capacity(max_nodes, comm.world)
     lib = _lib.load()
     h, send, recv, gmask = _handle(lib, dev, L, cyclically_reduce_after_moves, chunk, lcap, comm.rank,

@@ -358,7 +358,7 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     S->cyc = cyclical != 0;
     S->max_nodes = max_nodes;
     S->qcap = max_nodes + 12;
-    if (chunk_parents <= 0) chunk_parents = 1 << 21;
+    if (chunk_parents <= 0) chunk_parents = 1 << 19;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
     S->pmax = chunk_parents < S->qcap ? chunk_parents : S->qcap;
     // every node and every claimed chunk slot at load <= 1/2
     uint64_t ts = 1024;

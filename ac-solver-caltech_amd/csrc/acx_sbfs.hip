@@ -501,7 +501,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     S->rank = rank;
     S->world = world;
     S->lcap = local_cap;
-    if (chunk_parents <= 0) chunk_parents = 1 << 21;
+    if (chunk_parents <= 0) chunk_parents = 1 << 19;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
     if (chunk_parents > (1 << 24)) { delete S; return nullptr; }
     S->pmax = chunk_parents;
     S->rcap = 12 * S->pmax;  // every child of a chunk may have this owner

@@ -188,7 +188,7 @@ int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out,
  * with identical results): FIFO queue of packed node keys and the visited set (open-addressing
  * hash table) in HBM; the 12-way expansion, dedup against the visited set and within the chunk
  * (first occurrence in (parent, action) order wins), the success test and the per-parent node
- * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^21).
+ * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^19).
  *   acx_bfs_create   allocates the device workspace on the current device for searches of
  *                    up to max_nodes nodes (<= 2^30) at max_relator_length L; NULL on failure.
  *   acx_bfs_run      searches from `presentation` (HOST pointer, 2L int32, a valid presentation
@@ -217,7 +217,7 @@ int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
  * reference bfs (breadth_first.py:15-97).  The caller runs the same chunk loop on every rank
  * (acx/search/_sharded_bfs.py) and does the exchanges between the calls:
  *   acx_sbfs_create    workspace on the current device: this rank's node store (local_cap
- *                      nodes), chunks of <= chunk_parents parents (<= 0: 2^21); NULL on failure
+ *                      nodes), chunks of <= chunk_parents parents (<= 0: 2^19); NULL on failure
  *   acx_sbfs_owner     owner rank of a presentation's key (HOST pointer)
  *   acx_sbfs_reset     new search from `presentation` (HOST); returns the root's owner rank
  *   acx_sbfs_expand    expands this rank's parents among global ids [head, head + P);

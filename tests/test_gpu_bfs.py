@@ -21,7 +21,7 @@ def _ak3(L):
     return convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], L)
 
 
-@pytest.mark.parametrize("chunk", [0, 1, 3, 64])
+@pytest.mark.parametrize("chunk", [0, 1, 3, 64, 1 << 21])
 def test_device_bfs_random_reference_searches(chunk):
     from acx.search._device_bfs import LAST_STATS, device_bfs
     with open(os.path.join(GOLDEN, "kat_search_extra.json")) as f:
