@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("ACX_LIB", os.path.join(HERE, "libacx.so"))
 
 OK, E_ARG, E_LAUNCH = 0, -1, -2
 BFS_EXHAUSTED, BFS_FOUND, BFS_BUDGET, BFS_MOVE_ERROR = 0, 1, 2, 3
-ERR_NONE, ERR_INVALID, ERR_EMPTY_CONJ, ERR_DOMAIN, ERR_ACTION = 0, 1, 2, 3, 4
+ERR_NONE, ERR_INVALID, ERR_EMPTY_CONJ, ERR_DOMAIN, ERR_ACTION, ERR_PAD = 0, 1, 2, 3, 4, 9
 MAX_L = 128
 
 # every entry point declared in include/acx.h, with its ctypes signature
@@ -38,6 +38,12 @@ SIGNATURES = {
     "acx_expand12": ([_P] * 6 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_canonicalize": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_unpack_keys": ([_P] * 3 + [_I64, _I32, _P], ctypes.c_int),
+    # exact word functions on arbitrary letters (ac-solver-caltech_amd/csrc/acx_words.hip)
+    "acx_word_move": ([_P] * 7 + [_I64, _I32, _I32, _P], ctypes.c_int),
+    "acx_concatenate": ([_P] * 4 + [_I64, _I32, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_conjugate": ([_P] * 6 + [_I64, _I32, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_word_simplify_presentation": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),
+    "acx_word_simplify_relator": ([_P, _I32] + [_P] * 5 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_key_words": ([_I32], ctypes.c_int32),
     "acx_version": ([], ctypes.c_char_p),
     "acx_features": ([_P] * 5 + [_I64, _I32, _P], ctypes.c_int),
@@ -51,11 +57,15 @@ SIGNATURES = {
     "acx_search_path": ([_P, _P, _P, _I64], ctypes.c_int64),
     "acx_search_node_keys": ([_P, _P, _I64], ctypes.c_int64),
     "acx_search_stats": ([_P, _P], None),
+    "acx_search_min_trace": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_search_popped": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_search_found": ([_P, _P, _P], ctypes.c_int32),
     # device BFS (ac-solver-caltech_amd/csrc/acx_bfs.hip)
     "acx_bfs_create": ([_I32, _I64, _I64, _I32], ctypes.c_void_p),
     "acx_bfs_run": ([_P, _P, _I64, _P, _P, _I64, _P, _P], ctypes.c_int),
     "acx_bfs_destroy": ([_P], None),
     "acx_bfs_node_keys": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_bfs_min_trace": ([_P, _P, _I64], ctypes.c_int64),
     # owner-partitioned multi-GPU BFS (ac-solver-caltech_amd/csrc/acx_sbfs.hip)
     "acx_sbfs_create": ([_I32, _I64, _I64, _I32, _I32, _I32], ctypes.c_void_p),
     "acx_sbfs_destroy": ([_P], None),

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
-from .ac_moves import raise_for_err
+from .ac_moves import in_packed_domain, raise_for_err
 from .utils import is_array_valid_presentation
 
 
@@ -102,7 +102,6 @@ class ACEnv:
         self.horizon_length = config.horizon_length
         if config.use_supermoves:
             raise NotImplementedError("ACEnv with supermoves is not yet implemented in this library.")
-        _check_domain(self.initial_state)
         L = self.max_relator_length
         self.observation_space = Box(np.full(2 * L, -self.n_gen, np.int8), np.full(2 * L, self.n_gen, np.int8))
         self.action_space = Discrete(12)
@@ -124,6 +123,9 @@ class ACEnv:
     def _set_state(self, state: np.ndarray) -> None:
         L = self.max_relator_length
         self.state = np.asarray(state)
+        # letters +-1/+-2 with zeros only as right padding: the packed step kernel (acx_step);
+        # anything else the reference accepts (other integer letters): the exact word kernel
+        self._packed = in_packed_domain(self.state, L)
         self._state.copy_(torch.as_tensor(self.state.astype(np.int32)).reshape(1, 2 * L))
         self.lengths = [int(np.count_nonzero(self.state[i * L : (i + 1) * L])) for i in range(self.n_gen)]
         self.count_steps = 0
@@ -137,6 +139,8 @@ class ACEnv:
     def step(self, action):
         self.actions += [action]
         self._action.fill_(int(action))
+        if not self._packed:
+            return self._step_words()
         ops.step(self._state, self._action, state_out=self._state, step_count=self._count,
                  horizon=self.horizon_length, cyclical=True, reward=self._reward, done=self._done,
                  truncated=self._trunc, lengths=self._lens, err=self._err)
@@ -151,10 +155,25 @@ class ACEnv:
         self.count_steps += 1
         return self.state, reward, done, truncated, ({"actions": self.actions.copy()} if done else {})
 
+    def _step_words(self):
+        """ac_env.py:91-111 for states outside the packed domain: acx_word_move (ACMove with
+        cyclical=True, exact on any integer letters) + the env's reward / truncation bookkeeping."""
+        L = self.max_relator_length
+        out, lens, done, err = ops.word_move(self._state, self._action, cyclical=True)
+        host = torch.cat([out.reshape(-1), lens.reshape(-1), done.to(torch.int32), err.to(torch.int32)]).cpu().numpy()
+        raise_for_err(int(host[-1]), "ACEnv.step")
+        self._state.copy_(out)
+        self.state = host[: 2 * L].astype(self._dtype)
+        self.lengths = [int(host[2 * L]), int(host[2 * L + 1])]
+        done = bool(host[2 * L + 2])
+        reward = self.max_reward * done - sum(self.lengths) * (1 - done)
+        self.count_steps += 1
+        truncated = self.count_steps >= self.horizon_length
+        return self.state, reward, done, truncated, ({"actions": self.actions.copy()} if done else {})
+
     def reset(self, *, seed=None, options=None):
         start = options["starting_state"] if options and "starting_state" in options else self.initial_state
         start = np.copy(start)
-        _check_domain(start)
         self._set_state(start)
         self.actions = []
         return self.state, {}

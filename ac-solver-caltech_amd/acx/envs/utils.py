@@ -5,8 +5,9 @@ Format (utils.py:1-8): a balanced presentation is an even-length array, relator 
 first half and r1 in the second, letters +-1 (x) / +-2 (y), zeros only as right padding.
 
 The setup-time helpers (validation, triviality, padding, conversion) are host numpy; the
-word reductions (`simplify_presentation`, `simplify_relator`) run on the GPU through
-acx_canonicalize -- they are the same reduction the step kernel fuses.
+word reductions (`simplify_presentation`, `simplify_relator`) run on the GPU through the exact
+int32-letter kernels (acx_word_simplify_*, csrc/acx_words.hip), so they accept any integer
+letters as the reference does; batched reduction of +-1/+-2 presentations is acx.ops.canonicalize.
 """
 
 from __future__ import annotations
@@ -83,46 +84,39 @@ def _device(device):
 
 
 def simplify_presentation(presentation, max_relator_length, lengths_of_words=None, cyclical=True, device=None):
-    """utils.py:246-283 on the GPU (acx_canonicalize).  Returns (presentation, [n0, n1]).
-
-    Raises AssertionError for an invalid presentation, as the reference does."""
-    p = np.asarray(presentation)
+    """utils.py:246-283 on the GPU (acx_word_simplify_presentation: exact on any integer letters).
+    Returns (presentation, [n0, n1]); raises AssertionError for an invalid presentation, as the
+    reference does."""
+    p = np.array(presentation)
     L = int(max_relator_length)
-    assert len(p) == 2 * L
     assert is_array_valid_presentation(p), (
         f"{p} is not a valid presentation. Expect all zeros to be padded to the right."
     )
+    assert len(p) == 2 * L
     t = torch.as_tensor(p.astype(np.int32)).reshape(1, 2 * L).to(_device(device))
-    out, lens, err = ops.canonicalize(t, cyclical=bool(cyclical))
-    e = int(err.item())
-    if e == 3:
-        raise ValueError("letters outside {-2,-1,1,2} are outside the acx kernel domain")
-    assert e == 0
-    return out[0].cpu().numpy().astype(p.dtype), [int(v) for v in lens[0].tolist()]
+    out, lens, err = ops.word_simplify_presentation(t, cyclical=bool(cyclical))
+    host = torch.cat([out.reshape(-1), lens.reshape(-1), err.to(torch.int32)]).cpu().numpy()
+    _raise(int(host[-1]))
+    return host[: 2 * L].astype(p.dtype), [int(host[2 * L]), int(host[2 * L + 1])]
+
+
+def _raise(code: int) -> None:
+    from .ac_moves import raise_for_err
+    raise_for_err(code, "simplify")
 
 
 def simplify_relator(relator, max_relator_length, cyclical=False, padded=True, device=None):
-    """utils.py:178-243 for one relator (letters +-1, +-2), on the GPU.  Returns (relator, length)."""
-    r = np.asarray(relator)
-    n = int(np.count_nonzero(r))
-    if len(r) > n:
-        assert (r[n:] == 0).all(), "expect all zeros to be at the right end"
-    L = int(max(max_relator_length, len(r), 1))
-    if n == 0:
-        out = np.zeros(max_relator_length if padded else 0, dtype=r.dtype if r.size else np.int64)
-        return out, 0
-    pres = np.zeros(2 * L, dtype=np.int32)
-    pres[:n] = r[:n]
-    pres[L] = 1  # a placeholder second relator
-    t = torch.as_tensor(pres).reshape(1, 2 * L).to(_device(device))
-    out, lens, err = ops.canonicalize(t, cyclical=bool(cyclical))
-    e = int(err.item())
-    if e == 3:
-        raise ValueError("letters outside {-2,-1,1,2} are outside the acx kernel domain")
-    assert e == 0
-    m = int(lens[0, 0].item())
-    word = out[0, :m].cpu().numpy().astype(r.dtype)
-    assert max_relator_length >= m, "Increase max length! Length of simplified word is bigger than maximum allowed length."
-    if padded:
-        word = np.pad(word, (0, max_relator_length - len(word)))
-    return word, m
+    """utils.py:178-243 on the GPU (acx_word_simplify_relator: exact on any integer letters, and on
+    arrays longer than max_relator_length).  Returns (relator, length) like the reference: the
+    reduced array, padded with zeros to max_relator_length when `padded`, else the array after the
+    deletions (its trailing zeros included)."""
+    assert isinstance(relator, np.ndarray), "expect relator to be a numpy array"
+    r = relator
+    m = int(r.shape[0])
+    L = int(max_relator_length)
+    t = torch.as_tensor(r.astype(np.int32)).reshape(1, m).to(_device(device))
+    out, ol, n, err = ops.word_simplify_relator(t, L, cyclical=bool(cyclical), padded=bool(padded))
+    w = out.shape[1]
+    host = torch.cat([out.reshape(-1), ol, n, err.to(torch.int32)]).cpu().numpy()
+    _raise(int(host[-1]))
+    return host[: int(host[w])].astype(r.dtype), int(host[w + 1])

@@ -298,3 +298,96 @@ def token_ids(*, states: Optional[torch.Tensor] = None, keys: Optional[torch.Ten
     st = lib.acx_token_ids(_ptr(states), _ptr(keys), _ptr(out), M, L, D, _stream(dev))
     _lib.check(st, "acx_token_ids")
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# exact word functions on arbitrary int32 letters (csrc/acx_words.hip)
+# ---------------------------------------------------------------------------------------------
+def _word_setup(states: torch.Tensor, name: str):
+    _need_gpu(states, name)
+    if states.dim() != 2 or states.shape[1] % 2 or states.shape[1] == 0:
+        raise ValueError(f"{name} must be (B, 2L), got {tuple(states.shape)}")
+    if states.dtype != _INT32 or not states.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous int32 tensor")
+    return states.shape[0], states.shape[1] // 2, states.device
+
+
+def word_move(states: torch.Tensor, action: torch.Tensor, *, cyclical: bool = True):
+    """acx_word_move: ACMove (ac_moves.py:159-231) on arbitrary letters, one move id per row.
+    Returns (out, lengths (B,2), done (B) strict triviality, err (B) ACX_ERR_* codes)."""
+    lib = _lib.load()
+    B, L, dev = _word_setup(states, "states")
+    _check(action, "action", _INT32, (B,), dev)
+    out = torch.empty_like(states)
+    lens = torch.empty((B, 2), dtype=_INT32, device=dev)
+    done = torch.empty(B, dtype=_UINT8, device=dev)
+    err = torch.empty(B, dtype=_UINT8, device=dev)
+    st = lib.acx_word_move(_ptr(states), _ptr(out), _ptr(action), _ptr(lens), _ptr(done), _ptr(err), None, B, L,
+                           int(bool(cyclical)), _stream(dev))
+    _lib.check(st, "acx_word_move")
+    return out, lens, done, err
+
+
+def concatenate(states: torch.Tensor, i: int, j: int, sign: int, lengths: Optional[torch.Tensor] = None):
+    """acx_concatenate: concatenate_relators (ac_moves.py:4-76) over a batch, r_i <- r_i r_j^sign,
+    no reduction.  Returns (out, lengths_out)."""
+    lib = _lib.load()
+    B, L, dev = _word_setup(states, "states")
+    _check(lengths, "lengths", _INT32, (B, 2), dev)
+    out = torch.empty_like(states)
+    lo = torch.empty((B, 2), dtype=_INT32, device=dev)
+    st = lib.acx_concatenate(_ptr(states), _ptr(out), _ptr(lengths), _ptr(lo), B, L, int(i), int(j), int(sign),
+                             _stream(dev))
+    _lib.check(st, "acx_concatenate")
+    return out, lo
+
+
+def conjugate(states: torch.Tensor, i: int, j: int, sign: int, lengths: Optional[torch.Tensor] = None):
+    """acx_conjugate: conjugate (ac_moves.py:79-156) over a batch, r_i <- x_j^sign r_i x_j^-sign,
+    no reduction.  Returns (out, lengths_out, err) -- err 2 where the reference raises IndexError."""
+    lib = _lib.load()
+    B, L, dev = _word_setup(states, "states")
+    _check(lengths, "lengths", _INT32, (B, 2), dev)
+    out = torch.empty_like(states)
+    lo = torch.empty((B, 2), dtype=_INT32, device=dev)
+    err = torch.empty(B, dtype=_UINT8, device=dev)
+    st = lib.acx_conjugate(_ptr(states), _ptr(out), _ptr(lengths), _ptr(lo), _ptr(err), None, B, L, int(i), int(j),
+                           int(sign), _stream(dev))
+    _lib.check(st, "acx_conjugate")
+    return out, lo, err
+
+
+def word_simplify_presentation(states: torch.Tensor, *, cyclical: bool = True):
+    """acx_word_simplify_presentation: simplify_presentation (utils.py:246-283) on arbitrary
+    letters.  Returns (out, lengths, err)."""
+    lib = _lib.load()
+    B, L, dev = _word_setup(states, "states")
+    out = torch.empty_like(states)
+    lo = torch.empty((B, 2), dtype=_INT32, device=dev)
+    err = torch.empty(B, dtype=_UINT8, device=dev)
+    st = lib.acx_word_simplify_presentation(_ptr(states), _ptr(out), _ptr(lo), _ptr(err), None, B, L,
+                                            int(bool(cyclical)), _stream(dev))
+    _lib.check(st, "acx_word_simplify_presentation")
+    return out, lo, err
+
+
+def word_simplify_relator(relators: torch.Tensor, max_relator_length: int, *, cyclical: bool = False,
+                          padded: bool = True):
+    """acx_word_simplify_relator: simplify_relator (utils.py:178-243) on (B, m) relator arrays.
+    Returns (out (B, max(m, L)), out_len (B), n (B), err (B)): row b's returned array is
+    out[b, :out_len[b]]."""
+    lib = _lib.load()
+    _need_gpu(relators, "relators")
+    if relators.dim() != 2 or relators.dtype != _INT32 or not relators.is_contiguous():
+        raise TypeError("relators must be a contiguous (B, m) int32 tensor")
+    B, m = relators.shape
+    L = int(max_relator_length)
+    dev = relators.device
+    out = torch.empty((B, max(m, L)), dtype=_INT32, device=dev)
+    ol = torch.empty(B, dtype=_INT32, device=dev)
+    n = torch.zeros(B, dtype=_INT32, device=dev)
+    err = torch.empty(B, dtype=_UINT8, device=dev)
+    st = lib.acx_word_simplify_relator(_ptr(relators), m, _ptr(out), _ptr(ol), _ptr(n), _ptr(err), None, B, L,
+                                       int(bool(cyclical)), int(bool(padded)), _stream(dev))
+    _lib.check(st, "acx_word_simplify_relator")
+    return out, ol, n, err

@@ -81,10 +81,15 @@ def device_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclical
         if n > 0:
             lib.acx_bfs_node_keys(h, nk.ctypes.data, n)
         LAST_STATS["node_keys"] = nk
+    ntr = lib.acx_bfs_min_trace(h, None, 0)
+    trace = np.zeros(max(ntr, 1), np.int32)
+    lib.acx_bfs_min_trace(h, trace.ctypes.data, ntr)
+    LAST_STATS["min_trace"] = [int(v) for v in trace[:ntr]]
+    if verbose:  # breadth_first.py:79-82, in the order the reference prints them
+        for v in LAST_STATS["min_trace"]:
+            print(f"New minimal length found: {v}")
     if st == _lib.BFS_MOVE_ERROR:
         raise AssertionError("bfs: a move produced an invalid presentation (utils.py:264-266)")
-    if verbose:
-        print(f"Minimal total length found: {int(stats[3])}")
     if st == _lib.BFS_BUDGET:
         print(f"Exiting search as number of explored nodes = {int(stats[0])} has exceeded the limit "
               f"{max_nodes_to_explore}")

@@ -112,20 +112,38 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
             nk = np.zeros((n_nodes.value, kw), np.uint64)
             lib.acx_search_node_keys(h, nk.ctypes.data, n_nodes.value)
             LAST_STATS["node_keys"] = nk
+            npop = lib.acx_search_popped(h, None, 0)
+            pops = np.zeros(max(npop, 1), np.int64)
+            lib.acx_search_popped(h, pops.ctypes.data, npop)
+            LAST_STATS["popped"] = pops[:npop]
+        ntr = lib.acx_search_min_trace(h, None, 0)
+        trace = np.zeros(max(ntr, 1), np.int32)
+        lib.acx_search_min_trace(h, trace.ctypes.data, ntr)
+        LAST_STATS["min_trace"] = [int(v) for v in trace[:ntr]]
+        LAST_STATS["min_length"] = int(min_len.value)
+        if verbose:  # greedy.py:86-89 / breadth_first.py:79-82, in the reference's order
+            for v in LAST_STATS["min_trace"]:
+                print(f"New minimal length found: {v}")
         if status == 3:
             raise AssertionError("a move produced an invalid presentation (utils.py:264-266)")
-        if verbose:
-            print(f"Minimal total length found: {min_len.value}")
-        if budget.value:
-            print(
-                f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
-                f"{max_nodes_to_explore}"
-            )
         cap = 1 << 16
         acts = np.zeros(cap, np.int32)
         tots = np.zeros(cap, np.int32)
         m = lib.acx_search_path(h, acts.ctypes.data, tots.ctypes.data, cap)
         path = [(int(acts[i]), int(tots[i])) for i in range(min(m, cap))]
+        if verbose and status == 1 and mode == GREEDY:  # greedy.py:92-99
+            first = np.zeros(2, np.int32)
+            explored = ctypes.c_int64(0)
+            lib.acx_search_found(h, first.ctypes.data, ctypes.byref(explored))
+            found = (np.array([first[0]], np.int8), np.array([first[1]], np.int8))
+            print(f"Found {found} after exploring {explored.value} nodes")
+            print(f"Path to a trivial state: (tuples are of form (action, length of a state)) {path}")
+            print(f"Total path length: {len(path)}")
+        if budget.value:
+            print(
+                f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
+                f"{max_nodes_to_explore}"
+            )
         return status == 1, path
     finally:
         lib.acx_search_destroy(h)

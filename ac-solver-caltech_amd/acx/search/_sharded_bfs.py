@@ -134,20 +134,36 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     chunk = int(chunk) if chunk else 1 << 19
     lcap = local_capacity(max_nodes, comm.world)
     lib = _lib.load()
-    h, send, recv, gmask = _handle(lib, dev, L, cyclically_reduce_after_moves, chunk, lcap, comm.rank,
-                                   comm.world)
+    # A failure on one rank must fail every rank at the same point, or its peers would block in
+    # the next collective: local failures are recorded and agreed on through the exchanges the
+    # search makes anyway (the gathered expand rows, the per-chunk status sum).
+    local_err = None
+    try:
+        h, send, recv, gmask = _handle(lib, dev, L, cyclically_reduce_after_moves, chunk, lcap, comm.rank,
+                                       comm.world)
+    except _lib.ACXError as e:
+        local_err = e
+    if comm.sum_rows([local_err is not None])[0]:
+        raise local_err or _lib.ACXError("sharded bfs: workspace creation failed on another rank")
     kw = _lib.key_words(L)
     rw = kw + 1
     pres = np.ascontiguousarray(p, dtype=np.int32)
     total0 = int(np.count_nonzero(pres))
     stream = torch.cuda.current_stream(dev).cuda_stream
     W = comm.world
-    exp_out = np.zeros(5 + W, np.int64)
+    exp_out = np.zeros(6 + W, np.int64)  # acx_sbfs_expand's 5 + W values, then this rank's failure flag
     com_out = np.zeros(5, np.int64)
+    failed = []  # (call, status) of failed C calls on this rank
 
     def ok(st, what):
         if st < 0:
-            _lib.check(st, what)
+            failed.append((what, int(st)))
+
+    def agree(flag_sum, what):
+        if flag_sum:
+            if failed:
+                _lib.check(failed[0][1], failed[0][0])
+            raise _lib.ACXError(f"sharded bfs: {what} failed on another rank")
 
     with torch.cuda.device(dev):
         ok(lib.acx_sbfs_reset(h, pres.ctypes.data, stream), "acx_sbfs_reset")
@@ -156,12 +172,14 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
         while head < n_nodes:
             P = min(n_nodes - head, chunk)
             ok(lib.acx_sbfs_expand(h, head, P, exp_out.ctypes.data, stream), "acx_sbfs_expand")
-            rows = comm.all_gather_rows(exp_out)  # (W, 5 + W)
+            exp_out[5 + W] = len(failed)
+            rows = comm.all_gather_rows(exp_out)  # (W, 6 + W)
+            agree(rows[:, 5 + W].sum(), "a C call")
             if rows[:, 4].any():
                 raise _lib.ACXError("sharded bfs: hash table overflow")
             succ_seq, err_seq = int(rows[:, 0].min()), int(rows[:, 1].min())
             chunk_min = int(rows[:, 2].min())
-            send_counts = rows[comm.rank, 5:]
+            send_counts = rows[comm.rank, 5 : 5 + W]
             recv_counts = rows[:, 5 + comm.rank]
             nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
             ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
@@ -175,7 +193,9 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
             ok(lib.acx_sbfs_commit(h, gmask.data_ptr(), n_nodes, max_nodes - n_nodes, com_out.ctypes.data, stream),
                "acx_sbfs_commit")
             chunks += 1
-            if comm.sum_rows([com_out[4]])[0]:
+            st_rows = comm.sum_rows([com_out[4], len(failed)])
+            agree(st_rows[1], "a C call")
+            if st_rows[0]:
                 raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
             total_new, cut_p, nodes_at_cut = int(com_out[0]), int(com_out[1]), int(com_out[2])
             cut = cut_p if cut_p >= 0 else None
@@ -214,6 +234,7 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
             while g > 0:
                 ok(lib.acx_sbfs_lookup(h, g, look.ctypes.data, stream), "acx_sbfs_lookup")
                 found = comm.sum_rows(look * (look[0] != 0))
+                agree(comm.sum_rows([len(failed)])[0], "acx_sbfs_lookup")
                 if found[0] != 1:
                     raise _lib.ACXError(f"sharded bfs: node {g} stored on {found[0]} ranks")
                 edges.append((int(found[2]), int(found[3])))

@@ -12,6 +12,6 @@ from ._engine import GREEDY, run_search
 def greedy_search(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
                   device=None, batch=None):
     """Returns (is_search_successful, path) with path = [(action, total_length), ...]
-    starting at (-1, initial_total_length), as greedy.py:162-247."""
+    starting at (-1, initial_total_length), as greedy.py:15-121."""
     return run_search(GREEDY, presentation, max_nodes_to_explore, verbose, cyclically_reduce_after_moves,
                       device=device, batch=batch)

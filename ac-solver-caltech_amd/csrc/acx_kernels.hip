@@ -168,6 +168,11 @@ struct FastTile {
         tile_bad = __any(flagged);
         wave_sync();
     }
+    // additionally flag the rows of lanes with f (their store copies the fallback row)
+    __device__ __forceinline__ void flag_rows(int lane, bool f) {
+        if (f) flags[lane] = 1;
+        tile_bad = tile_bad || __any(f);
+    }
     __device__ __forceinline__ FastTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
@@ -397,6 +402,10 @@ struct CodeTile {
         tile_bad = __any(flagged);
         wave_sync();
     }
+    __device__ __forceinline__ void flag_rows(int lane, bool f) {
+        if (f) flags[lane] = 1;
+        tile_bad = tile_bad || __any(f);
+    }
     __device__ __forceinline__ CodeTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
@@ -585,6 +594,9 @@ struct GenericTile {
         flags[lane] = flagged;
         wave_sync();
     }
+    __device__ __forceinline__ void flag_rows(int lane, bool f) {
+        if (f) flags[lane] = 1;
+    }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(base + r * rowb); }
 
     // (row, pos) of a chunk of VEC int32; chunks never straddle rows (2L % VEC == 0)
@@ -743,6 +755,60 @@ __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>&
     }
 }
 
+// One lane packs its own row straight from HBM (per-lane loads, no LDS staging): the same
+// result as tile.load + tile.pack for that row.  Used by the autoreset of a few lanes of a
+// wave, where a coalesced reload of the whole 64-row tile would move 64 rows to use a few.
+// Rolled loops (one load in flight): it is a rare path and must not add register pressure
+// to the kernels that inline it.
+template <int NW, int LC>
+__device__ __forceinline__ bool pack_row_global(const int32_t* __restrict__ row, int Lr, PresRegs<NW>& p) {
+    const int L = LC > 0 ? LC : Lr;
+    bool bad = false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Word<NW> w = wzero<NW>();
+        uint64_t mlo = 0, mhi = 0;
+        const int32_t* src = row + h * L;
+        if constexpr (LC > 0 && LC % 4 == 0) {
+#pragma unroll 1
+            for (int k = 0; k < LC / 4; ++k) {
+                const int4 v = reinterpret_cast<const int4*>(src)[k];
+                const uint32_t d = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
+                                   (to_i8(v.w, bad) << 24);
+                uint32_t c8, nz4;
+                swar_pack4(d, c8, nz4);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) w.w[j] |= (k >> 2) == j ? c8 << (8 * (k & 3)) : 0u;
+                if (k < 16) mlo |= (uint64_t)nz4 << (4 * k);
+                else mhi |= (uint64_t)nz4 << (4 * (k - 16));
+            }
+        } else {
+#pragma unroll 1
+            for (int k = 0; k < L; ++k) {
+                const uint32_t b = to_i8(src[k], bad);
+                const bool nz = b != 0u;
+                const uint32_t code = nz ? (((~b & 1u) << 1) | ((b >> 7) & 1u)) : 0u;
+#pragma unroll
+                for (int j = 0; j < NW; ++j) w.w[j] |= (k >> 4) == j ? code << (2 * (k & 15)) : 0u;
+                if (k < 64) mlo |= (uint64_t)nz << k;
+                else mhi |= (uint64_t)nz << (k - 64);
+            }
+        }
+        const int n = __builtin_popcountll(mlo) + __builtin_popcountll(mhi);
+        const uint64_t elo = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+        const uint64_t ehi = n <= 64 ? 0ull : (n >= 128 ? ~0ull : ((1ull << (n - 64)) - 1ull));
+        bad |= (mlo != elo) || (mhi != ehi);
+        if (h == 0) { p.w0 = w; p.n0 = n; }
+        else        { p.w1 = w; p.n1 = n; }
+    }
+    return bad;
+}
+
+// A wave reloads its whole tile of starting states (one coalesced pass) when more than this
+// many of its lanes reset on the same step (a synchronised truncation); fewer resetting lanes
+// each read their own row (pack_row_global), so scattered resets cost their own rows only.
+constexpr int RESET_TILE_MIN = 8;
+
 // common per-wave prologue: tile index, rows in the tile, LDS slice
 struct WaveCtx {
     int lane, wid;
@@ -810,7 +876,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     bool reset = false;  // same-step autoreset of this env
     bool keep = false;   // the env's row is left as loaded (out of domain, or its move failed)
     PresRegs<NW> p;
-    int cnt = 0, e = ACX_ERR_NONE;
+    int cnt0 = 0, cnt = 0, e = ACX_ERR_NONE;
     if (w.active) {
         int act;
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
@@ -819,7 +885,8 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         } else {
             act = a.action[env];
         }
-        cnt = a.step_count ? a.step_count[env] + 1 : 0;
+        cnt0 = a.step_count ? a.step_count[env] : 0;
+        cnt = a.step_count ? cnt0 + 1 : 0;
         // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
         // at [k][i] -- envs at the same episode position write one coalesced row segment (an
         // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
@@ -830,9 +897,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         else if (is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         keep = e != ACX_ERR_NONE;
+        if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
         if (!keep) tile.unpack(w.lane, p);
         const bool triv = !keep && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
-        const bool trunc = a.step_count ? (cnt >= a.horizon) : false;
+        const bool trunc = !keep && a.step_count && cnt >= a.horizon;
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
@@ -843,22 +911,41 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
         }
         reset = fin && a.reset_state && !keep;
-        if (reset) {
-            // final_obs <- post-move state (per lane: rare, and only with final_obs)
-            if (a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
-            cnt = 0;
-        }
+        // final_obs <- post-move state (per lane: rare, and only with final_obs)
+        if (reset && a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
     }
-    if (__any(reset)) {
-        // same-step autoreset: the tile's starting states, one coalesced load (a per-lane row
-        // read cost ~1 ms on the step of a whole-batch truncation); resetting envs pack theirs,
-        // the others re-stage their state, rows left as loaded copy state_in in the store
-        wave_sync();
-        tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
-        if (reset) tile.pack(w.lane, p);
-        wave_sync();
-        if (w.active && !keep) tile.unpack(w.lane, p);
-        tile.restore_flags(w.lane, w.active && keep);
+    const uint64_t rb = __ballot(reset);
+    if (rb) {
+        // same-step autoreset to the env's starting state.  An out-of-domain starting row
+        // fails the env instead (err ACX_ERR_DOMAIN, state and step_count keep their inputs).
+        bool rbad = false;
+        if (__popcll(rb) > RESET_TILE_MIN) {
+            // many lanes (a synchronised truncation): one coalesced load of the tile's starting
+            // states (per-lane reads of every row cost ~1 ms on a whole-batch truncation step);
+            // the other lanes re-stage their state, rows left as loaded copy state_in
+            wave_sync();
+            tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+            if (reset) rbad = tile.pack(w.lane, p);
+            wave_sync();
+            keep = keep || rbad;
+            if (w.active && !keep) tile.unpack(w.lane, p);
+            tile.restore_flags(w.lane, w.active && keep);
+        } else {
+            // a few lanes: each reads its own starting row (scattered resets cost their rows only)
+            if (reset) {
+                rbad = pack_row_global<NW, LC>(a.reset_state + env * twoL, L, p);
+                if (!rbad) tile.unpack(w.lane, p);
+            }
+            keep = keep || rbad;
+            tile.flag_rows(w.lane, rbad);
+        }
+        if (rbad) {  // rare: the reported lengths are those of the kept input row
+            reset = false;
+            e = ACX_ERR_DOMAIN;
+            cnt = cnt0;
+            pack_row_global<NW, LC>(a.state_in + env * twoL, L, p);
+        }
+        if (reset) cnt = 0;
     }
     if (w.active) {
         if (a.step_count) a.step_count[env] = cnt;
@@ -909,16 +996,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
 
-    // starting states: validated here, re-read (coalesced, through the tile) only when an
-    // episode of the tile ends -- not kept in registers, which are the rollout's occupancy
-    // limit (one reload per horizon per tile)
+    // starting states are read only when an episode ends (not kept in registers, which are
+    // the rollout's occupancy limit): by the resetting lane alone, or by a coalesced reload of
+    // the tile when many lanes of the wave reset together; an out-of-domain starting row fails
+    // its env then (err ACX_ERR_DOMAIN, the env stops and its state keeps its input)
     bool bad = false;
-    {
-        PresRegs<NW> rs;
-        tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
-        if (w.active) bad = tile.pack(w.lane, rs);
-        wave_sync();
-    }
     PresRegs<NW> p;
     tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
@@ -926,7 +1008,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     const bool cyc = a.cyclical != 0;
     bool clean = false;
     if (w.active) {
-        bad |= tile.pack(w.lane, p);
+        bad = tile.pack(w.lane, p);
         cnt = a.step_count[env];
         if (bad) first_err = ACX_ERR_DOMAIN;
         clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
@@ -963,13 +1045,21 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             reset = (triv || trunc) && !bad;
             if (reset) cnt = 0;
         }
-        if (__any(reset)) {  // same-step autoreset: the tile's starting states, coalesced
-            tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
-            if (reset) {
-                tile.pack(w.lane, p);
-                clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+        const uint64_t rb = __ballot(reset);
+        if (rb) {  // same-step autoreset to the starting states
+            bool rbad = false;
+            if (__popcll(rb) > RESET_TILE_MIN) {  // many lanes: one coalesced tile reload
+                tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
+                if (reset) rbad = tile.pack(w.lane, p);
+                wave_sync();
+            } else if (reset) {  // a few lanes: their own rows only
+                rbad = pack_row_global<NW, LC>(a.reset_state + (w.r0 + ln) * twoL, L, p);
             }
-            wave_sync();
+            if (reset) {
+                clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+                bad = rbad;
+                if (rbad && first_err == ACX_ERR_NONE) first_err = ACX_ERR_DOMAIN;
+            }
         }
         if constexpr (OBS) {
             if (w.active && !bad) tile.unpack(w.lane, p);

@@ -66,7 +66,7 @@ struct Args {
     uint8_t* lact;    // (lcap) move id that produced the node
     uint64_t* ckeys;  // (12, Pr) keys of the local parents' children, action-major
     uint8_t* cown;    // (12, Pr) owner of each child, 0xff: parent not in the chunk
-    uint8_t* pmin;    // (Pr) min child total per local parent
+    uint16_t* pmin;   // (Pr) min child total per local parent (totals reach 2L = 256)
     uint32_t* map;    // (12 P) seq -> received record, NONE if not received here
     uint32_t* rslot;  // (rcap) slot claimed/joined by a received child, SEEN if known
     uint32_t* bsum;   // (nb) all survivors per block of parents -> exclusive offsets
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
         const bool clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, cyc);
         const uint32_t p = (uint32_t)(gid - a.head);
         uint32_t succ = NONE, err = NONE;
-        int mn = 255;
+        int mn = 0xffff;
         for (int act = 0; act < 12; ++act) {
             PresRegs<NW> q = pr;
             const int e = clean ? ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc)
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
             own[act] = (uint8_t)owner_of(khash<NW + 1>(key, a.kw), a.world);
             a.cown[(int64_t)act * a.Pr + j] = own[act];
         }
-        a.pmin[j] = (uint8_t)mn;
+        a.pmin[j] = (uint16_t)mn;
         mn_lane = (uint32_t)mn;
         if (succ != NONE) atomicMin(&a.ctl->succ_seq, succ);
         if (err != NONE) atomicMin(&a.ctl->err_seq, err);

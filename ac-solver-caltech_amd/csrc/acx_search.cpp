@@ -9,7 +9,7 @@
 //     (breadth_first.py:61-95).  Parents are expanded ahead in FIFO order, which cannot
 //     change the result because expansion is a pure function of the state.
 //   * greedy: priority order (total length, path length, state tuple) -- a total order,
-//     so heapq's pop sequence equals popping a min-heap on that order (greedy.py:181-239).  The smallest not-yet-expanded nodes are expanded
+//     so heapq's pop sequence equals popping a min-heap on that order (greedy.py:71-113).  The smallest not-yet-expanded nodes are expanded
 //     speculatively in one launch; children are cached until their parent is popped.
 // Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
 // acx_key_words(L) uint64 words.
@@ -23,6 +23,7 @@ namespace {
 
 constexpr int ACT = 12;
 constexpr size_t PREFETCH = 6;  // parents of lookahead for hash-slot prefetches (BFS)
+constexpr int HDR = 40;         // priority-key header bits: total (9) | depth (31)
 
 inline uint64_t mix64(uint64_t x) {
     x ^= x >> 30;
@@ -52,9 +53,9 @@ struct Engine {
     std::vector<int64_t> queue;
     size_t head = 0, requested = 0;
     // greedy ordered frontier: the heap tuple (total, path length, state tuple) of
-    // greedy.py:161-167,231-239 packed MSB-first into pk words per node -- total (8 bits),
-    // depth (24 bits), then every letter + 2 (3 bits, r0 then r1 incl. padding) -- so
-    // comparing the words as unsigned integers is Python's tuple order.  Two 4-ary min-heaps
+    // greedy.py:55-64,104-113 packed MSB-first into pk words per node -- total (9 bits: up to
+    // 2L = 256), depth (31 bits), then every letter + 2 (3 bits, r0 then r1 incl. padding) --
+    // so comparing the words as unsigned integers is Python's tuple order.  Two 4-ary min-heaps
     // with the keys inline (no pointer chasing per comparison): all unpopped nodes (pop
     // order) and the subset not yet sent to the GPU (speculative expansion order).
     int pk = 0;
@@ -132,13 +133,17 @@ struct Engine {
     int64_t last_popped = -1;
     int min_length = 0;
     int budget_hit = 0;
+    std::vector<int32_t> trace;  // each new minimum total, in the order found (greedy.py:86-89)
+    std::vector<int64_t> popped; // node ids in expansion (pop) order
+    int64_t found_explored = 0;  // len(tree_nodes) - len(to_explore) at the success (greedy.py:94)
+    uint64_t found_key[ACX_MAX_L / 16 + 2] = {0};
     // statistics: rounds (next_batch calls that returned parents), parents expanded, pops
     int64_t st_rounds = 0, st_expanded = 0, st_pops = 0;
 
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
         table.assign(1 << 12, 0);
         mask = table.size() - 1;
-        pk = (32 + 6 * L + 63) / 64;
+        pk = (HDR + 6 * L + 63) / 64;
         frontier.pk = unexpanded.pk = pk;
     }
 
@@ -206,9 +211,9 @@ struct Engine {
             n[1] = (int)(((lo | hi) >> 8) & 0xff);
         }
         for (int i = 0; i < pk; ++i) out[i] = 0;
-        out[0] = ((uint64_t)tot << 56) | ((uint64_t)(dep & 0xffffff) << 32);
+        out[0] = ((uint64_t)(tot & 0x1ff) << 55) | ((uint64_t)(dep & 0x7fffffff) << 24);
         static const uint64_t val[4] = {3, 1, 4, 0};  // letter + 2 for codes x, x^-1, y, y^-1
-        int pos = 32;  // next free bit, counted from the MSB of word 0
+        int pos = HDR;  // next free bit, counted from the MSB of word 0
         for (int h = 0; h < 2; ++h)
             for (int i = 0; i < L; ++i, pos += 3) {
                 const int bit = 2 * (h * L + i);
@@ -303,6 +308,7 @@ struct Engine {
         const uint64_t* hs = &cache_hash[off / kw];
         last_popped = id;
         ++st_pops;
+        popped.push_back(id);
         bool ended = false;
         for (int a = 0; a < ACT && !ended; ++a) {
             const uint64_t* k = ck + (size_t)a * kw;
@@ -314,12 +320,17 @@ struct Engine {
             const int len = key_len(k, L);
             last_action = a;
             last_len = len;
-            if (len < min_length) min_length = len;
-            if (len == 2) {  // greedy.py:217, breadth_first.py:84
+            if (len < min_length) {
+                min_length = len;
+                trace.push_back(len);
+            }
+            if (len == 2) {  // greedy.py:91, breadth_first.py:84
                 status = 1;
                 found_parent = id;
                 found_action = a;
                 found_len = len;
+                found_explored = n_set - (int64_t)(mode == 0 ? queue.size() - head : frontier.id.size());
+                std::memcpy(found_key, k, sizeof(uint64_t) * kw);
                 ended = true;
                 break;
             }
@@ -334,7 +345,7 @@ struct Engine {
         }
         cache_pos[id] = -1;
         free_slots.push_back(off);
-        if (!ended && n_set >= max_nodes) {  // greedy.py:241, breadth_first.py:91
+        if (!ended && n_set >= max_nodes) {  // greedy.py:115, breadth_first.py:91
             status = 2;
             budget_hit = 1;
             ended = true;
@@ -421,7 +432,7 @@ int32_t acx_search_status(void* h, int32_t* budget_hit, int32_t* min_length, int
 }
 
 // success: path of the found child; failure (greedy): path of the last popped node plus its
-// last child (greedy.py:247).  Returns the number of (action, total) entries.
+// last child (greedy.py:121).  Returns the number of (action, total) entries.
 int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap) {
     Engine* e = static_cast<Engine*>(h);
     if (e->status == 1) return e->path(e->found_parent, actions, totals, cap, true);
@@ -435,6 +446,37 @@ void acx_search_stats(void* h, int64_t* out) {
     out[0] = e->st_rounds;
     out[1] = e->st_expanded;
     out[2] = e->st_pops;
+}
+
+// ids of the expanded (popped) nodes in the reference's expansion order; returns the count
+int64_t acx_search_popped(void* h, int64_t* ids, int64_t cap) {
+    Engine* e = static_cast<Engine*>(h);
+    const int64_t n = (int64_t)e->popped.size();
+    for (int64_t i = 0; ids && i < n && i < cap; ++i) ids[i] = e->popped[(size_t)i];
+    return n;
+}
+
+// the new minimum totals in the order found (the verbose "New minimal length found" lines)
+int64_t acx_search_min_trace(void* h, int32_t* out, int64_t cap) {
+    Engine* e = static_cast<Engine*>(h);
+    const int64_t n = (int64_t)e->trace.size();
+    for (int64_t i = 0; out && i < n && i < cap; ++i) out[i] = e->trace[(size_t)i];
+    return n;
+}
+
+// after a success: the first letters of both relators of the found child (each of length 1) and
+// len(tree_nodes) - len(to_explore) at that moment (greedy.py:92-95); returns 1, else 0
+int32_t acx_search_found(void* h, int32_t* first_letters, int64_t* explored) {
+    Engine* e = static_cast<Engine*>(h);
+    if (e->status != 1) return 0;
+    static const int32_t letter[4] = {1, -1, 2, -2};
+    const int bit1 = 2 * e->L;
+    if (first_letters) {
+        first_letters[0] = letter[e->found_key[0] & 3u];
+        first_letters[1] = letter[(e->found_key[bit1 >> 6] >> (bit1 & 63)) & 3u];
+    }
+    if (explored) *explored = e->found_explored;
+    return 1;
 }
 
 // copy the packed keys of the first min(cap, n_nodes) discovered nodes (discovery order)

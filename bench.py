@@ -153,6 +153,7 @@ def main():
     ap.add_argument("--no-learner", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-bfs", action="store_true")
+    ap.add_argument("--no-desync", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -238,17 +239,77 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    n_err = int(err_count.item())
+    n_err = int(err_count.item())  # the headline rollout's env errors (warmup + timed)
 
     # algorithmic bytes of the rollout launch (DESIGN.md "Roofline"): per env-step action 4 B
     # + obs 8L B + reward 4 + done 1 + truncated 1; per env per launch state in/out 2*8L,
-    # reset state 8L, step count in/out 8, err 1
+    # step count in/out 8, err 1; plus the starting state (8L) of every env that resets
     step_bytes = 4 + 8 * L + 4 + 1 + 1
     n_launch = -(-K // T_buf)
-    launch_bytes = K * B * step_bytes + n_launch * B * (24 * L + 8 + 1)
+
+    def count_resets(T):
+        # resets of the last launch = done | truncated over its steps (both never hold together
+        # in a way that matters: a reset reads one row either way)
+        if T > T_buf:
+            return None
+        return int((done[:T] | trunc[:T]).sum().item())
+
+    def rollout_bytes(n_resets):
+        return K * B * step_bytes + n_launch * B * (16 * L + 8 + 1) + (n_resets or 0) * 8 * L
+
+    resets = count_resets(K)
+    launch_bytes = rollout_bytes(resets)
     achieved = launch_bytes / kernel_s / 1e9
 
     variants = {}
+
+    def desync_variant(start_rows, count0, what):
+        # the rollout with the episodes out of phase (step_count[i] = i mod H): ~B/H envs reset
+        # on every step, scattered over the waves -- the steady state of a PPO rollout, which
+        # the headline's synchronised counts (all 0 at the start) never show in K < H steps
+        st = start_rows.clone()
+        cnt = count0.clone()
+        err_count.zero_()
+
+        def go(a, T):
+            for t0 in range(0, T, T_buf):
+                t1 = min(T, t0 + T_buf)
+                ops.rollout(st, a[t0:t1], start_rows, cnt, horizon=H, cyclical=True, obs_traj=obs[: t1 - t0],
+                            reward_traj=rew[: t1 - t0], done_traj=done[: t1 - t0], trunc_traj=trunc[: t1 - t0],
+                            err=err, err_count=err_count)
+
+        if W > 0:
+            go(actions[:W], W)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        go(actions[W : W + K], K)
+        e1.record()
+        torch.cuda.synchronize()
+        s_d = e0.elapsed_time(e1) / 1e3
+        nres = count_resets(K)
+        nb = rollout_bytes(nres)
+        return {"value": B * K / s_d, "unit": "env-steps/s", "kernel_ms": s_d * 1e3, "ms_per_step": s_d / K * 1e3,
+                "resets_per_step": None if nres is None else nres / K, "env_errors": int(err_count.item()),
+                "workload": what,
+                "roofline": {"bound": "hbm", "achieved": nb / s_d / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": nb / s_d / 1e9 / HBM_PEAK_GBS, "launch_bytes": nb}}
+
+    if not args.no_desync:
+        desync = torch.arange(B, dtype=torch.int32, device=dev) % H
+        variants["rollout_desync"] = desync_variant(
+            starts, desync, "the headline rollout with step_count[i] = i mod H (Miller-Schupp starts): about B/H "
+                            "truncations per step, scattered over the waves")
+        triv = np.zeros((8, 2 * L), np.int32)
+        for r, (a0, a1) in enumerate([(1, 2), (1, -2), (-1, 2), (-1, -2), (2, 1), (2, -1), (-2, 1), (-2, -1)]):
+            triv[r, 0], triv[r, L] = a0, a1
+        tstarts = torch.as_tensor(triv[np.arange(B) % 8]).to(dev)
+        variants["rollout_done_heavy"] = desync_variant(
+            tstarts, desync, "done-heavy: every env starts at one of the 8 trivial presentations "
+                             "(generate_trivial_states, utils.py:91-114) with step_count[i] = i mod H, so dones "
+                             "and resets fire on a large share of env-steps")
+        del tstarts, desync
     if not args.no_step_api:
         # per-call acx_step API: one launch per env step, state in/out of HBM each step
         rew1 = torch.empty(B, dtype=torch.int32, device=dev)
@@ -262,6 +323,7 @@ def main():
             ops.step(st1, a, state_out=st1, reset_state=starts, step_count=cnt1, horizon=H, cyclical=True,
                      reward=rew1, done=dn1, truncated=tr1, lengths=lens1, err=err, err_count=err_count)
 
+        err_count.zero_()
         for t in range(W):
             step(actions[t])
         torch.cuda.synchronize()
@@ -283,8 +345,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": B * sb / (s_api / K) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS,
                          "bytes_per_env_step": sb},
+            "env_errors": int(err_count.item()),
         }
-        n_err = int(err_count.item())
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
         # the ctypes launches on the capture stream) and replayed: no per-launch host cost
@@ -311,7 +373,6 @@ def main():
                              "bytes_per_env_step": sb},
             }
             del graph
-            n_err = int(err_count.item())
 
     if not args.no_learner and world == 1:
         # PPO plumbing (acx.agents.LearnerEnv): per step one acx_step_learner (int64 policy
@@ -389,9 +450,13 @@ def main():
     # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
     # used only when that profile's workload matches this run's
+    # (the newest committed profile of this workload at this K; profile_cmd.sh profiles the
+    # driver's own command, bench.py --steps 20 --warmup 5, and the K = 200 default)
     traffic, traffic_src = None, None
-    prof = os.path.join(REPO, "profiles", "r01", "r01_summary.json")
-    if os.path.exists(prof):
+    for tag in ("r02_k20", "r02", "r01"):
+        prof = os.path.join(REPO, "profiles", tag.split("_")[0], f"{tag}_summary.json")
+        if traffic is not None or not os.path.exists(prof):
+            continue
         with open(prof) as f:
             ps = json.load(f)
         pc = ps.get("bench_line", {}).get("config", {})
@@ -399,7 +464,8 @@ def main():
         if (pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and ps["bench_line"].get("steps") == K
                 and td.get("pmc_hbm_bytes")):
             traffic = td["pmc_hbm_bytes"]
-            traffic_src = "profiles/r01/r01_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE, same command"
+            traffic_src = (f"profiles/{tag.split('_')[0]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + "
+                           f"--pmc WRITE_SIZE of this command (K={K})")
 
     value = world * B * K / elapsed
     line = {
@@ -437,6 +503,7 @@ def main():
             "kernel": f"acx::pack_actions_kernel + acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,true>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
+            "resets_in_launch": resets,
             "launches": n_launch,
             "kernel_ms": kernel_s * 1e3,
             "host_launch_ms": t_launch * 1e3,

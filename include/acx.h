@@ -15,7 +15,7 @@
  *   acx_rollout     T fused ACEnv.step calls (the PPO rollout collection loop,
  *                   ac_solver/agents/training.py:221-356), state kept on chip.
  *   acx_expand12    the 12-way neighbour expansion of greedy_search / bfs
- *                   (ac_solver/search/greedy.py:202-210, breadth_first.py:69-77).
+ *                   (ac_solver/search/greedy.py:76-83, breadth_first.py:69-76).
  *   acx_canonicalize  simplify_presentation (utils.py:246-283) over a batch.
  *   acx_unpack_keys   packed child keys (acx_expand12) -> int32 presentations.
  *
@@ -54,9 +54,14 @@ extern "C" {
                                 (a relator became empty), utils.py:264-266 */
 #define ACX_ERR_EMPTY_CONJ 2 /* reference IndexError: conjugating an empty relator,
                                 ac_moves.py:117-120 */
-#define ACX_ERR_DOMAIN 3     /* input outside the kernel domain: a letter not in {-2..2} or a
-                                zero inside a relator (ACEnvConfig rejects both, ac_env.py:34) */
+#define ACX_ERR_DOMAIN 3     /* input outside the packed kernels' domain: a letter not in {-2..2}
+                                or a zero inside a relator.  The reference's word functions take
+                                any integer letters (ACEnvConfig validates only the zero padding,
+                                utils.py:13-54): the acx_word_* / acx_concatenate / acx_conjugate
+                                entry points below compute those rows exactly */
 #define ACX_ERR_ACTION 4     /* move id not in [0,12) (reference AssertionError ac_moves.py:188) */
+#define ACX_ERR_PAD 9        /* reference ValueError: np.pad with a negative width (a relator
+                                array longer than max_relator_length, utils.py:235-236) */
 
 /*
  * Batched ACEnv.step / ACMove.
@@ -179,6 +184,37 @@ int acx_expand12(const int32_t* parents, int32_t* children, int32_t* child_len, 
 int acx_canonicalize(const int32_t* state_in, int32_t* state_out, int32_t* lengths_out, uint8_t* err,
                      int32_t* err_count, int64_t B, int32_t L, int32_t cyclical, void* stream);
 
+/*
+ * The reference's word functions on ARBITRARY int32 letters (csrc/acx_words.hip): exact, including
+ * letters beyond +-2 (its unit tests use 3..6) and zeros inside a relator, one lane per row with
+ * the rows staged through LDS.  A row whose reference call raises keeps its input and gets the
+ * ACX_ERR_* code of the exception (err / err_count nullable).
+ *   acx_word_move      ACMove (ac_moves.py:159-231) per row: move id action[b]; lengths_out (B,2);
+ *                      done (nullable) = strict triviality of the result (ac_env.py:99)
+ *   acx_concatenate    concatenate_relators (ac_moves.py:4-76): r_i <- r_i r_j^sign, no reduction;
+ *                      lengths_out = the caller's lengths_in (or the non-zero counts when NULL)
+ *                      with [i] replaced by the new size when it fits (the reference updates the
+ *                      list it is given)
+ *   acx_conjugate      conjugate (ac_moves.py:79-156): r_i <- x_j^sign r_i x_j^-sign, no reduction
+ *   acx_word_simplify_presentation  simplify_presentation (utils.py:246-283)
+ *   acx_word_simplify_relator  simplify_relator (utils.py:178-243) on (B, m) relator arrays: out
+ *                      (B, max(m, L)) holds the returned array in its first out_len[b] entries
+ *                      (L when padded), n_out[b] the word length
+ */
+int acx_word_move(const int32_t* state_in, int32_t* state_out, const int32_t* action, int32_t* lengths_out,
+                  uint8_t* done, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t cyclical,
+                  void* stream);
+int acx_concatenate(const int32_t* state_in, int32_t* state_out, const int32_t* lengths_in, int32_t* lengths_out,
+                    int64_t B, int32_t L, int32_t i, int32_t j, int32_t sign, void* stream);
+int acx_conjugate(const int32_t* state_in, int32_t* state_out, const int32_t* lengths_in, int32_t* lengths_out,
+                  uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t i, int32_t j, int32_t sign,
+                  void* stream);
+int acx_word_simplify_presentation(const int32_t* state_in, int32_t* state_out, int32_t* lengths_out, uint8_t* err,
+                                   int32_t* err_count, int64_t B, int32_t L, int32_t cyclical, void* stream);
+int acx_word_simplify_relator(const int32_t* relators, int32_t m, int32_t* out, int32_t* out_len, int32_t* n_out,
+                              uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t cyclical,
+                              int32_t padded, void* stream);
+
 /* packed keys (M, acx_key_words(L)) -> presentations (M,2L) int32 (+ lengths (M,2), nullable) */
 int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out, int64_t M, int32_t L,
                     void* stream);
@@ -190,7 +226,9 @@ int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out,
  * (first occurrence in (parent, action) order wins), the success test and the per-parent node
  * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^19).
  *   acx_bfs_create   allocates the device workspace on the current device for searches of
- *                    up to max_nodes nodes (<= 2^30) at max_relator_length L; NULL on failure.
+ *                    up to max_nodes nodes (<= 2^30) at max_relator_length L; NULL on failure
+ *                    (every child key of every expanded parent is kept: ~12 * 8 * kw bytes
+ *                    per node, 2.9 GB at 10^7 nodes and L = 36).
  *   acx_bfs_run      searches from `presentation` (HOST pointer, 2L int32, a valid presentation
  *                    with letters +-1, +-2) with budget max_nodes (<= the create-time value);
  *                    synchronous on `stream`.  On ACX_BFS_FOUND the reference's path
@@ -210,6 +248,10 @@ void acx_bfs_destroy(void* h);
 /* packed keys (acx.h key format) of the first min(cap, n) nodes of the last run in discovery
    (FIFO) order, n = nodes held (<= max_nodes + 12); returns n */
 int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
+/* the new minimal total lengths of the last run in the order the reference finds them (its
+   verbose "New minimal length found: m" lines, breadth_first.py:79-82): writes the first cap,
+   returns how many there are */
+int64_t acx_bfs_min_trace(void* h, int32_t* out, int64_t cap);
 
 /*
  * Breadth-first search with the node store and the visited set partitioned over G GPUs by key
@@ -278,6 +320,11 @@ int acx_token_ids(const int32_t* states, const uint64_t* keys, int64_t* out, int
  *   acx_search_path        the result path (see acx_search.cpp); returns its length
  *   acx_search_stats       out[0] rounds, out[1] parents expanded, out[2] parents popped
  *   acx_search_node_keys   the packed keys of the discovered nodes in discovery order
+ *   acx_search_min_trace   the new minimum totals in the order found (the verbose "New minimal
+ *                          length found" lines, greedy.py:86-89, breadth_first.py:79-82)
+ *   acx_search_popped      the ids (discovery index) of the expanded nodes in pop order
+ *   acx_search_found       after a success: the first letters of the found child's relators and
+ *                          len(tree_nodes) - len(to_explore) then (greedy.py:92-95); returns 1
  */
 void* acx_search_create(int32_t mode, int32_t L, const uint64_t* start_key, int64_t max_nodes);
 void acx_search_destroy(void* h);
@@ -287,6 +334,9 @@ int32_t acx_search_status(void* h, int32_t* budget_hit, int32_t* min_length, int
 int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap);
 void acx_search_stats(void* h, int64_t* out);
 int64_t acx_search_node_keys(void* h, uint64_t* out, int64_t cap);
+int64_t acx_search_min_trace(void* h, int32_t* out, int64_t cap);
+int64_t acx_search_popped(void* h, int64_t* ids, int64_t cap);
+int32_t acx_search_found(void* h, int32_t* first_letters, int64_t* explored);
 
 /* number of uint64 words in one packed key: ceil((4L + 16) / 64) */
 int32_t acx_key_words(int32_t L);

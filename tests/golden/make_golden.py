@@ -325,6 +325,28 @@ def gen_unit_cases(ref):
         lens = [int(np.count_nonzero(p[:L])), int(np.count_nonzero(p[L:]))]
         o, ol = M.conjugate(np.array(p), L, i, j, s, list(lens))
         cases["conjugate"].append(dict(p=p, L=L, i=i, j=j, sign=s, out=to_jsonable(o), lengths=to_jsonable(ol)))
+    # test_ACMove (tests/test_ac_env.py:495-538): moves 0..5 from one presentation, cyclical=True
+    cases["acmove"] = []
+    for n in range(12):
+        for cyc in (True, False):
+            p = np.array([1, 2, 0, 0, -2, 0, 0, 0])
+            try:
+                o, ol = M.ACMove(n, p, 4, [4, 4], cyclical=cyc)
+                cases["acmove"].append(dict(p=to_jsonable(p), L=4, move=n, cyclical=cyc, out=to_jsonable(o),
+                                            lengths=to_jsonable(ol), raises=None))
+            except (AssertionError, IndexError) as e:
+                cases["acmove"].append(dict(p=to_jsonable(p), L=4, move=n, cyclical=cyc, raises=type(e).__name__))
+    # the unit cases' letters beyond +-2 through ACMove and simplify_presentation too
+    for p, L in (([1, 2, 0, 3, 4, 0], 3), ([1, 2, 0, 0, 3, 4, 0, 0], 4), ([1, 2, 3, 0, -3, -2, -1, 0], 4),
+                 ([5, -6, 0, 6, 0, 0], 3), ([3, 3, 0, -3, 0, 0], 3)):
+        for n in range(12):
+            for cyc in (True, False):
+                try:
+                    o, ol = M.ACMove(n, np.array(p), L, [0, 0], cyclical=cyc)
+                    cases["acmove"].append(dict(p=p, L=L, move=n, cyclical=cyc, out=to_jsonable(o),
+                                                lengths=to_jsonable(ol), raises=None))
+                except (AssertionError, IndexError) as e:
+                    cases["acmove"].append(dict(p=p, L=L, move=n, cyclical=cyc, raises=type(e).__name__))
     return cases
 
 
@@ -391,6 +413,96 @@ def gen_kat_search_extra(ref, n_cases=240):
         rec["budget_nodes"] = int(m.group(1)) if m else None
         cases.append(rec)
     return cases
+
+
+SCALE_CHECKPOINTS = (1, 10, 100, 1000, 10000, 100000, 1000000)
+
+
+def run_recorded_search(ref, fn, pres, budget, cyclical):
+    """One reference search with ACMove wrapped by a recorder inside the search module's
+    namespace (breadth_first.py:70 / greedy.py:77 call it through their module globals).
+
+    Recorded: the parent-expansion order as a rolling sha256 over the int8 bytes of every
+    parent state in call order (a parent is the `presentation` of an action-0 call, i.e. the
+    node popped at breadth_first.py:62 / greedy.py:72), digests at SCALE_CHECKPOINTS parents,
+    the parent count, the result and path, and everything the search printed with
+    verbose=True (new-minimum lines, the found message, the budget message)."""
+    import contextlib
+    import hashlib
+    import io
+
+    mod = ref.bfs if fn == "bfs" else ref.greedy
+    orig = mod.ACMove
+    h = hashlib.sha256()
+    rec = {"parents": 0, "checkpoints": {}}
+
+    def shim(*args, **kw):
+        move_id = kw.get("move_id", args[0] if args else None)
+        state = kw.get("presentation", args[1] if len(args) > 1 else None)
+        if move_id == 0:
+            h.update(np.asarray(state, np.int8).tobytes())
+            rec["parents"] += 1
+            if rec["parents"] in SCALE_CHECKPOINTS:
+                rec["checkpoints"][str(rec["parents"])] = h.hexdigest()
+        return orig(*args, **kw)
+
+    search = ref.bfs.bfs if fn == "bfs" else ref.greedy.greedy_search
+    buf = io.StringIO()
+    mod.ACMove = shim
+    try:
+        with contextlib.redirect_stdout(buf):
+            ok, path = search(presentation=np.array(pres), max_nodes_to_explore=int(budget), verbose=True,
+                              cyclically_reduce_after_moves=bool(cyclical))
+    finally:
+        mod.ACMove = orig
+    return dict(search_fn=fn, presentation=to_jsonable(np.asarray(pres)), L=len(pres) // 2, budget=int(budget),
+                cyclical=bool(cyclical), ok=bool(ok), path=to_jsonable(path), parents=rec["parents"],
+                digest=h.hexdigest(), checkpoints=rec["checkpoints"], stdout=buf.getvalue().splitlines())
+
+
+def scale_cases(ref):
+    """The search-scale cases (config 4 and its neighbours): AK(3) at L = 36 to 10^6 nodes for
+    both searches, the cyclical variants, a Miller-Schupp start, and near-full relators at
+    L = 128 (totals 254-256, the top of the 8-bit length fields)."""
+    rng = np.random.default_rng(44)
+    ak3 = ref.utils.convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
+    ms = np.load(os.path.join(PKG_DATA, "all_presentations.npy"))
+    ms17 = ref.utils.change_max_relator_length_of_presentation(list(ms[17]), 36)
+    long = []
+    for n0, n1 in ((128, 128), (128, 127), (127, 127)):
+        p = np.zeros(256, np.int8)
+        p[:n0] = random_reduced_word(rng, n0)
+        p[128 : 128 + n1] = random_reduced_word(rng, n1)
+        long.append(p)
+    return [
+        ("bfs", ak3, 10 ** 6, False),
+        ("greedy_search", ak3, 10 ** 6, False),
+        ("bfs", ak3, 2 * 10 ** 5, True),
+        ("greedy_search", ak3, 2 * 10 ** 5, True),
+        ("greedy_search", ms17, 2 * 10 ** 5, False),
+        ("bfs", ms17, 2 * 10 ** 5, False),
+        ("greedy_search", long[0], 3000, False),
+        ("greedy_search", long[1], 3000, False),
+        ("greedy_search", long[2], 3000, True),
+        ("bfs", long[0], 3000, False),
+        ("bfs", long[1], 3000, True),
+    ]
+
+
+def _scale_worker(args):
+    root, k = args
+    ref = load_reference(root)
+    fn, pres, budget, cyc = scale_cases(ref)[k]
+    return run_recorded_search(ref, fn, pres, budget, cyc)
+
+
+def gen_search_scale(root, procs=6):
+    from multiprocessing import Pool
+
+    ref = load_reference(root)
+    n = len(scale_cases(ref))
+    with Pool(procs) as pool:
+        return pool.map(_scale_worker, [(root, k) for k in range(n)], chunksize=1)
 
 
 def gen_features(root, ms, rng):
@@ -544,6 +656,21 @@ if __name__ == "__main__":
         ms = np.load(os.path.join(PKG_DATA, "all_presentations.npy"))
         np.savez_compressed(os.path.join(HERE, "features.npz"),
                             **gen_features(root, ms, np.random.default_rng(11)))
+    elif "--unit" in sys.argv:  # only (re)generate unit_cases.json
+        sys.argv.remove("--unit")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--reference", default="/root/reference")
+        with open(os.path.join(HERE, "unit_cases.json"), "w") as f:
+            json.dump(gen_unit_cases(load_reference(ap.parse_args().reference)), f)
+    elif "--search-scale" in sys.argv:  # only (re)generate search_scale.json
+        sys.argv.remove("--search-scale")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--reference", default="/root/reference")
+        out = gen_search_scale(ap.parse_args().reference)
+        with open(os.path.join(HERE, "search_scale.json"), "w") as f:
+            json.dump(out, f)
+        for r in out:
+            print(r["search_fn"], r["L"], r["budget"], r["cyclical"], r["ok"], r["parents"], r["stdout"][-1:])
     elif "--search-extra" in sys.argv:  # only (re)generate kat_search_extra.json
         sys.argv.remove("--search-extra")
         ap = argparse.ArgumentParser()

@@ -204,3 +204,52 @@ def test_engine_matches_reference_on_random_searches():
             assert path == [tuple(x) for x in c["path"]], c
         if c["budget_nodes"] is not None:
             assert n_nodes == c["budget_nodes"], c
+
+
+def test_engine_matches_reference_scale_cases_at_L128_on_oracle_expansions():
+    """search_scale.json's L = 128 cases (near-full relators, totals 254..256 -- the top of the
+    8-bit length fields and of the greedy priority key's total field): the engine's pop order,
+    result and budget count on oracle expansions equal the reference's."""
+    from conftest import state_digest, unpack_keys_np
+    with open(os.path.join(GOLDEN, "search_scale.json")) as f:
+        cases = [c for c in json.load(f) if c["L"] == 128]
+    assert len(cases) == 5
+    import ctypes
+    for c in cases:
+        p = np.array(c["presentation"])
+        L = c["L"]
+        mode = E.BFS if c["search_fn"] == "bfs" else E.GREEDY
+        lib = _lib.load()
+        kw = _lib.key_words(L)
+        h = lib.acx_search_create(mode, L, E._pack_key(p.astype(np.int64), L).ctypes.data, c["budget"])
+        try:
+            buf = np.zeros((256, kw), np.uint64)
+            status = 0
+            while status == 0:
+                n = lib.acx_search_next_batch(h, buf.ctypes.data, 256)
+                if n == 0:
+                    break
+                parents = unpack_keys_np(buf[:n], L).astype(np.int32)
+                keys = np.ascontiguousarray(_oracle_keys(parents, L, c["cyclical"]))
+                status = lib.acx_search_feed(h, keys.ctypes.data, n)
+            n_nodes = ctypes.c_int64(0)
+            status = lib.acx_search_status(h, None, None, ctypes.byref(n_nodes))
+            npop = lib.acx_search_popped(h, None, 0)
+            pops = np.zeros(npop, np.int64)
+            lib.acx_search_popped(h, pops.ctypes.data, npop)
+            nk = np.zeros((n_nodes.value, kw), np.uint64)
+            lib.acx_search_node_keys(h, nk.ctypes.data, n_nodes.value)
+            ntr = lib.acx_search_min_trace(h, None, 0)
+            tr = np.zeros(max(ntr, 1), np.int32)
+            lib.acx_search_min_trace(h, tr.ctypes.data, ntr)
+        finally:
+            lib.acx_search_destroy(h)
+        assert (status == 1) == c["ok"]
+        assert len(pops) == c["parents"], c["search_fn"]
+        dig, cps = state_digest(unpack_keys_np(nk[pops], L), c["checkpoints"].keys())
+        assert dig == c["digest"] and cps == c["checkpoints"]
+        want = [int(x.split(": ")[1]) for x in c["stdout"] if x.startswith("New minimal")]
+        assert [int(v) for v in tr[:ntr]] == want
+        budget = [x for x in c["stdout"] if x.startswith("Exiting")]
+        assert budget == [f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
+                          f"{c['budget']}"]

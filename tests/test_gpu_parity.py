@@ -482,3 +482,18 @@ def test_step_api_under_hipgraph_capture():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(st_g, st_e) and torch.equal(cnt_g, cnt_e) and torch.equal(rew_g, rew_e)
+
+
+def test_acenv_error_does_not_count_a_step():
+    """A move that raises (ac_env.py:93-95 -> utils.py:264-266) happens before count_steps += 1
+    (ac_env.py:102): a caller that catches it and keeps stepping truncates at the same step as
+    the reference (the device step counter is not advanced either)."""
+    import acx
+    env = acx.ACEnv(acx.ACEnvConfig(initial_state=np.array([1, 0, 1, 0]), horizon_length=2))
+    with pytest.raises(AssertionError):
+        env.step(1)  # r0 <- r0 r1^-1 = x x^-1: empty relator
+    assert env.count_steps == 0 and env.actions == [1]
+    s, r, d, t, info = env.step(4)
+    assert not t and env.count_steps == 1
+    s, r, d, t, info = env.step(4)
+    assert t and env.count_steps == 2

@@ -29,12 +29,13 @@ def _starts(L, B, seed=0):
     return out
 
 
-def _roll(starts, acts, L, H, cyc, pack):
+def _roll(starts, acts, L, H, cyc, pack, count0=None, resets=None):
     from acx import ops
     T, B = acts.shape
     st = torch.as_tensor(starts).to(DEV)
-    rs = st.clone()
-    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    rs = st.clone() if resets is None else torch.as_tensor(resets).to(DEV)
+    cnt = (torch.zeros(B, dtype=torch.int32, device=DEV) if count0 is None
+           else torch.as_tensor(count0.astype(np.int32)).to(DEV))
     obs = torch.full((T, B, 2 * L), -7, dtype=torch.int32, device=DEV)
     rew = torch.zeros((T, B), dtype=torch.int32, device=DEV)
     dn = torch.zeros((T, B), dtype=torch.uint8, device=DEV)
@@ -102,3 +103,100 @@ def test_pack_actions_layout(B):
     for t in range(T):
         want[t // 8] |= ids[t] << np.uint32(4 * (t % 8))
     assert np.array_equal(got, want)
+
+
+def _trivial_starts(L, B):
+    t = np.zeros((8, 2 * L), np.int32)
+    for r, (a0, a1) in enumerate([(1, 2), (1, -2), (-1, 2), (-1, -2), (2, 1), (2, -1), (-2, 1), (-2, -1)]):
+        t[r, 0], t[r, L] = a0, a1
+    return t[np.arange(B) % 8]
+
+
+@pytest.mark.parametrize("L,B,T,H", [(36, 4096, 40, 5), (36, 4096, 60, 50), (36, 1000, 30, 13), (128, 700, 25, 7),
+                                     (17, 333, 20, 9)])
+@pytest.mark.parametrize("kind", ["ms", "trivial"])
+def test_desynchronised_resets_equal_oracle(L, B, T, H, kind):
+    """Episodes out of phase (step_count[i] = i mod H): on every step a scattered subset of each
+    wave resets -- a few lanes (each reads its own starting row) or many (the wave reloads its
+    tile) -- and, with trivial starts, dones fire on a large share of steps.  Both action paths
+    equal the oracle's env replay step by step."""
+    rng = np.random.default_rng(L + T + H)
+    starts = _starts(L, B, seed=H) if kind == "ms" else _trivial_starts(L, B)
+    count0 = (np.arange(B) % H).astype(np.int32)
+    acts = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    a = _roll(starts, acts, L, H, True, pack=False, count0=count0)
+    b = _roll(starts, acts, L, H, True, pack=True, count0=count0)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    st = starts.copy()
+    cnt = count0.copy()
+    n_reset = 0
+    for t in range(T):
+        r, d, tr, e, _, _ = O.env_step(st, acts[t], L, H, cnt, reset_state=starts, cyclical=True)
+        n_reset += int((d | tr).sum())
+        assert np.array_equal(a[2][t], st), t
+        assert np.array_equal(a[3][t], r) and np.array_equal(a[4][t], d) and np.array_equal(a[5][t], tr)
+    assert np.array_equal(a[0], st) and np.array_equal(a[1], cnt)
+    assert int(a[7][0]) == 0 and n_reset > T
+
+
+@pytest.mark.parametrize("L", [36, 128, 17])
+def test_bad_starting_row_fails_env_at_its_reset(L):
+    """A starting row outside the domain is found when the env resets to it: err = 3
+    (ACX_ERR_DOMAIN), the env stops and its state keeps its input; other envs are unaffected."""
+    B, T, H = 256, 12, 4
+    starts = _starts(L, B, seed=3)
+    resets = starts.copy()
+    resets[5, 0] = 3          # a letter outside {-2..2}
+    resets[70, L + 1] = 0     # a zero inside r1 ...
+    resets[70, L + 2] = 1
+    count0 = (np.arange(B) % H).astype(np.int32)
+    rng = np.random.default_rng(9)
+    acts = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    for pack in (False, True):
+        st, cnt, obs, rew, dn, tr, err, ec = _roll(starts, acts, L, H, True, pack=pack, count0=count0, resets=resets)
+        assert err[5] == 3 and err[70] == 3 and int(ec[0]) == 2
+        assert (np.delete(err, [5, 70]) == 0).all()
+        assert np.array_equal(st[5], starts[5]) and np.array_equal(st[70], starts[70])
+        good = np.setdiff1d(np.arange(B), [5, 70])
+        o_st = starts.copy()
+        o_cnt = count0.copy()
+        for t in range(T):
+            O.env_step(o_st, acts[t], L, H, o_cnt, reset_state=resets, cyclical=True)
+            assert np.array_equal(obs[t][good], o_st[good]), t
+        assert np.array_equal(st[good], o_st[good])
+
+
+@pytest.mark.parametrize("L,H", [(36, 5), (36, 60), (128, 7), (17, 9)])
+def test_step_api_desynchronised_resets_equal_oracle(L, H):
+    """acx_step with step_count[i] = i mod H: the per-lane and whole-tile reset paths and
+    final_observation, every step against the oracle."""
+    from acx import ops
+    B, T = 3000, 25
+    rng = np.random.default_rng(H)
+    starts = _starts(L, B, seed=H)
+    count0 = (np.arange(B) % H).astype(np.int32)
+    st = torch.as_tensor(starts).to(DEV)
+    rs = st.clone()
+    cnt = torch.as_tensor(count0).to(DEV)
+    rew = torch.zeros(B, dtype=torch.int32, device=DEV)
+    dn = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    tr = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    lens = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
+    fo = torch.zeros_like(st)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    o_st = starts.copy()
+    o_cnt = count0.copy()
+    for t in range(T):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        ops.step(st, torch.as_tensor(a).to(DEV), state_out=st, reset_state=rs, step_count=cnt, horizon=H,
+                 cyclical=True, reward=rew, done=dn, truncated=tr, lengths=lens, final_obs=fo, err=err)
+        r, d, trn, e, o_len, o_fo = O.env_step(o_st, a, L, H, o_cnt, reset_state=starts, cyclical=True,
+                                               want_final=True)
+        assert np.array_equal(st.cpu().numpy(), o_st), t
+        assert np.array_equal(cnt.cpu().numpy(), o_cnt), t
+        assert np.array_equal(rew.cpu().numpy(), r) and np.array_equal(dn.cpu().numpy(), d)
+        assert np.array_equal(tr.cpu().numpy(), trn) and np.array_equal(lens.cpu().numpy(), o_len)
+        fin = (d | trn).astype(bool)
+        assert np.array_equal(fo.cpu().numpy()[fin], o_fo[fin]), t
+        assert (err.cpu().numpy() == 0).all()

@@ -1,0 +1,125 @@
+"""Config 4 at scale, pinned to the reference itself: tests/golden/search_scale.json holds
+reference runs of bfs / greedy_search (tests/golden/make_golden.py --search-scale) -- AK(3) at
+L = 36 to 10^6 nodes, cyclical variants, a Miller-Schupp start, near-full relators at L = 128 --
+with the parent-expansion order as a rolling sha256 over the parent states (checkpoints at
+1, 10, ..., 10^6 parents), the parent count, the verbose output and the result.
+
+Every GPU engine is checked against them: the device BFS (csrc/acx_bfs.hip, two chunk sizes),
+the host-dedup BFS and greedy over GPU expansions (csrc/acx_search.cpp + acx_expand12) and the
+owner-partitioned BFS at one rank (csrc/acx_sbfs.hip); the 240 reference runs of
+kat_search_extra.json go through the GPU paths too."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, state_digest, unpack_keys_np
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+with open(os.path.join(GOLDEN, "search_scale.json")) as _f:
+    SCALE = json.load(_f)
+BFS_CASES = [c for c in SCALE if c["search_fn"] == "bfs"]
+GREEDY_CASES = [c for c in SCALE if c["search_fn"] == "greedy_search"]
+
+
+def _id(c):
+    return f"L{c['L']}-n{c['budget']}-{'cyc' if c['cyclical'] else 'nocyc'}-{c['presentation'][:3]}"
+
+
+def _check_order(states, c):
+    assert len(states) == c["parents"], (len(states), c["parents"])
+    dig, cps = state_digest(states, c["checkpoints"].keys())
+    assert cps == c["checkpoints"]
+    assert dig == c["digest"]
+
+
+def _result(ok, path):
+    return [bool(ok), None if path is None else [list(x) for x in path]]
+
+
+@pytest.mark.parametrize("chunk", [0, 4099])
+@pytest.mark.parametrize("c", BFS_CASES, ids=_id)
+def test_device_bfs_matches_reference_at_scale(c, chunk, capsys):
+    from acx.search import _device_bfs as D
+    res = D.device_bfs(np.array(c["presentation"]), c["budget"], verbose=True,
+                       cyclically_reduce_after_moves=c["cyclical"], device=DEV, chunk=chunk, keep_node_keys=True)
+    out = capsys.readouterr().out.splitlines()
+    assert out == c["stdout"]
+    assert _result(*res) == [c["ok"], c["path"]]
+    st = D.LAST_STATS
+    assert st["parents"] == c["parents"]
+    _check_order(unpack_keys_np(st["node_keys"][: c["parents"]], c["L"]), c)
+
+
+@pytest.mark.parametrize("c", BFS_CASES, ids=_id)
+def test_host_engine_bfs_matches_reference_at_scale(c, capsys):
+    from acx.search import _engine as E
+    ok, path = E.run_search(E.BFS, np.array(c["presentation"]), c["budget"], True, c["cyclical"], device=DEV,
+                            keep_node_keys=True)
+    out = capsys.readouterr().out.splitlines()
+    assert out == c["stdout"]
+    assert _result(ok, path if ok else None) == [c["ok"], c["path"]]
+    st = E.LAST_STATS
+    _check_order(unpack_keys_np(st["node_keys"][st["popped"]], c["L"]), c)
+
+
+@pytest.mark.parametrize("c", BFS_CASES, ids=_id)
+def test_sharded_bfs_one_rank_matches_reference_at_scale(c, capsys):
+    from acx.search import _sharded_bfs as SB
+    res = SB.sharded_bfs(np.array(c["presentation"]), c["budget"], cyclically_reduce_after_moves=c["cyclical"],
+                         device=DEV, keep_node_keys=True)
+    out = capsys.readouterr().out.splitlines()
+    assert out == [ln for ln in c["stdout"] if ln.startswith("Exiting")]
+    assert _result(*res) == [c["ok"], c["path"]]
+    st = SB.LAST_STATS
+    assert st["parents"] == c["parents"]
+    order = np.argsort(st["node_ids"])
+    keys = st["node_keys"][order][: c["parents"]]
+    _check_order(unpack_keys_np(keys, c["L"]), c)
+    SB.release_workspaces()
+
+
+@pytest.mark.parametrize("c", GREEDY_CASES, ids=_id)
+def test_greedy_matches_reference_at_scale(c, capsys):
+    from acx.search import _engine as E
+    ok, path = E.run_search(E.GREEDY, np.array(c["presentation"]), c["budget"], True, c["cyclical"], device=DEV,
+                            keep_node_keys=True)
+    out = capsys.readouterr().out.splitlines()
+    assert out == c["stdout"]
+    assert [bool(ok), [list(x) for x in path]] == [c["ok"], c["path"]]
+    st = E.LAST_STATS
+    _check_order(unpack_keys_np(st["node_keys"][st["popped"]], c["L"]), c)
+
+
+def test_reference_random_searches_through_gpu_paths():
+    """kat_search_extra.json (240 reference runs, budgets 1..5000, both cyclical flags, runs that
+    raise, the budget message's node count) through acx.bfs (device and host engines) and
+    acx.greedy_search, i.e. with the GPU expansion."""
+    import contextlib
+    import io
+    import re
+
+    import acx
+    with open(os.path.join(GOLDEN, "kat_search_extra.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        pres = np.array(c["presentation"])
+        fns = ([lambda **k: acx.bfs(engine="device", **k), lambda **k: acx.bfs(engine="host", **k)]
+               if c["search_fn"] == "bfs" else [acx.greedy_search])
+        for fn in fns:
+            buf = io.StringIO()
+            kw = dict(presentation=pres, max_nodes_to_explore=c["budget"], cyclically_reduce_after_moves=c["cyclical"])
+            if c["raises"]:
+                with pytest.raises(AssertionError), contextlib.redirect_stdout(buf):
+                    fn(**kw)
+                continue
+            with contextlib.redirect_stdout(buf):
+                ok, path = fn(**kw)
+            assert _result(ok, path) == [c["ok"], c["path"]], c
+            m = re.search(r"number of explored nodes = (\d+)", buf.getvalue())
+            assert (int(m.group(1)) if m else None) == c["budget_nodes"], c

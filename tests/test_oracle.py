@@ -53,6 +53,16 @@ def test_concatenate_conjugate_cases(unit):
         assert out.tolist() == c["out"], c
 
 
+def test_acmove_unit_cases(unit):
+    # tests/test_ac_env.py:495-538 (all 12 moves, both flags) and the unit cases' letters 3..6
+    for c in unit["acmove"]:
+        out, lens, e = O.move(np.array(c["p"]), c["L"], c["move"], c["cyclical"])
+        if c["raises"]:
+            assert e == {"AssertionError": 1, "IndexError": 2}[c["raises"]], c
+        else:
+            assert e == 0 and out.tolist() == c["out"] and list(lens) == c["lengths"], c
+
+
 @pytest.mark.parametrize("L", [7, 18, 36, 128])
 @pytest.mark.parametrize("cyc", [1, 0])
 def test_transitions(L, cyc):

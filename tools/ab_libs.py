@@ -1,9 +1,12 @@
-"""Interleaved A/B of two libacx.so builds in ONE process (cdna_hip_programming.md rule 24).
+"""Interleaved A/B of libacx.so builds in ONE process (cdna_hip_programming.md rule 24).
 
-    python tools/ab_libs.py libA.so libB.so [--reps 7] [--mode rollout|step|expand]
+    python tools/ab_libs.py libA.so libB.so [--reps 7] [--mode rollout|step|expand] [--T 200]
+                            [--desync] [--unpacked]
 
-Each build gets its own ctypes handle (RTLD_LOCAL); both time the same acx_rollout
-(B = 2^20, L = 36, T = 200, all outputs) or 200 acx_step launches, alternating."""
+Each build gets its own ctypes handle (RTLD_LOCAL); all time the same rollout (B = 2^20,
+L = 36, T steps, all outputs; acx_pack_actions + acx_rollout_packed as bench.py does, or
+acx_rollout with --unpacked), T acx_step launches, or an expand12 pass, alternating.
+--desync starts the step counts at i mod H (scattered resets) instead of 0."""
 import argparse
 import ctypes
 import json
@@ -26,6 +29,8 @@ ap.add_argument("--mode", default="rollout")
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--L", type=int, default=36)
 ap.add_argument("--rounds", type=int, default=1, help="fresh output allocations (the speed depends on the mapping)")
+ap.add_argument("--desync", action="store_true")
+ap.add_argument("--unpacked", action="store_true")
 args = ap.parse_args()
 
 libs = []
@@ -43,19 +48,27 @@ starts = torch.as_tensor(ms_starts(L, B)).to(dev)
 g = torch.Generator(device=dev)
 g.manual_seed(0)
 acts = torch.randint(0, 12, (T, B), dtype=torch.int32, device=dev, generator=g)
+packed = torch.empty(((T + 7) // 8, B), dtype=torch.int32, device=dev)
 lens = torch.zeros((B, 2), dtype=torch.int32, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 
 
 def run(lib):
     state = starts.clone()
-    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    cnt = (torch.arange(B, dtype=torch.int32, device=dev) % H) if args.desync else torch.zeros(B, dtype=torch.int32, device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
-    if args.mode == "rollout":
+    if args.mode == "rollout" and args.unpacked:
         rc = lib.acx_rollout(state.data_ptr(), acts.data_ptr(), starts.data_ptr(), cnt.data_ptr(), obs.data_ptr(),
                              rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), None, None, T, B, L, H, 1, stream)
+        assert rc == 0
+    elif args.mode == "rollout":
+        rc = lib.acx_pack_actions(acts.data_ptr(), packed.data_ptr(), T, B, stream)
+        assert rc == 0
+        rc = lib.acx_rollout_packed(state.data_ptr(), packed.data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                    obs.data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), None, None, T, B, L,
+                                    H, 1, stream)
         assert rc == 0
     elif args.mode == "expand":  # config 4's kernel: 12 packed child keys per parent (search setting)
         rc = lib.acx_expand12(exp_par.data_ptr(), None, None, exp_keys.data_ptr(), None, None, exp_par.shape[0], L, 0,

@@ -33,7 +33,10 @@ __global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, 
     uint32_t acc = 0, acts = 0;
     int32_t nv[8];  // prefetched raw action loads of the next batch (consumed 8 steps later)
     if (F & F_ACTPF) {
-        for (int k = 0; k < 8; ++k) nv[k] = act[(int64_t)k * B + env];
+        // rows clamped to T - 1: an unguarded k < 8 read runs past the (T, B) id array when
+        // T < 8 -- the round-1 rollout prefetch faulted the same way on its last batch, reading
+        // rows t + 8.. >= T past the end of the allocation at full size
+        for (int k = 0; k < 8; ++k) nv[k] = act[(int64_t)(k < T ? k : T - 1) * B + env];
     }
     for (int t = 0; t < T; ++t) {
         if ((F & (F_ACT8 | F_ACTPF)) && (t & 7) == 0) {
@@ -112,6 +115,7 @@ __global__ __launch_bounds__(256) void linear_fill(int4* p, int64_t n) {
 
 extern "C" int sp_tile(void* obs, void* rew, void* dn, void* tr, const void* act, int64_t B, int T, int row_chunks,
                        int flags, void* stream) {
+    if (B <= 0 || B % 64 != 0 || T <= 0 || row_chunks <= 0) return -1;  // a wave writes whole 64-row tiles
     dim3 grid((unsigned)((B + 255) / 256));
     switch (flags) {
         CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83) CASE(129)

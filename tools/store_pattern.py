@@ -14,7 +14,7 @@ lib.sp_tile.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int, ct
                                                ctypes.c_void_p]
 lib.sp_linear.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
 dev = torch.device("cuda:0")
-B, T, L = 1 << 20, 200, 36
+B, T, L = int(os.environ.get("SP_B", 1 << 20)), int(os.environ.get("SP_T", 200)), 36
 rc = 2 * L // 4
 obs = torch.zeros((T, B, 2 * L), dtype=torch.int32, device=dev)
 rew = torch.zeros((T, B), dtype=torch.int32, device=dev)
