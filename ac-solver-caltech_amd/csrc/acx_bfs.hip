@@ -28,9 +28,9 @@
 // (`lost`), so survivors are known without re-reading the table.
 //
 // Kernels per chunk of P parents (FIFO indices [head, head + P)):
-//   1. bfs_expand_kernel  wave per tile: parent keys (via queue), 12 moves, child keys staged
-//                         through LDS and written coalesced; first success / move-error seq,
-//                         per-parent min child total;
+//   1. bfs_expand_kernel  block per tile: parent keys (via queue), 3 moves per lane (wave w:
+//                         actions 3w..3w+2), child keys staged through LDS and written
+//                         coalesced; first success / move-error seq, per-parent min child total;
 //   2. bfs_insert_kernel  lane per child (up to the search's last child): probe / claim /
 //                         join the state's table entry;
 //   3. bfs_count_kernel   wave per tile: survivors per tile;
@@ -119,29 +119,36 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// (1) expand: wave per tile of 64 parents, 12 moves per lane, coalesced child-key stores
+// (1) expand: one block per tile of 64 parents; wave w makes the children of actions 3w..3w+2
+// (4x the lanes of a lane-per-parent loop: the move chain is latency-bound, and a 2^19-parent
+// chunk is only ~8 waves per SIMD that way); keys staged through LDS, written coalesced
+constexpr int APW = 12 / (TPB / WAVE);  // actions per wave (3)
 template <int NW>
 __global__ __launch_bounds__(TPB) void bfs_expand_kernel(Args a) {
     __shared__ uint64_t kst[TPB / WAVE][TILE * (NW + 1)];
+    __shared__ uint32_t smin[TILE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-    const int t = blockIdx.x * (TPB / WAVE) + wid;
-    if (t >= a.ntiles) return;  // wave-uniform; no block-wide barrier below
-    const int64_t gt = (a.tile0 + t) * TILE;  // FIFO index of the tile's lane 0
+    const int t = blockIdx.x;  // one tile per block
+    const int64_t gt = (a.tile0 + t) * TILE;  // FIFO index of the tile's parent 0
     const int64_t g = gt + lane;
     const bool active = g >= a.head && g < a.head + a.P;
     const bool full = __ballot(active) == ~0ull;
     const int kw = a.kw;
+    if (wid == 0) smin[lane] = 0xffffu;
     PresRegs<NW> pr;
     bool clean = false;
     if (active) {
         load_key<NW>(a.store + store_index(a.queue[g]) * kw, kw, a.L, pr);
         clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, a.cyc != 0);
     }
+    __syncthreads();
     const uint32_t p = (uint32_t)(g - a.head);
     uint32_t succ = NONE, err = NONE, mn = 0xffffu;
     uint64_t* out = a.store + (1 + (a.tile0 + t) * TILE_CH) * kw;
     uint64_t* st = kst[wid];
-    for (int act = 0; act < 12; ++act) {
+#pragma unroll 1
+    for (int j = 0; j < APW; ++j) {
+        const int act = wid * APW + j;
         if (active) {
             PresRegs<NW> q = pr;
             const int e = clean ? ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, a.cyc != 0)
@@ -172,15 +179,17 @@ __global__ __launch_bounds__(TPB) void bfs_expand_kernel(Args a) {
         }
         wsync();
     }
-    if (active) a.pmin[p] = (uint16_t)mn;
+    if (active) atomicMin(&smin[lane], mn);
     succ = wave_min(succ);
     err = wave_min(err);
-    mn = wave_min(mn);
+    const uint32_t wm = wave_min(mn);
     if (lane == 0) {
         if (succ != NONE) atomicMin(&a.ctl->succ, succ);
         if (err != NONE) atomicMin(&a.ctl->err, err);
-        atomicMin(&a.ctl->min_len, mn);
+        atomicMin(&a.ctl->min_len, wm);
     }
+    __syncthreads();
+    if (wid == 0 && active) a.pmin[p] = (uint16_t)smin[lane];
 }
 
 // chunk-local position (in cand / lost) of the child with code c of this chunk
@@ -485,7 +494,7 @@ struct ChunkLaunch {
         Args& a = S->a;
         const unsigned wb = (unsigned)((a.ntiles + TPB / WAVE - 1) / (TPB / WAVE));
         const int64_t nc = (int64_t)a.ntiles * TILE_CH;
-        bfs_expand_kernel<NW><<<dim3(wb), dim3(TPB), 0, st>>>(a);
+        bfs_expand_kernel<NW><<<dim3((unsigned)a.ntiles), dim3(TPB), 0, st>>>(a);
         bfs_insert_kernel<NW + 1><<<dim3((unsigned)((nc + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(a);
         bfs_count_kernel<<<dim3(wb), dim3(TPB), 0, st>>>(a);
         bfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a);

@@ -237,6 +237,35 @@ struct FastTile {
         wave_sync();
     }
 
+    // the rows of the lanes in the wave-uniform mask `rows` only (a few resetting envs),
+    // cooperatively: lane l loads 16-byte chunk l % CPR of the (l / CPR)-th selected row, so a
+    // wave-instruction fetches 64 / CPR whole rows (3 at L = 36) with one round trip per group
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+        constexpr int RPI = WAVE / CPR;
+        static_assert(RPI >= 1, "a row must fit one wave-instruction");
+        const int s = lane / CPR, c = lane - s * CPR;
+        const int n = __popcll(rows);
+        if ((rows >> lane) & 1ull) flags[lane] = 0;
+        wave_sync();
+        bool any_bad = false;
+        for (int k0 = 0; k0 < n; k0 += RPI) {
+            const int k = k0 + s;
+            if (s < RPI && k < n) {
+                uint64_t m = rows;
+                for (int i = 0; i < k; ++i) m &= m - 1;
+                const int r = __builtin_ctzll(m);
+                const int4 v = reinterpret_cast<const int4*>(g + (int64_t)r * twoL)[c];
+                bool bad = false;
+                lds[r * S + c] = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
+                                 (to_i8(v.w, bad) << 24);
+                if (bad) flags[r] = 1;
+                any_bad |= bad;
+            }
+        }
+        tile_bad = tile_bad || __any(any_bad);
+        wave_sync();
+    }
+
     template <bool NT, bool F32, bool FULL>
     __device__ __forceinline__ void store_flat(int4* dst, int ln, int nc) const {
 #pragma unroll
@@ -454,6 +483,30 @@ struct CodeTile {
         wave_sync();
     }
 
+    // the rows of the lanes in `rows` only (see FastTile::load_rows); a row is >= one
+    // wave-instruction here (CPR >= 16 chunks), so row by row, lanes over its chunks
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+        if ((rows >> lane) & 1ull) flags[lane] = 0;
+        wave_sync();
+        bool any_bad = false;
+        for (uint64_t m = rows; m; m &= m - 1) {
+            const int r = __builtin_ctzll(m);
+            for (int c = lane; c < CPR; c += WAVE) {
+                const int4 v = reinterpret_cast<const int4*>(g + (int64_t)r * twoL)[c];
+                bool bad = false;
+                const uint32_t d = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
+                                   (to_i8(v.w, bad) << 24);
+                uint32_t c8, nz4;
+                swar_pack4(d, c8, nz4);
+                slots(r)[c] = (uint16_t)(c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+                if (bad) flags[r] = 1;
+                any_bad |= bad;
+            }
+        }
+        tile_bad = tile_bad || __any(any_bad);
+        wave_sync();
+    }
+
     // LDS -> R contiguous global rows, exactly CPR store instructions on every path (see
     // FastTile::store_rows)
     template <bool NT>
@@ -596,6 +649,11 @@ struct GenericTile {
     }
     __device__ __forceinline__ void flag_rows(int lane, bool f) {
         if (f) flags[lane] = 1;
+    }
+    // (the generic-L instantiations serve parity, not speed: reload the whole tile)
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
+        (void)rows;
+        load(g, R, lane);
     }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(base + r * rowb); }
 
@@ -756,10 +814,9 @@ __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>&
 }
 
 // One lane packs its own row straight from HBM (per-lane loads, no LDS staging): the same
-// result as tile.load + tile.pack for that row.  Used by the autoreset of a few lanes of a
-// wave, where a coalesced reload of the whole 64-row tile would move 64 rows to use a few.
-// Rolled loops (one load in flight): it is a rare path and must not add register pressure
-// to the kernels that inline it.
+// result as tile.load + tile.pack for that row.  Only for a step-kernel env whose starting row
+// turned out invalid (it keeps its input row, whose lengths are re-read here).  Rolled loops
+// (one load in flight): a rare path that must not add register pressure to the kernel.
 template <int NW, int LC>
 __device__ __forceinline__ bool pack_row_global(const int32_t* __restrict__ row, int Lr, PresRegs<NW>& p) {
     const int L = LC > 0 ? LC : Lr;
@@ -805,9 +862,9 @@ __device__ __forceinline__ bool pack_row_global(const int32_t* __restrict__ row,
 }
 
 // A wave reloads its whole tile of starting states (one coalesced pass) when more than this
-// many of its lanes reset on the same step (a synchronised truncation); fewer resetting lanes
-// each read their own row (pack_row_global), so scattered resets cost their own rows only.
-constexpr int RESET_TILE_MIN = 8;
+// many of its lanes reset on the same step (a synchronised truncation); for fewer resetting
+// lanes the wave loads just their rows (tile.load_rows), so scattered resets cost their rows.
+constexpr int RESET_TILE_MIN = 24;
 
 // common per-wave prologue: tile index, rows in the tile, LDS slice
 struct WaveCtx {
@@ -931,9 +988,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             if (w.active && !keep) tile.unpack(w.lane, p);
             tile.restore_flags(w.lane, w.active && keep);
         } else {
-            // a few lanes: each reads its own starting row (scattered resets cost their rows only)
+            // a few lanes: the wave loads just their rows (scattered resets cost their rows only)
+            tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
             if (reset) {
-                rbad = pack_row_global<NW, LC>(a.reset_state + env * twoL, L, p);
+                rbad = tile.pack(w.lane, p);
                 if (!rbad) tile.unpack(w.lane, p);
             }
             keep = keep || rbad;
@@ -1052,8 +1110,9 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
                 if (reset) rbad = tile.pack(w.lane, p);
                 wave_sync();
-            } else if (reset) {  // a few lanes: their own rows only
-                rbad = pack_row_global<NW, LC>(a.reset_state + (w.r0 + ln) * twoL, L, p);
+            } else {  // a few lanes: the wave loads just their rows
+                tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
+                if (reset) rbad = tile.pack(w.lane, p);
             }
             if (reset) {
                 clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
@@ -1262,6 +1321,106 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
     if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
 }
 
+// expand12 without int32 children (the search path: packed child keys, optional lengths/err):
+// one block of 4 waves per tile of 64 parents; wave 0 stages and packs the tile, every wave then
+// makes the children of 3 actions (wave w: 3w..3w+2) -- 4x the lanes of a lane-per-parent loop
+// over 12 moves, whose dependent VALU chain left most issue slots empty -- and the block's
+// 12 * 64 keys are staged in LDS (parent-major, as in HBM) and written as one contiguous run.
+constexpr int KEYS_APW = 12 / WPB;  // actions per wave (3)
+
+template <int NW>
+__host__ __device__ constexpr int packed_words() { return 2 * NW + 2; }
+
+template <int NW, int LC, int VEC>
+struct ExpandKeysSmem {
+    static __host__ __device__ size_t region_a(int L) {
+        const size_t t = TileFor<NW, LC, VEC>::wave_bytes(L);
+        const size_t k = (size_t)WAVE * 12 * (size_t)((4 * L + 16 + 63) / 64) * 8;
+        return ((t > k ? t : k) + 15) & ~(size_t)15;
+    }
+    static __host__ __device__ size_t bytes(int L) { return region_a(L) + (size_t)WAVE * packed_words<NW>() * 4; }
+};
+
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
+    using Smem = ExpandKeysSmem<NW, LC, VEC>;
+    constexpr int PW = packed_words<NW>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t r0 = (int64_t)blockIdx.x * WAVE;
+    if (r0 >= a.N) return;  // block-uniform
+    const int R = (int)((a.N - r0) < WAVE ? (a.N - r0) : WAVE);
+    const int L = LC > 0 ? LC : a.L;
+    const int kw = LC > 0 ? (4 * LC + 16 + 63) / 64 : a.kw64;
+    char* region = smem;
+    uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::region_a(a.L));
+    const bool cyc = a.cyclical != 0;
+    if (wid == 0) {
+        Tile tile(region, a.L);
+        tile.load(a.parents + r0 * 2 * L, R, lane);
+        if (lane < R) {
+            PresRegs<NW> p;
+            const bool bad = tile.pack(lane, p);
+            const bool clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+            uint32_t* d = packed + lane * PW;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                d[k] = p.w0.w[k];
+                d[NW + k] = p.w1.w[k];
+            }
+            d[2 * NW] = (uint32_t)p.n0 | ((uint32_t)p.n1 << 8);
+            d[2 * NW + 1] = (uint32_t)bad | ((uint32_t)clean << 1);
+        }
+    }
+    __syncthreads();
+    uint64_t* kst = reinterpret_cast<uint64_t*>(region);
+    int nerr = 0;
+    if (lane < R) {
+        PresRegs<NW> p;
+        const uint32_t* d = packed + lane * PW;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            p.w0.w[k] = d[k];
+            p.w1.w[k] = d[NW + k];
+        }
+        p.n0 = (int)(d[2 * NW] & 0xffu);
+        p.n1 = (int)((d[2 * NW] >> 8) & 0xffu);
+        const bool bad = (d[2 * NW + 1] & 1u) != 0, clean = (d[2 * NW + 1] & 2u) != 0;
+        const int64_t par = r0 + lane;
+#pragma unroll 1
+        for (int j = 0; j < KEYS_APW; ++j) {
+            const int act = wid * KEYS_APW + j;
+            PresRegs<NW> q = p;
+            int e;
+            if (bad) e = ACX_ERR_DOMAIN;
+            else if (clean) e = ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            else e = ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            const int64_t ci = par * 12 + act;
+            nerr += e != ACX_ERR_NONE;
+            if (a.err) a.err[ci] = (uint8_t)e;
+            if (a.child_len) {
+                a.child_len[2 * ci] = q.n0;
+                a.child_len[2 * ci + 1] = q.n1;
+            }
+            if (e != ACX_ERR_NONE) {  // the error sentinel: both length bytes 0xFF (acx.h)
+                q.n0 = 0xff;
+                q.n1 = 0xff;
+            }
+            uint64_t key[NW + 1];
+            make_key<NW>(L, q, key);
+#pragma unroll
+            for (int k = 0; k < NW + 1; ++k)
+                if (k < kw) kst[(lane * 12 + act) * kw + k] = key[k];
+        }
+    }
+    __syncthreads();
+    uint64_t* dst = a.child_key + r0 * 12 * kw;
+    for (int i = threadIdx.x; i < R * 12 * kw; i += BLOCK) dst[i] = kst[i];
+    if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
+}
+
 struct CanonArgs {
     const int32_t* state_in;
     int32_t* state_out;
@@ -1403,6 +1562,11 @@ struct ExpandLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
+        const size_t kshm = ExpandKeysSmem<NW, LC, VEC>::bytes(a.L);
+        if (!a.children && a.child_key && kshm <= 40 * 1024) {  // the search path
+            expand12_keys_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), kshm, s>>>(a);
+            return finish_launch();
+        }
         const size_t shm = (size_t)WPB * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L);
         expand12_kernel<NW, LC, VEC><<<dim3(grid_for(a.N)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();

@@ -11,11 +11,13 @@
 //   F_PACK8   pre-packed actions: one uint32 (8 ids x 4 bits) per lane per 8 steps
 //   F_BLK     the block's 4 waves write its 4 tiles interleaved (wave k: every 4th KB) after a
 //             per-step barrier: 4 KB contiguous per store instruction round instead of 1 KB
+//   F_ROT     each wave starts its tile's stores at chunk (tile mod row_chunks), so waves in
+//             lockstep do not all write the same offset of their tiles at the same time
 // Compared with the same bytes written linearly (grid-stride, like a fill).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-enum { F_NT = 1, F_SCAL = 2, F_ACT8 = 4, F_ACTPF = 8, F_LDS = 16, F_ACT32 = 32, F_PACK8 = 64, F_BLK = 128 };
+enum { F_NT = 1, F_SCAL = 2, F_ACT8 = 4, F_ACTPF = 8, F_LDS = 16, F_ACT32 = 32, F_PACK8 = 64, F_BLK = 128, F_ROT = 256 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -89,6 +91,14 @@ __global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, 
                 const v4i x = {v.x, v.y, v.z, v.w};
                 __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(bdst + (u * 4 + wid) * 64));
             }
+        } else if (F & F_ROT) {
+            const int rot = (int)(tile % row_chunks);
+            for (int u = 0; u < row_chunks; ++u) {
+                int uu = u + rot;
+                uu = uu >= row_chunks ? uu - row_chunks : uu;
+                v4i x = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(dst + uu * 64));
+            }
         } else {
             for (int u = 0; u < row_chunks; ++u) {
                 if (F & F_NT) {
@@ -100,6 +110,32 @@ __global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, 
             }
         }
     }
+}
+
+// each wave owns TWO 64-row tiles and writes both every step (4 waves/SIMD, so a 2^20-env batch
+// is resident in one round instead of two rounds of one-tile waves)
+__global__ __launch_bounds__(256, 4) void tile2_pattern(int4* obs, int64_t B, int T, int row_chunks) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + wid;
+    if (pair * 128 >= B) return;
+    const int64_t chunks_per_step = B * row_chunks;
+    int4 v = make_int4(lane, 1, 2, 3);
+    for (int t = 0; t < T; ++t) {
+        v.y += 1;
+        for (int h = 0; h < 2; ++h) {
+            int4* dst = obs + t * chunks_per_step + (2 * pair + h) * 64 * row_chunks + lane;
+            for (int u = 0; u < row_chunks; ++u) {
+                v4i x = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(dst + u * 64));
+            }
+        }
+    }
+}
+extern "C" int sp_tile2(void* obs, int64_t B, int T, int row_chunks, void* stream) {
+    if (B <= 0 || B % 128 != 0 || T <= 0) return -1;
+    tile2_pattern<<<(unsigned)((B + 511) / 512), 256, 0, (hipStream_t)stream>>>((int4*)obs, B, T, row_chunks);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 __global__ __launch_bounds__(256) void linear_fill(int4* p, int64_t n) {
@@ -118,9 +154,21 @@ extern "C" int sp_tile(void* obs, void* rew, void* dn, void* tr, const void* act
     if (B <= 0 || B % 64 != 0 || T <= 0 || row_chunks <= 0) return -1;  // a wave writes whole 64-row tiles
     dim3 grid((unsigned)((B + 255) / 256));
     switch (flags) {
-        CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83) CASE(129)
+        CASE(0) CASE(1) CASE(3) CASE(5) CASE(9) CASE(7) CASE(11) CASE(17) CASE(19) CASE(23) CASE(27) CASE(33) CASE(51) CASE(65) CASE(83) CASE(129) CASE(257)
         default: return -1;
     }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+// each thread writes `per` consecutive 16-byte vectors (torch's elementwise launch shape)
+__global__ __launch_bounds__(256) void chunk_fill(int4* p, int64_t n, int per) {
+    int4 v = make_int4(1, 2, 3, 4);
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * per;
+    for (int k = 0; k < per; ++k)
+        if (i0 + k < n) p[i0 + k] = v;
+}
+extern "C" int sp_chunk(void* p, int64_t n16, int per, void* stream) {
+    const int64_t threads = (n16 + per - 1) / per;
+    chunk_fill<<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>((int4*)p, n16, per);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 extern "C" int sp_linear(void* p, int64_t n16, int blocks, void* stream) {

@@ -13,6 +13,7 @@ lib = ctypes.CDLL(so)
 lib.sp_tile.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_void_p]
 lib.sp_linear.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+lib.sp_chunk.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
 dev = torch.device("cuda:0")
 B, T, L = int(os.environ.get("SP_B", 1 << 20)), int(os.environ.get("SP_T", 200)), 36
 rc = 2 * L // 4
@@ -37,7 +38,7 @@ def timeit(fn, name, nbytes):
     res[name] = {"ms": round(best, 4), "GBps": round(nbytes / best / 1e6, 1)}
 
 
-NAMES = {1: "NT", 2: "SCAL", 4: "ACT8", 8: "ACTPF", 16: "LDS", 32: "ACT32", 64: "PACK8", 128: "BLK"}
+NAMES = {1: "NT", 2: "SCAL", 4: "ACT8", 8: "ACTPF", 16: "LDS", 32: "ACT32", 64: "PACK8", 128: "BLK", 256: "ROT"}
 import sys as _sys
 flag_list = [int(x) for x in _sys.argv[1].split(",")] if len(_sys.argv) > 1 else [1, 5, 33, 65, 19, 23, 51, 83, 1, 19]
 for flags in flag_list:
@@ -46,7 +47,12 @@ for flags in flag_list:
     name = name if name not in res else name + "_again"
     timeit(lambda: lib.sp_tile(obs.data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), act.data_ptr(), B, T, rc,
                                flags, s), name, nb)
-for blocks in (8192,):
+lib.sp_tile2.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+if os.environ.get("SP_TILE2"):
+    timeit(lambda: lib.sp_tile2(obs.data_ptr(), B, T, rc, s), "tile2_NT", obs_bytes)
+for blocks in [int(x) for x in os.environ.get("SP_BLOCKS", "8192").split(",")]:
     timeit(lambda: lib.sp_linear(obs.data_ptr(), obs_bytes // 16, blocks, s), f"linear_{blocks}", obs_bytes)
+for per in [int(x) for x in os.environ.get("SP_PER", "").split(",") if x]:
+    timeit(lambda: lib.sp_chunk(obs.data_ptr(), obs_bytes // 16, per, s), f"chunk_{per}", obs_bytes)
 timeit(lambda: (obs.fill_(3), 0)[1], "torch_fill", obs_bytes)
 print(json.dumps(res, indent=0))
