@@ -60,6 +60,16 @@ SIGNATURES = {
     "acx_search_min_trace": ([_P, _P, _I64], ctypes.c_int64),
     "acx_search_popped": ([_P, _P, _I64], ctypes.c_int64),
     "acx_search_found": ([_P, _P, _P], ctypes.c_int32),
+    # greedy with the device visited set (ac-solver-caltech_amd/csrc/acx_greedy.hip)
+    "acx_greedy_run": ([_P, _I32, _I64, _I32, _I32, _P], ctypes.c_int),
+    "acx_greedy_destroy": ([_P], None),
+    "acx_greedy_status": ([_P, _P, _P, _P], ctypes.c_int32),
+    "acx_greedy_path": ([_P, _P, _P, _I64], ctypes.c_int64),
+    "acx_greedy_stats": ([_P, _P], None),
+    "acx_greedy_min_trace": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_greedy_popped": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_greedy_node_keys": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_greedy_found": ([_P, _P, _P], ctypes.c_int32),
     # device BFS (ac-solver-caltech_amd/csrc/acx_bfs.hip)
     "acx_bfs_create": ([_I32, _I64, _I64, _I32], ctypes.c_void_p),
     "acx_bfs_run": ([_P, _P, _I64, _P, _P, _I64, _P, _P], ctypes.c_int),

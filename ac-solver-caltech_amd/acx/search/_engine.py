@@ -5,6 +5,7 @@ reference's sequential pop / expand / dedup / budget logic on those keys."""
 from __future__ import annotations
 
 import ctypes
+import time
 
 import numpy as np
 import torch
@@ -49,13 +50,84 @@ def _devices(device):
     return [torch.device(device if device is not None else "cuda")]
 
 
+def _print_verbose_found(lib_found, h, path):
+    first = np.zeros(2, np.int32)
+    explored = ctypes.c_int64(0)
+    lib_found(h, first.ctypes.data, ctypes.byref(explored))
+    found = (np.array([first[0]], np.int8), np.array([first[1]], np.int8))
+    print(f"Found {found} after exploring {explored.value} nodes")  # greedy.py:92-99
+    print(f"Path to a trivial state: (tuples are of form (action, length of a state)) {path}")
+    print(f"Total path length: {len(path)}")
+
+
+def run_greedy_device(p, max_nodes_to_explore, verbose, cyclical, device=None, batch=None, keep_node_keys=False):
+    """greedy_search on one GPU with the device visited set (csrc/acx_greedy.hip): the expansion
+    rounds run in C++ (no Python per round)."""
+    L = len(p) // 2
+    dev = _devices(device)[0]
+    lib = _lib.load()
+    kw = _lib.key_words(L)
+    pres = np.ascontiguousarray(p, dtype=np.int32)
+    h = ctypes.c_void_p(0)
+    with torch.cuda.device(dev):
+        st = lib.acx_greedy_run(pres.ctypes.data, L, max(int(max_nodes_to_explore), 1), int(bool(cyclical)),
+                                int(batch or 0), ctypes.byref(h))
+    try:
+        if st != _lib.OK:
+            _lib.check(st, "acx_greedy_run")
+        stats = np.zeros(7, np.int64)
+        lib.acx_greedy_stats(h, stats.ctypes.data)
+        budget = ctypes.c_int32(0)
+        min_len = ctypes.c_int32(0)
+        n_nodes = ctypes.c_int64(0)
+        status = lib.acx_greedy_status(h, ctypes.byref(budget), ctypes.byref(min_len), ctypes.byref(n_nodes))
+        LAST_STATS.clear()
+        LAST_STATS.update(rounds=int(stats[0]), expanded=int(stats[1]), pops=int(stats[2]),
+                          device_known_children=int(stats[3]), host_select_s=stats[4] / 1e9,
+                          gpu_roundtrip_s=stats[5] / 1e9, host_replay_s=stats[6] / 1e9, nodes=int(n_nodes.value),
+                          status=int(status), min_length=int(min_len.value), engine="device-visited-set")
+        ntr = lib.acx_greedy_min_trace(h, None, 0)
+        trace = np.zeros(max(ntr, 1), np.int32)
+        lib.acx_greedy_min_trace(h, trace.ctypes.data, ntr)
+        LAST_STATS["min_trace"] = [int(v) for v in trace[:ntr]]
+        if keep_node_keys:
+            nk = np.zeros((n_nodes.value, kw), np.uint64)
+            lib.acx_greedy_node_keys(h, nk.ctypes.data, n_nodes.value)
+            LAST_STATS["node_keys"] = nk
+            npop = lib.acx_greedy_popped(h, None, 0)
+            pops = np.zeros(max(npop, 1), np.int64)
+            lib.acx_greedy_popped(h, pops.ctypes.data, npop)
+            LAST_STATS["popped"] = pops[:npop]
+        if verbose:  # greedy.py:86-89
+            for v in LAST_STATS["min_trace"]:
+                print(f"New minimal length found: {v}")
+        if status == 3:
+            raise AssertionError("a move produced an invalid presentation (utils.py:264-266)")
+        cap = 1 << 16
+        acts = np.zeros(cap, np.int32)
+        tots = np.zeros(cap, np.int32)
+        m = lib.acx_greedy_path(h, acts.ctypes.data, tots.ctypes.data, cap)
+        path = [(int(acts[i]), int(tots[i])) for i in range(min(m, cap))]
+        if verbose and status == 1:
+            _print_verbose_found(lib.acx_greedy_found, h, path)
+        if budget.value:
+            print(f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
+                  f"{max_nodes_to_explore}")
+        return status == 1, path
+    finally:
+        if h.value:
+            lib.acx_greedy_destroy(h)
+
+
 def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, device=None, batch=None,
-               keep_node_keys=False):
+               keep_node_keys=False, engine=None):
     p = np.asarray(presentation)
     assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
     L = len(p) // 2
     if np.any(np.abs(p) > 2):
         raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
+    if mode == GREEDY and engine in (None, "device") and not isinstance(device, (list, tuple)):
+        return run_greedy_device(p, max_nodes_to_explore, verbose, cyclical, device, batch, keep_node_keys)
     devs = _devices(device)
     lib = _lib.load()
     kw = _lib.key_words(L)
@@ -78,10 +150,12 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
                          torch.empty((per, 2 * L), dtype=torch.int32, device=d),
                          {"keys": torch.empty((per, 12, kw), dtype=torch.int64, device=d)}))
         status = 0
+        t_gpu = 0.0
         while status == 0:
             n = lib.acx_search_next_batch(h, parent_keys.ctypes.data, batch)
             if n == 0:
                 break
+            g0 = time.perf_counter()
             pinned_in[:n].numpy()[:] = parent_keys[:n].view(np.int64)
             # contiguous parent slices, one per GPU, launched asynchronously on each GPU's stream
             bounds = [n * g // G for g in range(G + 1)]
@@ -98,11 +172,13 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
                     pinned_out[a:b].copy_(res["keys"][: b - a], non_blocking=True)
             for d in devs:
                 torch.cuda.synchronize(d)
+            t_gpu += time.perf_counter() - g0
             status = lib.acx_search_feed(h, pinned_out.data_ptr(), n)
-        st = np.zeros(3, np.int64)
+        st = np.zeros(6, np.int64)
         lib.acx_search_stats(h, st.ctypes.data)
         LAST_STATS.clear()
-        LAST_STATS.update(rounds=int(st[0]), expanded=int(st[1]), pops=int(st[2]))
+        LAST_STATS.update(rounds=int(st[0]), expanded=int(st[1]), pops=int(st[2]), host_next_s=st[3] / 1e9,
+                          host_store_s=st[4] / 1e9, host_replay_s=st[5] / 1e9, gpu_roundtrip_s=t_gpu)
         budget = ctypes.c_int32(0)
         min_len = ctypes.c_int32(0)
         n_nodes = ctypes.c_int64(0)
@@ -131,14 +207,8 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
         tots = np.zeros(cap, np.int32)
         m = lib.acx_search_path(h, acts.ctypes.data, tots.ctypes.data, cap)
         path = [(int(acts[i]), int(tots[i])) for i in range(min(m, cap))]
-        if verbose and status == 1 and mode == GREEDY:  # greedy.py:92-99
-            first = np.zeros(2, np.int32)
-            explored = ctypes.c_int64(0)
-            lib.acx_search_found(h, first.ctypes.data, ctypes.byref(explored))
-            found = (np.array([first[0]], np.int8), np.array([first[1]], np.int8))
-            print(f"Found {found} after exploring {explored.value} nodes")
-            print(f"Path to a trivial state: (tuples are of form (action, length of a state)) {path}")
-            print(f"Total path length: {len(path)}")
+        if verbose and status == 1 and mode == GREEDY:
+            _print_verbose_found(lib.acx_search_found, h, path)
         if budget.value:
             print(
                 f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "

@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "acx", "libacx.so")
 INCLUDE = os.path.join(REPO, "include")
 SOURCES = ["acx_kernels.hip", "acx_bfs.hip", "acx_sbfs.hip", "acx_features.hip", "acx_curriculum.hip", "acx_words.hip",
-           "acx_search.cpp"]
+           "acx_greedy.hip", "acx_search.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ACX_OFFLOAD_ARCH", "gfx950")
 

@@ -90,6 +90,7 @@ struct Args {
     uint8_t* lost;     // (ntiles * 768) another child of the chunk replaced its entry (zeroed per chunk)
     uint16_t* pmin;    // (pmax) min child total per parent, 0xffff when every move raised
     uint32_t* tsum;    // (tiles) survivors per tile -> exclusive offsets
+    uint32_t* tmin;    // (tiles) min child total per tile
     uint64_t* table;   // (buckets * 8) visited set
     Ctl* ctl;
     uint16_t* trace;   // (TRACE_CAP) the trace walk's new minima
@@ -180,16 +181,22 @@ __global__ __launch_bounds__(TPB) void bfs_expand_kernel(Args a) {
         wsync();
     }
     if (active) atomicMin(&smin[lane], mn);
+    // success / move error are rare: one global atomic per wave that has one; the chunk's min
+    // child total goes through a per-tile value the scan kernel reduces (a same-address atomic
+    // from every wave of a chunk serialises: 4x the waves made it cost 90 us per chunk)
     succ = wave_min(succ);
     err = wave_min(err);
-    const uint32_t wm = wave_min(mn);
     if (lane == 0) {
         if (succ != NONE) atomicMin(&a.ctl->succ, succ);
         if (err != NONE) atomicMin(&a.ctl->err, err);
-        atomicMin(&a.ctl->min_len, wm);
     }
     __syncthreads();
-    if (wid == 0 && active) a.pmin[p] = (uint16_t)smin[lane];
+    if (wid == 0) {
+        const uint32_t m = smin[lane];
+        if (active) a.pmin[p] = (uint16_t)m;
+        const uint32_t tm = wave_min(m);
+        if (lane == 0) a.tmin[t] = tm;
+    }
 }
 
 // chunk-local position (in cand / lost) of the child with code c of this chunk
@@ -300,8 +307,13 @@ __global__ __launch_bounds__(1024) void bfs_scan_kernel(Args a) {
     const int nb = a.ntiles;
     const int per = (nb + 1023) / 1024;
     const int b0 = t * per, b1 = min(nb, b0 + per);
-    uint32_t loc = 0;
-    for (int i = b0; i < b1; ++i) loc += a.tsum[i];
+    uint32_t loc = 0, mn = 0xffffffffu;
+    for (int i = b0; i < b1; ++i) {
+        loc += a.tsum[i];
+        mn = min(mn, a.tmin[i]);
+    }
+    mn = wave_min(mn);
+    if (lane == 0) atomicMin(&a.ctl->min_len, mn);  // 16 per chunk
     uint32_t x = loc;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -470,7 +482,8 @@ struct Search {
     std::vector<int32_t> trace;  // new minima of the last run, in order
 
     ~Search() {
-        void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.table, a.ctl, a.trace, path_dev, path_n_dev};
+        void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.tmin, a.table, a.ctl, a.trace, path_dev,
+                        path_n_dev};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
@@ -544,14 +557,17 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     S->tiles_max = S->pmax / TILE + 2;
     // every parent that can be expanded (< qcap) has its 12 child slots; one spare tile
     S->scap = 1 + ((S->qcap + TILE - 1) / TILE + 1) * TILE_CH;
-    // every node and every claimed chunk entry at load <= 1/2, buckets of 8
+    // every node and every claimed chunk entry at load <= 1/2, buckets of 8 (one 64-B line per
+    // probe).  (Half that -- load <= 1, 134 MB at 10^7 nodes, inside the 256 MB MALL -- measured
+    // 1.83 vs 1.93 ms at 10^7 but 18.4 vs 17.0 ms at 10^8 nodes: not taken.)
     uint64_t ts = 1024;
     while (ts < 2 * (uint64_t)(S->qcap + 12 * S->pmax)) ts <<= 1;
     S->tsize = ts;
     Args& a = S->a;
     bool ok = dalloc(a.store, (size_t)(S->scap * S->kw)) && dalloc(a.queue, (size_t)S->qcap) &&
               dalloc(a.cand, (size_t)(S->tiles_max * TILE_CH)) && dalloc(a.lost, (size_t)(S->tiles_max * TILE_CH)) &&
-              dalloc(a.pmin, (size_t)S->pmax) && dalloc(a.tsum, (size_t)S->tiles_max) && dalloc(a.table, (size_t)ts) &&
+              dalloc(a.pmin, (size_t)S->pmax) && dalloc(a.tsum, (size_t)S->tiles_max) &&
+              dalloc(a.tmin, (size_t)S->tiles_max) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.trace, (size_t)TRACE_CAP) && dalloc(S->path_dev, (size_t)(2 * PATH_CAP)) &&
               dalloc(S->path_n_dev, 1) &&
               hipHostMalloc((void**)&S->ctl_host, sizeof(Ctl), hipHostMallocDefault) == hipSuccess &&

@@ -1,0 +1,715 @@
+// acx_greedy.hip -- greedy_search (ac_solver/search/greedy.py:15-121) with the visited set on the
+// device and the expansion rounds driven from C++.
+//
+// The reference pops the smallest (total, path length, state tuple) node, expands it with 12
+// ACMove calls, tests each child (min length, success = total 2) and pushes the unseen ones.  The
+// pop order is inherently sequential; what moves to the GPU is everything around it:
+//   * expansion -- every round, the smallest frontier nodes not yet expanded (a second heap of
+//     the unexpanded nodes) are expanded speculatively in one launch, lane per (parent, action),
+//     from their packed keys; each child's key hash is computed there too;
+//   * the visited set -- the keys of all committed nodes live in HBM with a bucketed hash table
+//     (as in the device BFS); the expansion kernel probes it, so every child that is already a
+//     node (as of that round) comes back marked with the node's id and the host never looks it
+//     up.  Nodes the host appends are committed to the device table at the start of the next
+//     round.
+// The host replays the reference's order exactly: pops while the frontier's top has cached
+// children; a child the device did not know is checked only against the nodes appended since
+// its round (the in-flight conflicts), kept in a host table of the last 2^20..2^21 appended
+// nodes; children cached before the last 2^20 appends are dropped and their parent re-expanded
+// when it comes up again, which bounds that table.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <new>
+#include <vector>
+
+#include "acx.h"
+#include "acx_moves.h"
+
+#include "acx_bfs_common.h"
+
+namespace acx {
+namespace greedy {
+
+using bfs::fmix64;
+using bfs::Key;
+using bfs::keq;
+using bfs::khash;
+using bfs::kload;
+
+constexpr int ACT = 12;
+constexpr int BUCKET = 8;
+constexpr uint32_t FP_MASK = 0xffffffu;
+constexpr int HDR = 40;  // priority-key header bits: total (9) | path length (31)
+constexpr int64_t AGE = 1 << 20;  // a cached expansion stays usable while fewer nodes than this have been
+                                  // appended since its probe (bounds the in-flight table)
+
+struct DevArgs {
+    const uint64_t* parents;  // (n, kw) keys of the round's parents
+    uint64_t* ckeys;          // (n, 12, kw) child keys (error sentinel: both length bytes 0xFF)
+    uint64_t* chash;          // (n, 12) child key hashes
+    int64_t* cknown;          // (n, 12) id of the node the child equals, -1 if none (as of this round)
+    uint64_t* nkeys;          // (cap, kw) node keys by id
+    const uint64_t* commit;   // (hi - lo, kw) keys of the nodes being committed
+    uint64_t* table;          // buckets of 8: (id + 1) << 24 | fp24
+    uint64_t bmask;
+    int64_t lo, hi;           // commit: node ids [lo, hi)
+    int n, L, kw, cyc;
+};
+
+// lane per (parent, action): one move, the child's key, its hash, its id if already a node
+template <int NW>
+__global__ __launch_bounds__(256) void greedy_expand_kernel(DevArgs a) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.n * ACT) return;
+    const int p = t / ACT, act = t - p * ACT;
+    PresRegs<NW> q;
+    load_key<NW>(a.parents + (int64_t)p * a.kw, a.kw, a.L, q);
+    const bool cyc = a.cyc != 0;
+    const int e = is_clean<NW>(q.w0, q.n0, q.w1, q.n1, cyc) ? ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc)
+                                                             : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc);
+    if (e != ACX_ERR_NONE) {
+        q.n0 = 0xff;
+        q.n1 = 0xff;
+    }
+    uint64_t key[NW + 1];
+    make_key<NW>(a.L, q, key);
+    uint64_t* dst = a.ckeys + (int64_t)t * a.kw;
+#pragma unroll
+    for (int k = 0; k < NW + 1; ++k)
+        if (k < a.kw) dst[k] = key[k];
+    Key<NW + 1> kk;
+#pragma unroll
+    for (int k = 0; k < NW + 1; ++k) kk.w[k] = k < a.kw ? key[k] : 0ull;
+    const uint64_t h = khash<NW + 1>(kk, a.kw);
+    a.chash[t] = h;
+    int64_t known = -1;
+    if (e == ACX_ERR_NONE) {
+        const uint32_t fp = (uint32_t)(h >> 40);
+        uint64_t b = h & a.bmask;
+        for (uint64_t it = 0; it <= a.bmask && known < 0; ++it) {
+            const uint64_t* bk = a.table + b * BUCKET;
+            bool empty = false;
+#pragma unroll
+            for (int j = 0; j < BUCKET; ++j) {
+                const uint64_t v = bk[j];
+                if (v == 0) {
+                    empty = true;
+                    break;
+                }
+                if (((uint32_t)v & FP_MASK) == fp) {
+                    const int64_t id = (int64_t)(v >> 24) - 1;
+                    if (keq<NW + 1>(a.nkeys + id * a.kw, kk, a.kw)) {
+                        known = id;
+                        break;
+                    }
+                }
+            }
+            if (empty) break;
+            b = (b + 1) & a.bmask;
+        }
+    }
+    a.cknown[t] = known;
+}
+
+// commit the node ids [lo, hi): store their keys and enter them in the table (all distinct, new)
+template <int KWM>
+__global__ __launch_bounds__(256) void greedy_commit_kernel(DevArgs a) {
+    const int64_t id = a.lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (id >= a.hi) return;
+    const Key<KWM> k = kload<KWM>(a.commit + (id - a.lo) * a.kw, a.kw);
+#pragma unroll
+    for (int i = 0; i < KWM; ++i)
+        if (i < a.kw) a.nkeys[id * a.kw + i] = k.w[i];
+    const uint64_t h = khash<KWM>(k, a.kw);
+    const uint64_t my = ((uint64_t)(id + 1) << 24) | (uint32_t)(h >> 40);
+    uint64_t b = h & a.bmask;
+    for (uint64_t it = 0; it <= a.bmask; ++it) {
+        uint64_t* bk = a.table + b * BUCKET;
+        for (int j = 0; j < BUCKET; ++j)
+            if (atomicCAS((unsigned long long*)(bk + j), 0ull, (unsigned long long)my) == 0ull) return;
+        b = (b + 1) & a.bmask;
+    }
+}
+
+// host restatement of bfs::khash (the kernels' hash): the host tables index by it
+static inline uint64_t host_hash(const uint64_t* k, int kw) {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int i = 0; i < kw; ++i) h = fmix64(h ^ k[i]) + 0x632be59bd9b4e019ull;
+    return fmix64(h);
+}
+
+static inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct Engine {
+    int L = 0, kw = 0, pk = 0, cyc = 0, dev = 0;
+    int64_t max_nodes = 0, cap = 0;
+    int batch_cap = 512;
+    // nodes (ids in discovery order)
+    std::vector<uint64_t> keys;
+    std::vector<int64_t> parent;
+    std::vector<int8_t> action;
+    std::vector<int16_t> total;
+    std::vector<int32_t> depth;
+    std::vector<int32_t> cache_slot;  // -1: no cached children
+    // cached children: per slot 12 keys, hashes, device-known ids, and the round of the probe
+    std::vector<uint64_t> c_keys, c_hash;
+    std::vector<int64_t> c_known;
+    std::vector<int32_t> c_round;
+    std::vector<int32_t> free_slots;
+    // nodes appended in the last W rounds (the in-flight set): open addressing on the hash
+    std::vector<int64_t> recent;  // id + 1, 0 = empty
+    uint64_t rmask = 0;
+    int64_t recent_floor = 0;      // the table holds every id >= recent_floor
+    std::vector<int64_t> n_at_round;  // node count when round r's kernel probed the device table
+    int64_t committed = 0;            // ids < committed are in the device table
+    int round = 0;
+    // result (greedy.py:86-121)
+    int status = 0;  // 0 running, 1 success, 2 failed, 3 move error
+    int budget_hit = 0;
+    int min_length = 0;
+    std::vector<int32_t> trace;
+    std::vector<int64_t> popped;
+    int64_t found_parent = -1, found_explored = 0, last_popped = -1;
+    int found_action = -1, last_action = -1, last_len = -1;
+    uint64_t found_key[ACX_MAX_L / 16 + 2] = {0};
+    int64_t st_rounds = 0, st_expanded = 0, ns_select = 0, ns_gpu = 0, ns_replay = 0, st_known = 0;
+    // device: one staging buffer each way per round (parents + committed keys in; child keys,
+    // hashes and known ids out), so a round is 1 H2D + 2 launches + 1 D2H + 1 sync
+    hipStream_t stream = nullptr;
+    DevArgs d{};
+    uint64_t *d_in = nullptr, *d_out = nullptr;
+    uint64_t *h_in = nullptr, *h_out = nullptr;  // pinned
+    int64_t commit_cap = 0;
+
+    ~Engine() {
+        void* dp[] = {d_in, d_out, d.nkeys, d.table};
+        for (void* p : dp)
+            if (p) (void)hipFree(p);
+        void* hp[] = {h_in, h_out};
+        for (void* p : hp)
+            if (p) (void)hipHostFree(p);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    bool init(int L_, int64_t max_nodes_, int cyc_, int batch) {
+        L = L_;
+        kw = acx_key_words(L);
+        pk = (HDR + 6 * L + 63) / 64;
+        frontier.pk = unexpanded.pk = pk;
+        cyc = cyc_;
+        max_nodes = max_nodes_;
+        cap = max_nodes + 12;
+        batch_cap = batch > 0 ? batch : 512;
+        if (hipGetDevice(&dev) != hipSuccess) return false;
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+        uint64_t ts = 1024;
+        while (ts < 2 * (uint64_t)cap) ts <<= 1;
+        commit_cap = 4 * (int64_t)batch_cap * ACT + 64;
+        const size_t nb = (size_t)batch_cap;
+        const size_t in_words = (nb + (size_t)commit_cap) * kw, out_words = nb * ACT * (kw + 2);
+        bool ok = hipMalloc((void**)&d_in, in_words * 8) == hipSuccess &&
+                  hipMalloc((void**)&d_out, out_words * 8) == hipSuccess &&
+                  hipMalloc((void**)&d.nkeys, (size_t)cap * kw * 8) == hipSuccess &&
+                  hipMalloc((void**)&d.table, ts * 8) == hipSuccess &&
+                  hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocDefault) == hipSuccess &&
+                  hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocDefault) == hipSuccess &&
+                  hipMemsetAsync(d.table, 0, ts * 8, stream) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            return false;
+        }
+        d.bmask = ts / BUCKET - 1;
+        d.L = L;
+        d.kw = kw;
+        d.cyc = cyc;
+        recent.assign(1 << 12, 0);
+        rmask = recent.size() - 1;
+        return true;
+    }
+
+    // ---------------------------------------------------------------- key helpers
+    int len_field(const uint64_t* k, int h) const {
+        const int bit = 4 * L + 8 * h;
+        const uint64_t lo = k[bit >> 6] >> (bit & 63);
+        const uint64_t hi = (bit & 63) > 56 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
+        return (int)((lo | hi) & 0xff);
+    }
+    int key_total(const uint64_t* k) const { return len_field(k, 0) + len_field(k, 1); }
+    bool key_is_error(const uint64_t* k) const { return len_field(k, 0) == 0xff && len_field(k, 1) == 0xff; }
+    uint32_t byte_at(const uint64_t* k, int bit) const {
+        const uint64_t lo = k[bit >> 6] >> (bit & 63);
+        const uint64_t hi = (bit & 63) > 56 ? (k[(bit >> 6) + 1] << (64 - (bit & 63))) : 0ull;
+        return (uint32_t)((lo | hi) & 0xff);
+    }
+
+    // the heap key: total (9 bits) | path length (31) | every letter + 2 in 3 bits, MSB first
+    // (x = 3, x^-1 = 1, y = 4, y^-1 = 0, padding = 2): unsigned word order = Python's tuple
+    // order of (total, path length, state tuple) (greedy.py:55-64,104-113)
+    void prio_key(const uint64_t* k, int tot, int dep, uint64_t* out) const {
+        static uint16_t tbl[256];
+        static bool init = false;
+        if (!init) {
+            static const uint32_t val[4] = {3, 1, 4, 0};
+            for (int b = 0; b < 256; ++b) {
+                uint32_t v = 0;
+                for (int j = 0; j < 4; ++j) v = (v << 3) | val[(b >> (2 * j)) & 3];
+                tbl[b] = (uint16_t)v;
+            }
+            init = true;
+        }
+        for (int i = 0; i < pk; ++i) out[i] = 0;
+        out[0] = ((uint64_t)(tot & 0x1ff) << 55) | ((uint64_t)(dep & 0x7fffffff) << 24);
+        int pos = HDR;
+        auto put = [&](uint64_t v, int nbits) {  // append nbits (<= 61) MSB-first
+            const int w = pos >> 6, o = pos & 63;
+            if (o + nbits <= 64) {
+                out[w] |= v << (64 - o - nbits);
+            } else {
+                out[w] |= v >> (o + nbits - 64);
+                out[w + 1] |= v << (128 - o - nbits);
+            }
+            pos += nbits;
+        };
+        constexpr uint64_t PAD20 = 0x492492492492492ull >> 0;  // 20 x 010 (60 bits): padding letters
+        for (int h = 0; h < 2; ++h) {
+            const int n = len_field(k, h);
+            int i = 0;
+            for (; i + 4 <= n; i += 4) put(tbl[byte_at(k, 2 * (h * L + i))], 12);
+            for (; i < n; ++i) {
+                static const uint32_t val[4] = {3, 1, 4, 0};
+                put(val[byte_at(k, 2 * (h * L + i)) & 3], 3);
+            }
+            for (int m = L - n; m > 0; m -= 20) {
+                const int c = m < 20 ? m : 20;
+                put(PAD20 >> (3 * (20 - c)), 3 * c);
+            }
+        }
+    }
+
+    struct Heap {  // 4-ary min-heap of node ids on their packed keys (pk words, inline)
+        int pk = 0;
+        std::vector<uint64_t> k;
+        std::vector<int64_t> id;
+        bool less(const uint64_t* x, const uint64_t* y) const {
+            if (x[0] != y[0]) return x[0] < y[0];  // total | depth | 24 letter bits: nearly always decides
+            for (int i = 1; i < pk; ++i)
+                if (x[i] != y[i]) return x[i] < y[i];
+            return false;
+        }
+        bool empty() const { return id.empty(); }
+        size_t size() const { return id.size(); }
+        int64_t top() const { return id[0]; }
+        void push(const uint64_t* key, int64_t v) {
+            size_t i = id.size();
+            id.push_back(v);
+            k.resize(k.size() + pk);
+            uint64_t tmp[32];
+            memcpy(tmp, key, 8 * pk);
+            while (i > 0) {
+                const size_t par = (i - 1) / 4;
+                if (!less(tmp, &k[par * pk])) break;
+                memcpy(&k[i * pk], &k[par * pk], 8 * pk);
+                id[i] = id[par];
+                i = par;
+            }
+            memcpy(&k[i * pk], tmp, 8 * pk);
+            id[i] = v;
+        }
+        void pop() {
+            const size_t n = id.size() - 1;
+            if (n == 0) {
+                id.clear();
+                k.clear();
+                return;
+            }
+            uint64_t tmp[32];
+            memcpy(tmp, &k[n * pk], 8 * pk);
+            const int64_t v = id[n];
+            id.pop_back();
+            k.resize(n * pk);
+            size_t i = 0;
+            while (true) {
+                const size_t c0 = 4 * i + 1;
+                if (c0 >= n) break;
+                size_t best = c0;
+                const size_t ce = c0 + 4 < n ? c0 + 4 : n;
+                for (size_t c = c0 + 1; c < ce; ++c)
+                    if (less(&k[c * pk], &k[best * pk])) best = c;
+                if (!less(&k[best * pk], tmp)) break;
+                memcpy(&k[i * pk], &k[best * pk], 8 * pk);
+                id[i] = id[best];
+                i = best;
+            }
+            memcpy(&k[i * pk], tmp, 8 * pk);
+            id[i] = v;
+        }
+        const uint64_t* top_key() const { return k.data(); }
+    };
+    Heap frontier;    // every node not popped yet: the reference's to_explore (pop order)
+    Heap unexpanded;  // the subset without usable cached children (expansion order)
+
+    // ---------------------------------------------------------------- in-flight table
+    void recent_insert(int64_t id, uint64_t h) {
+        uint64_t s = h & rmask;
+        while (recent[s]) s = (s + 1) & rmask;
+        recent[s] = id + 1;
+    }
+    void recent_rebuild(int64_t floor, size_t need) {
+        size_t sz = 1 << 12;
+        while (sz < 2 * need + 16) sz <<= 1;
+        recent.assign(sz, 0);
+        rmask = sz - 1;
+        recent_floor = floor;
+        const int64_t n = (int64_t)parent.size();
+        for (int64_t id = floor; id < n; ++id) recent_insert(id, host_hash(&keys[(size_t)id * kw], kw));
+    }
+    // a node with id >= from equal to key k, or -1
+    int64_t recent_find(const uint64_t* k, uint64_t h, int64_t from) const {
+        for (uint64_t s = h & rmask; recent[s]; s = (s + 1) & rmask) {
+            const int64_t id = recent[s] - 1;
+            if (id >= from && memcmp(&keys[(size_t)id * kw], k, 8 * kw) == 0) return id;
+        }
+        return -1;
+    }
+
+    int64_t add_node(const uint64_t* k, uint64_t h, int64_t par, int act, int tot, int dep) {
+        const int64_t id = (int64_t)parent.size();
+        keys.insert(keys.end(), k, k + kw);
+        parent.push_back(par);
+        action.push_back((int8_t)act);
+        total.push_back((int16_t)tot);
+        depth.push_back(dep);
+        cache_slot.push_back(-1);
+        recent_insert(id, h);
+        if ((int64_t)(id - recent_floor) * 2 + 16 > (int64_t)recent.size()) recent_rebuild(recent_floor, id - recent_floor + 1);
+        uint64_t pkey[32];
+        prio_key(k, tot, dep, pkey);
+        frontier.push(pkey, id);
+        unexpanded.push(pkey, id);
+        return id;
+    }
+
+    bool usable(int64_t id) const {
+        const int32_t s = cache_slot[id];
+        return s >= 0 && (int64_t)parent.size() - n_at_round[c_round[s]] <= AGE;
+    }
+    void drop_cache(int64_t id) {
+        const int32_t s = cache_slot[id];
+        if (s >= 0) {
+            free_slots.push_back(s);
+            cache_slot[id] = -1;
+        }
+    }
+
+    // ---------------------------------------------------------------- one popped node
+    bool visit(int64_t id) {
+        const int32_t s = cache_slot[id];
+        const uint64_t* ck = &c_keys[(size_t)s * ACT * kw];
+        const uint64_t* hs = &c_hash[(size_t)s * ACT];
+        const int64_t* kn = &c_known[(size_t)s * ACT];
+        const int64_t from = n_at_round[c_round[s]];
+        last_popped = id;
+        popped.push_back(id);
+        bool ended = false;
+        for (int a = 0; a < ACT; ++a) {
+            const uint64_t* k = ck + (size_t)a * kw;
+            if (key_is_error(k)) {  // ACMove raised (utils.py:264-266)
+                status = 3;
+                ended = true;
+                break;
+            }
+            const int len = key_total(k);
+            last_action = a;
+            last_len = len;
+            if (len < min_length) {  // greedy.py:86-89
+                min_length = len;
+                trace.push_back(len);
+            }
+            if (len == 2) {  // greedy.py:91-100
+                status = 1;
+                found_parent = id;
+                found_action = a;
+                found_explored = (int64_t)parent.size() - (int64_t)frontier.size();
+                memcpy(found_key, k, 8 * kw);
+                ended = true;
+                break;
+            }
+            // greedy.py:102-113: known to the device as of the probe, or appended since
+            if (kn[a] >= 0) {
+                ++st_known;
+                continue;
+            }
+            if (recent_find(k, hs[a], from) >= 0) continue;
+            add_node(k, hs[a], id, a, len, depth[id] + 1);
+        }
+        drop_cache(id);
+        if (!ended && (int64_t)parent.size() >= max_nodes) {  // greedy.py:115-119
+            status = 2;
+            budget_hit = 1;
+            ended = true;
+        }
+        return ended;
+    }
+
+    // the smallest frontier nodes without usable cached children (greedy expands them next)
+    void select(std::vector<int64_t>& out) {
+        out.clear();
+        while (!unexpanded.empty() && (int)out.size() < batch_cap) {
+            out.push_back(unexpanded.top());
+            unexpanded.pop();
+        }
+    }
+
+    int expand_round(const std::vector<int64_t>& batch);
+
+    int run(const int32_t* pres) {
+        // the root: the (unreduced) input presentation itself (greedy.py:36-68)
+        uint64_t root[ACX_MAX_L / 16 + 2];
+        bfs::pack_key(pres, L, kw, root);
+        int tot0 = 0;
+        for (int i = 0; i < 2 * L; ++i) tot0 += pres[i] != 0;
+        min_length = tot0;
+        keys.assign(root, root + kw);
+        parent.assign(1, -1);
+        action.assign(1, -1);
+        total.assign(1, (int16_t)tot0);
+        depth.assign(1, 0);
+        cache_slot.assign(1, -1);
+        recent_rebuild(0, 1);
+        uint64_t pkey[32];
+        prio_key(root, tot0, 0, pkey);
+        frontier.push(pkey, 0);
+        unexpanded.push(pkey, 0);
+        std::vector<int64_t> batch;
+        while (status == 0) {
+            const int64_t t0 = now_ns();
+            if (frontier.empty()) {  // to_explore ran empty (greedy.py:71)
+                status = 2;
+                break;
+            }
+            // the in-flight table must hold every id >= (nodes - AGE): the probes of usable caches
+            // saw everything below; refloored every AGE appended nodes, so it stays <= 2 AGE
+            const int64_t want_floor = (int64_t)parent.size() - AGE;
+            if (want_floor > recent_floor + AGE) recent_rebuild(want_floor, (size_t)AGE);
+            select(batch);
+            const int64_t t1 = now_ns();
+            ns_select += t1 - t0;
+            const int e = expand_round(batch);
+            if (e != ACX_OK) return e;
+            const int64_t t2 = now_ns();
+            ns_gpu += t2 - t1;
+            ++round;
+            // replay: pop while the top has usable cached children (greedy.py:71-119)
+            while (status == 0) {
+                if (frontier.empty()) {
+                    status = 2;
+                    break;
+                }
+                const int64_t id = frontier.top();
+                if (!usable(id)) {
+                    if (cache_slot[id] >= 0) {  // expanded before the last AGE appends: expand again
+                        drop_cache(id);
+                        unexpanded.push(frontier.top_key(), id);
+                    }
+                    break;
+                }
+                frontier.pop();
+                visit(id);
+            }
+            ns_replay += now_ns() - t2;
+        }
+        return ACX_OK;
+    }
+};
+
+struct ExpandLaunch {
+    Engine* E;
+    template <int NW>
+    void go() {
+        const int n = E->d.n * ACT;
+        greedy_expand_kernel<NW><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream>>>(E->d);
+    }
+};
+struct CommitLaunch {
+    Engine* E;
+    template <int NW>
+    void go() {
+        const int64_t n = E->d.hi - E->d.lo;
+        greedy_commit_kernel<NW + 1><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream>>>(E->d);
+    }
+};
+
+int Engine::expand_round(const std::vector<int64_t>& batch) {
+    const int n = (int)batch.size();
+    const int64_t n_nodes = (int64_t)parent.size();
+    // staging in: the batch's parent keys, then the keys of the nodes appended since the last
+    // round (committed to the device visited set before the expansion probes it)
+    for (int i = 0; i < n; ++i) memcpy(h_in + (size_t)i * kw, &keys[(size_t)batch[i] * kw], 8 * kw);
+    int64_t lo = committed;
+    while (true) {
+        const int64_t hi = std::min(n_nodes, lo + commit_cap);
+        uint64_t* cst = h_in + (size_t)n * kw;
+        if (hi > lo) memcpy(cst, &keys[(size_t)lo * kw], (size_t)(hi - lo) * kw * 8);
+        const size_t words = (size_t)(n + (hi - lo)) * kw;
+        if (hipMemcpyAsync(d_in, h_in, words * 8, hipMemcpyHostToDevice, stream) != hipSuccess) return ACX_E_LAUNCH;
+        if (hi > lo) {
+            d.commit = d_in + (size_t)n * kw;
+            d.lo = lo;
+            d.hi = hi;
+            CommitLaunch cl{this};
+            bfs::by_nw(L, cl);
+        }
+        lo = hi;
+        if (lo >= n_nodes) break;
+        if (hipStreamSynchronize(stream) != hipSuccess) return ACX_E_LAUNCH;  // h_in is reused
+    }
+    committed = n_nodes;
+    n_at_round.push_back(n_nodes);
+    if (n == 0) return hipStreamSynchronize(stream) == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+    d.n = n;
+    d.parents = d_in;
+    d.ckeys = d_out;
+    d.chash = d_out + (size_t)n * ACT * kw;
+    d.cknown = reinterpret_cast<int64_t*>(d.chash + (size_t)n * ACT);
+    ExpandLaunch el{this};
+    bfs::by_nw(L, el);
+    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMemcpyAsync(h_out, d_out, (size_t)n * ACT * (kw + 2) * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return ACX_E_LAUNCH;
+    const uint64_t* ck = h_out;
+    const uint64_t* ch = h_out + (size_t)n * ACT * kw;
+    const int64_t* kn = reinterpret_cast<const int64_t*>(ch + (size_t)n * ACT);
+    for (int i = 0; i < n; ++i) {
+        int32_t s;
+        if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+        } else {
+            s = (int32_t)c_round.size();
+            c_round.push_back(0);
+            c_keys.resize(c_keys.size() + (size_t)ACT * kw);
+            c_hash.resize(c_hash.size() + ACT);
+            c_known.resize(c_known.size() + ACT);
+        }
+        memcpy(&c_keys[(size_t)s * ACT * kw], ck + (size_t)i * ACT * kw, (size_t)ACT * kw * 8);
+        memcpy(&c_hash[(size_t)s * ACT], ch + (size_t)i * ACT, ACT * 8);
+        memcpy(&c_known[(size_t)s * ACT], kn + (size_t)i * ACT, ACT * 8);
+        c_round[s] = round;
+        cache_slot[batch[i]] = s;
+    }
+    ++st_rounds;
+    st_expanded += n;
+    return ACX_OK;
+}
+
+}  // namespace greedy
+}  // namespace acx
+
+using namespace acx::greedy;
+
+extern "C" {
+
+int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, int32_t cyclical, int32_t batch,
+                   void** out_handle) {
+    if (!presentation || !out_handle || L < 1 || L > ACX_MAX_L || max_nodes < 1 || max_nodes > (1ll << 31))
+        return ACX_E_ARG;
+    *out_handle = nullptr;
+    Engine* E = new (std::nothrow) Engine();
+    if (!E) return ACX_E_LAUNCH;
+    if (!E->init(L, max_nodes, cyclical != 0, batch)) {
+        delete E;
+        return ACX_E_LAUNCH;
+    }
+    const int st = E->run(presentation);
+    *out_handle = E;
+    return st;
+}
+
+void acx_greedy_destroy(void* h) { delete static_cast<Engine*>(h); }
+
+// 0 running, 1 success, 2 failed, 3 move error; budget_hit, min_length, nodes (len(tree_nodes))
+int32_t acx_greedy_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {
+    Engine* E = static_cast<Engine*>(h);
+    if (budget_hit) *budget_hit = E->budget_hit;
+    if (min_length) *min_length = E->min_length;
+    if (n_nodes) *n_nodes = (int64_t)E->parent.size();
+    return E->status;
+}
+
+// the returned path: success -> the found child's; otherwise the last popped node's plus its
+// last child (greedy.py:100,121).  Returns the number of (action, total) entries.
+int64_t acx_greedy_path(void* h, int32_t* actions, int32_t* totals, int64_t cap) {
+    Engine* E = static_cast<Engine*>(h);
+    const int64_t v0 = E->status == 1 ? E->found_parent : E->last_popped;
+    if (v0 < 0) return 0;
+    std::vector<int64_t> chain;
+    for (int64_t v = v0; v >= 0; v = E->parent[v]) chain.push_back(v);
+    int64_t n = 0;
+    for (auto it = chain.rbegin(); it != chain.rend(); ++it, ++n)
+        if (n < cap) {
+            actions[n] = E->action[*it];
+            totals[n] = E->total[*it];
+        }
+    if (n < cap) {
+        actions[n] = E->status == 1 ? E->found_action : E->last_action;
+        totals[n] = E->status == 1 ? 2 : E->last_len;
+    }
+    return n + 1;
+}
+
+// out[0] rounds, [1] parents expanded, [2] parents popped, [3] children the device knew,
+// [4..6] host ns selecting / in the GPU round trip / replaying
+void acx_greedy_stats(void* h, int64_t* out) {
+    Engine* E = static_cast<Engine*>(h);
+    out[0] = E->st_rounds;
+    out[1] = E->st_expanded;
+    out[2] = (int64_t)E->popped.size();
+    out[3] = E->st_known;
+    out[4] = E->ns_select;
+    out[5] = E->ns_gpu;
+    out[6] = E->ns_replay;
+}
+
+int64_t acx_greedy_min_trace(void* h, int32_t* out, int64_t cap) {
+    Engine* E = static_cast<Engine*>(h);
+    const int64_t n = (int64_t)E->trace.size();
+    for (int64_t i = 0; out && i < n && i < cap; ++i) out[i] = E->trace[(size_t)i];
+    return n;
+}
+
+int64_t acx_greedy_popped(void* h, int64_t* ids, int64_t cap) {
+    Engine* E = static_cast<Engine*>(h);
+    const int64_t n = (int64_t)E->popped.size();
+    for (int64_t i = 0; ids && i < n && i < cap; ++i) ids[i] = E->popped[(size_t)i];
+    return n;
+}
+
+int64_t acx_greedy_node_keys(void* h, uint64_t* out, int64_t cap) {
+    Engine* E = static_cast<Engine*>(h);
+    const int64_t n = (int64_t)E->parent.size();
+    if (out) memcpy(out, E->keys.data(), (size_t)(n < cap ? n : cap) * E->kw * 8);
+    return n;
+}
+
+int32_t acx_greedy_found(void* h, int32_t* first_letters, int64_t* explored) {
+    Engine* E = static_cast<Engine*>(h);
+    if (E->status != 1) return 0;
+    static const int32_t letter[4] = {1, -1, 2, -2};
+    const int bit1 = 2 * E->L;
+    if (first_letters) {
+        first_letters[0] = letter[E->found_key[0] & 3u];
+        first_letters[1] = letter[(E->found_key[bit1 >> 6] >> (bit1 & 63)) & 3u];
+    }
+    if (explored) *explored = E->found_explored;
+    return 1;
+}
+
+}  // extern "C"

@@ -650,10 +650,19 @@ struct GenericTile {
     __device__ __forceinline__ void flag_rows(int lane, bool f) {
         if (f) flags[lane] = 1;
     }
-    // (the generic-L instantiations serve parity, not speed: reload the whole tile)
-    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
-        (void)rows;
-        load(g, R, lane);
+    // the rows of the lanes in `rows` only, row by row (the generic-L instantiations serve
+    // parity, not speed)
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+        if ((rows >> lane) & 1ull) flags[lane] = 0;
+        wave_sync();
+        for (uint64_t m = rows; m; m &= m - 1) {
+            const int r = __builtin_ctzll(m);
+            bool bad = false;
+            for (int k = lane; k < twoL; k += WAVE)
+                row(r)[k] = (int8_t)to_i8(g[(int64_t)r * twoL + k], bad);
+            if (__any(bad) && lane == 0) flags[r] = 1;
+        }
+        wave_sync();
     }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(base + r * rowb); }
 
@@ -1510,6 +1519,10 @@ static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; 
 template <class F>
 static int dispatch(int L, F&& f) {
     const bool v4 = (2 * L) % 4 == 0;
+#ifdef ACX_ISA_L128_ONLY  // faster builds for ISA inspection only
+    (void)v4;
+    return L == 128 ? f.template go<8, 128, 4>() : ACX_E_ARG;
+#endif
     if (L == 36) return f.template go<3, 36, 4>();
 #ifdef ACX_ISA_L36_ONLY  // faster builds for ISA inspection only
     (void)v4;

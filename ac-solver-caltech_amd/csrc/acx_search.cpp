@@ -13,6 +13,7 @@
 //     speculatively in one launch; children are cached until their parent is popped.
 // Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
 // acx_key_words(L) uint64 words.
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -139,6 +140,11 @@ struct Engine {
     uint64_t found_key[ACX_MAX_L / 16 + 2] = {0};
     // statistics: rounds (next_batch calls that returned parents), parents expanded, pops
     int64_t st_rounds = 0, st_expanded = 0, st_pops = 0;
+    int64_t ns_next = 0, ns_store = 0, ns_visit = 0;  // host time in next_batch / caching children / replay
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
 
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
         table.assign(1 << 12, 0);
@@ -264,6 +270,12 @@ struct Engine {
     }
 
     int64_t next_batch(uint64_t* out, int64_t cap) {
+        const int64_t t0 = now_ns();
+        const int64_t n = next_batch_(out, cap);
+        ns_next += now_ns() - t0;
+        return n;
+    }
+    int64_t next_batch_(uint64_t* out, int64_t cap) {
         batch.clear();
         if (status != 0) return 0;
         if (mode == 0) {
@@ -354,9 +366,17 @@ struct Engine {
     }
 
     int feed(const uint64_t* child_keys, int64_t count) {
+        const int64_t t0 = now_ns();
         for (int64_t i = 0; i < count && i < (int64_t)batch.size(); ++i)
             store_children(batch[i], child_keys + (size_t)i * ACT * kw);
         batch.clear();
+        const int64_t t1 = now_ns();
+        ns_store += t1 - t0;
+        const int st = replay();
+        ns_visit += now_ns() - t1;
+        return st;
+    }
+    int replay() {
         // advance as far as the cache allows
         while (status == 0) {
             if (mode == 0) {
@@ -440,12 +460,16 @@ int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap)
     return e->path(e->last_popped, actions, totals, cap, true);
 }
 
-// statistics: out[0] = rounds, out[1] = parents expanded on the GPU, out[2] = parents popped
+// statistics: out[0] = rounds, out[1] = parents expanded on the GPU, out[2] = parents popped,
+// out[3..5] = host nanoseconds in next_batch / caching fed children / the replay
 void acx_search_stats(void* h, int64_t* out) {
     Engine* e = static_cast<Engine*>(h);
     out[0] = e->st_rounds;
     out[1] = e->st_expanded;
     out[2] = e->st_pops;
+    out[3] = e->ns_next;
+    out[4] = e->ns_store;
+    out[5] = e->ns_visit;
 }
 
 // ids of the expanded (popped) nodes in the reference's expansion order; returns the count

@@ -318,7 +318,8 @@ int acx_token_ids(const int32_t* states, const uint64_t* keys, int64_t* out, int
  *   acx_search_status      0 running, 1 success, 2 failed, 3 a child move raised (its key
  *                          is the acx_expand12 error sentinel): the reference's AssertionError
  *   acx_search_path        the result path (see acx_search.cpp); returns its length
- *   acx_search_stats       out[0] rounds, out[1] parents expanded, out[2] parents popped
+ *   acx_search_stats       out[0] rounds, out[1] parents expanded, out[2] parents popped,
+ *                          out[3..5] host ns in next_batch / caching children / the replay
  *   acx_search_node_keys   the packed keys of the discovered nodes in discovery order
  *   acx_search_min_trace   the new minimum totals in the order found (the verbose "New minimal
  *                          length found" lines, greedy.py:86-89, breadth_first.py:79-82)
@@ -337,6 +338,30 @@ int64_t acx_search_node_keys(void* h, uint64_t* out, int64_t cap);
 int64_t acx_search_min_trace(void* h, int32_t* out, int64_t cap);
 int64_t acx_search_popped(void* h, int64_t* ids, int64_t cap);
 int32_t acx_search_found(void* h, int32_t* first_letters, int64_t* explored);
+
+/*
+ * greedy_search (greedy.py:15-121) with the visited set on the device (csrc/acx_greedy.hip): the
+ * expansion rounds are driven from C++ on the current device -- each round expands the smallest
+ * frontier nodes not yet expanded (lane per (parent, action)) and probes every child against the
+ * HBM hash table of the committed nodes; the host replays the reference's pop / dedup / budget
+ * order exactly, checking only the children the device did not know against the nodes appended
+ * since (the in-flight conflicts).  batch = parents per round (<= 0: 512).
+ *   acx_greedy_run       searches from `presentation` (HOST pointer, 2L int32, letters +-1/+-2);
+ *                        *out_handle receives the finished search (query it, then destroy)
+ *   acx_greedy_status / _path / _min_trace / _popped / _node_keys / _found   as acx_search_*
+ *   acx_greedy_stats     out[0] rounds, [1] parents expanded, [2] popped, [3] children the device
+ *                        knew, [4..6] host ns selecting / GPU round trips / replaying
+ */
+int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, int32_t cyclical, int32_t batch,
+                   void** out_handle);
+void acx_greedy_destroy(void* h);
+int32_t acx_greedy_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes);
+int64_t acx_greedy_path(void* h, int32_t* actions, int32_t* totals, int64_t cap);
+void acx_greedy_stats(void* h, int64_t* out);
+int64_t acx_greedy_min_trace(void* h, int32_t* out, int64_t cap);
+int64_t acx_greedy_popped(void* h, int64_t* ids, int64_t cap);
+int64_t acx_greedy_node_keys(void* h, uint64_t* out, int64_t cap);
+int32_t acx_greedy_found(void* h, int32_t* first_letters, int64_t* explored);
 
 /* number of uint64 words in one packed key: ceil((4L + 16) / 64) */
 int32_t acx_key_words(int32_t L);

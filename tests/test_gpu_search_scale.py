@@ -84,11 +84,14 @@ def test_sharded_bfs_one_rank_matches_reference_at_scale(c, capsys):
     SB.release_workspaces()
 
 
+@pytest.mark.parametrize("engine", ["device", "host"])
 @pytest.mark.parametrize("c", GREEDY_CASES, ids=_id)
-def test_greedy_matches_reference_at_scale(c, capsys):
+def test_greedy_matches_reference_at_scale(c, engine, capsys):
+    """engine "device": csrc/acx_greedy.hip (visited set in HBM, C++-driven rounds); "host":
+    csrc/acx_search.cpp over acx_expand12 launches."""
     from acx.search import _engine as E
     ok, path = E.run_search(E.GREEDY, np.array(c["presentation"]), c["budget"], True, c["cyclical"], device=DEV,
-                            keep_node_keys=True)
+                            keep_node_keys=True, engine=engine)
     out = capsys.readouterr().out.splitlines()
     assert out == c["stdout"]
     assert [bool(ok), [list(x) for x in path]] == [c["ok"], c["path"]]
@@ -110,7 +113,8 @@ def test_reference_random_searches_through_gpu_paths():
     for c in cases:
         pres = np.array(c["presentation"])
         fns = ([lambda **k: acx.bfs(engine="device", **k), lambda **k: acx.bfs(engine="host", **k)]
-               if c["search_fn"] == "bfs" else [acx.greedy_search])
+               if c["search_fn"] == "bfs" else
+               [lambda **k: acx.greedy_search(engine="device", **k), lambda **k: acx.greedy_search(engine="host", **k)])
         for fn in fns:
             buf = io.StringIO()
             kw = dict(presentation=pres, max_nodes_to_explore=c["budget"], cyclically_reduce_after_moves=c["cyclical"])
@@ -123,3 +127,22 @@ def test_reference_random_searches_through_gpu_paths():
             assert _result(ok, path) == [c["ok"], c["path"]], c
             m = re.search(r"number of explored nodes = (\d+)", buf.getvalue())
             assert (int(m.group(1)) if m else None) == c["budget_nodes"], c
+
+
+@pytest.mark.parametrize("batch", [1, 7, 64, 1024])
+def test_greedy_device_engine_batch_sizes(batch):
+    """The round size only changes how far the speculation runs ahead, never the result: AK(3)
+    and a Miller-Schupp start at several batch sizes equal the reference's pop order."""
+    from acx.search import _engine as E
+    for c in [GREEDY_CASES[0], GREEDY_CASES[1]]:
+        budget = min(c["budget"], 20000)
+        ok, path = E.run_search(E.GREEDY, np.array(c["presentation"]), budget, False, c["cyclical"], device=DEV,
+                                keep_node_keys=True, batch=batch)
+        st = E.LAST_STATS
+        states = unpack_keys_np(st["node_keys"][st["popped"]], c["L"])
+        ref = next(r for r in SCALE if r["search_fn"] == "greedy_search" and r["presentation"] == c["presentation"]
+                   and r["cyclical"] == c["cyclical"])
+        want = {k: v for k, v in ref["checkpoints"].items() if int(k) <= len(states)}
+        assert len(want) >= 3
+        _, cps = state_digest(states, want.keys())
+        assert cps == want, batch

@@ -171,6 +171,40 @@ extern "C" int sp_chunk(void* p, int64_t n16, int per, void* stream) {
     chunk_fill<<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>((int4*)p, n16, per);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+// streaming copy, one 16-byte vector per thread per iteration (grid-stride): the read+write
+// ceiling the per-call step API (state in, state out) is measured against
+__global__ __launch_bounds__(256) void copy16(const int4* __restrict__ src, int4* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+// the step kernel's shape: each wave reads its whole tile (64 rows of row_chunks 16-byte chunks,
+// coalesced) into registers 8 chunks at a time, then writes it out
+__global__ __launch_bounds__(256) void tile_copy(const int4* __restrict__ src, int4* __restrict__ dst, int64_t B,
+                                                 int row_chunks) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile * 64 >= B) return;
+    const int64_t base = tile * 64 * row_chunks + lane;
+    const int n = 64 * row_chunks / 64;  // chunks per lane
+    for (int u0 = 0; u0 < n; u0 += 8) {
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (u0 + u < n) v[u] = src[base + (int64_t)(u0 + u) * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (u0 + u < n) dst[base + (int64_t)(u0 + u) * 64] = v[u];
+    }
+}
+extern "C" int sp_copy(const void* src, void* dst, int64_t n16, int mode, int64_t B, int row_chunks, void* stream) {
+    if (mode == 0) {
+        copy16<<<8192, 256, 0, (hipStream_t)stream>>>((const int4*)src, (int4*)dst, n16);
+    } else {
+        if (B % 64 != 0 || B * row_chunks != n16) return -1;
+        tile_copy<<<(unsigned)((B / 64 + 3) / 4), 256, 0, (hipStream_t)stream>>>((const int4*)src, (int4*)dst, B,
+                                                                                   row_chunks);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 extern "C" int sp_linear(void* p, int64_t n16, int blocks, void* stream) {
     linear_fill<<<blocks, 256, 0, (hipStream_t)stream>>>((int4*)p, n16);
     return hipGetLastError() == hipSuccess ? 0 : -2;
