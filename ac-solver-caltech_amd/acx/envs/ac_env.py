@@ -194,10 +194,21 @@ class VecACEnv:
     move ids and returns device tensors (obs, reward, done, truncated, info) where obs is
     the post-autoreset state and info["final_observation"] holds, for rows with
     done | truncated, the state before the reset.
+
+    record_actions=True keeps each env's episode moves on the device (acx_step_record) and
+    fills the info dict the PPO trainer reads for solved episodes (training.py:273-280), as
+    gymnasium's SyncVectorEnv builds it from ACEnv's per-env info (ac_env.py:105-110):
+      info_format "final_info" (gymnasium < 1.0, same-step autoreset): info["final_info"] is an
+        object array with {"actions": [...]} for done envs, {} for truncated ones, None else,
+        info["_final_info"] / info["_final_observation"] the finished mask;
+      info_format "actions" (the gymnasium >= 1.0 key layout): info["actions"][i] = the move list
+        of env i's solved episode, info["_actions"] its mask.
+    Building it synchronises with the device once per step (the trainer reads it on the host).
     """
 
     def __init__(self, initial_states, horizon_length: int = 1000, device=None, cyclical: bool = True,
-                 track_final_obs: bool = True, check_errors: bool = False):
+                 track_final_obs: bool = True, check_errors: bool = False, record_actions: bool = False,
+                 info_format: str = "final_info"):
         self.device = torch.device(device if device is not None else "cuda")
         init = torch.as_tensor(np.asarray(initial_states) if not torch.is_tensor(initial_states) else initial_states)
         if init.dim() != 2 or init.shape[1] % 2:
@@ -224,6 +235,14 @@ class VecACEnv:
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.final_obs = torch.zeros_like(self.state) if track_final_obs else None
+        if info_format not in ("final_info", "actions"):
+            raise ValueError("info_format must be 'final_info' or 'actions'")
+        self.record_actions = bool(record_actions)
+        self.info_format = info_format
+        if self.record_actions:
+            # move k of env i's current episode at [k, i]; an episode never outlives the horizon
+            self.action_hist = torch.zeros((max(1, self.horizon_length), B), dtype=torch.uint8, device=dev)
+            self.episode_len = torch.zeros(B, dtype=torch.int32, device=dev)
         self.action_space = Discrete(12)
         self.single_observation_space = Box(np.full(2 * L, -2, np.int8), np.full(2 * L, 2, np.int8))
 
@@ -265,14 +284,49 @@ class VecACEnv:
                 or actions.shape != (self.num_envs,)):
             actions = actions.to(self.device, torch.int32).contiguous().reshape(self.num_envs)
         s_in, s_out, rs, cnt, rew, dn, tr, ln, fo, err, ec = self._step_args()
-        st = self._lib.acx_step(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
-                                self.num_envs, self.max_relator_length, self.horizon_length, int(self.cyclical),
-                                torch.cuda.current_stream(self.device).cuda_stream)
-        _lib.check(st, "acx_step")
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        if self.record_actions:
+            st = self._lib.acx_step_record(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo,
+                                           self.action_hist.data_ptr(), self.action_hist.shape[0],
+                                           self.episode_len.data_ptr(), err, ec, self.num_envs,
+                                           self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
+            _lib.check(st, "acx_step_record")
+        else:
+            st = self._lib.acx_step(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
+                                    self.num_envs, self.max_relator_length, self.horizon_length, int(self.cyclical),
+                                    stream)
+            _lib.check(st, "acx_step")
         if self.check_errors:
             self.raise_if_errors()
         info = {"final_observation": self.final_obs} if self.final_obs is not None else {}
+        if self.record_actions:
+            info.update(self._episode_info())
         return self.state, self.reward, self.done, self.truncated, info
+
+    def _episode_info(self) -> dict:
+        """SyncVectorEnv's info entries for the envs whose episode ended this step (one D2H copy
+        of the masks, then one column of the move history per solved env)."""
+        B = self.num_envs
+        flags = torch.stack([self.done, self.truncated]).cpu().numpy().astype(bool)
+        done, fin = flags[0], flags[0] | flags[1]
+        if not fin.any():  # SyncVectorEnv adds the keys only when some env finished
+            return {}
+        solved = np.flatnonzero(done)
+        lists = {}
+        if solved.size:
+            idx = torch.as_tensor(solved, device=self.device)
+            lens = self.episode_len[idx].cpu().numpy()
+            cols = self.action_hist[: int(lens.max()), idx].cpu().numpy()  # (max_len, n_solved)
+            lists = {int(i): [int(a) for a in cols[: lens[k], k]] for k, i in enumerate(solved)}
+        if self.info_format == "final_info":
+            final_info = np.full(B, None, dtype=object)
+            for i in np.flatnonzero(fin):
+                final_info[i] = {"actions": lists[int(i)]} if done[i] else {}
+            return {"final_info": final_info, "_final_info": fin, "_final_observation": fin}
+        acts = np.full(B, None, dtype=object)
+        for i, v in lists.items():
+            acts[i] = v
+        return {"actions": acts, "_actions": done}
 
     def rollout(self, actions: torch.Tensor, obs_traj: Optional[torch.Tensor] = None, reward_traj=None,
                 done_traj=None, trunc_traj=None):

@@ -1648,6 +1648,22 @@ int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* actio
     return dispatch(L, f);
 }
 
+int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
+                    int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
+                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                    int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state_in || !state_out || !action || !step_count || !action_hist || hist_cap == 0) return ACX_E_ARG;
+    if (!aligned16(state_in) || !aligned16(state_out)) return ACX_E_ARG;
+    // the learner instantiation (it compiles the history writes) with the plain step's outputs
+    StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated, lengths_out, final_obs,
+               err, err_count, nullptr, nullptr, nullptr, nullptr, action_hist, episode_len, B, L, horizon, cyclical,
+               hist_cap};
+    StepLaunch f{a, (hipStream_t)stream, true};
+    return dispatch(L, f);
+}
+
 // acx_curriculum.hip (not in the public header)
 int acx_internal_curriculum_fused(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
                                   int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,

@@ -452,20 +452,31 @@ def main():
     # used only when that profile's workload matches this run's
     # (the newest committed profile of this workload at this K; profile_cmd.sh profiles the
     # driver's own command, bench.py --steps 20 --warmup 5, and the K = 200 default)
+    # A profile of the same (B, L, K) gives the launch's measured bytes directly; one of another K
+    # is carried over as its measured/algorithmic ratio (the launch's bytes are the same per-step
+    # and per-launch terms at any K, so the ratio is K-independent) and labelled as scaled.
     traffic, traffic_src = None, None
+    cands = []
     for tag in ("r02_k20", "r02", "r01"):
         prof = os.path.join(REPO, "profiles", tag.split("_")[0], f"{tag}_summary.json")
-        if traffic is not None or not os.path.exists(prof):
+        if not os.path.exists(prof):
             continue
         with open(prof) as f:
             ps = json.load(f)
         pc = ps.get("bench_line", {}).get("config", {})
         td = ps.get("rollout_timed_dispatch") or {}
-        if (pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and ps["bench_line"].get("steps") == K
-                and td.get("pmc_hbm_bytes")):
-            traffic = td["pmc_hbm_bytes"]
-            traffic_src = (f"profiles/{tag.split('_')[0]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + "
-                           f"--pmc WRITE_SIZE of this command (K={K})")
+        if pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and td.get("pmc_hbm_bytes"):
+            cands.append((ps["bench_line"].get("steps") != K, tag, ps["bench_line"].get("steps"), td))
+    if cands:
+        scaled, tag, kp, td = min(cands, key=lambda c: c[0])
+        where = f"profiles/{tag.split('_')[0]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE"
+        if not scaled:
+            traffic, traffic_src = td["pmc_hbm_bytes"], f"{where} of this command (K={K})"
+        else:
+            ratio = td["pmc_hbm_bytes"] / td["algorithmic_bytes"]
+            traffic = launch_bytes * ratio
+            traffic_src = (f"{where} at K={kp}: measured/algorithmic = {ratio:.4f}, applied to this launch's "
+                           "algorithmic bytes")
 
     value = world * B * K / elapsed
     line = {

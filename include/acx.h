@@ -110,6 +110,19 @@ int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* actio
                      int32_t cyclical, void* stream);
 
 /*
+ * acx_step plus the episode move history gymnasium's SyncVectorEnv hands the trainer
+ * (ac_env.py:92,105-110 -> infos["final_info"][i]["actions"] / infos["actions"][i],
+ * training.py:273-280): action_hist (hist_cap, B) uint8, move k of env i's current episode at
+ * [k, i]; episode_len (B) int32 or NULL = the length of the episode that ended this step
+ * (done | truncated), else 0.  step_count and action_hist are required; other arguments as
+ * acx_step.
+ */
+int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
+                    int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
+                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                    int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+
+/*
  * Start-state curriculum of the PPO trainer, round 1 (training.py:319-352): every env whose
  * episode ended this step (done | truncated), in env order, starts next from
  * curriculum_states[k], k = *next_index, *next_index + 1, ... (max(states_processed) + 1);

@@ -229,6 +229,44 @@ def test_vec_env_episodes_fixture():
     assert int(env.err_count.item()) == 0
 
 
+@pytest.mark.parametrize("fmt", ["final_info", "actions"])
+def test_vec_env_info_actions_contract(fmt):
+    """record_actions: the info dict training.py:273-280 reads for solved episodes.  Expected move
+    lists follow ACEnv's own bookkeeping over the reference's episodes (env_episodes.npz):
+    `self.actions += [action]` per step, cleared by reset (ac_env.py:92,105-110,124)."""
+    from acx import VecACEnv
+    d = _load("env_episodes.npz")
+    T, B = d["actions"].shape
+    env = VecACEnv(d["initial"].astype(np.int32), horizon_length=int(d["horizon"]), device=DEV,
+                   record_actions=True, info_format=fmt)
+    hist = [[] for _ in range(B)]
+    n_solved = 0
+    for t in range(T):
+        obs, rew, done, trunc, info = env.step(torch.as_tensor(d["actions"][t].astype(np.int32)).to(DEV))
+        assert np.array_equal(obs.cpu().numpy(), d["obs"][t].astype(np.int32)), t
+        dn, tr = d["done"][t].astype(bool), d["truncated"][t].astype(bool)
+        for i in range(B):
+            hist[i].append(int(d["actions"][t][i]))
+        if not (dn | tr).any():
+            assert info.keys() <= {"final_observation"}, t
+        for i in range(B):
+            if fmt == "final_info":
+                if dn[i] or tr[i]:
+                    assert info["_final_info"][i] and info["_final_observation"][i]
+                    # training.py:276-277
+                    assert info["final_info"][i] == ({"actions": hist[i]} if dn[i] else {}), (t, i)
+                elif "final_info" in info:
+                    assert not info["_final_info"][i] and info["final_info"][i] is None
+            elif dn[i]:
+                assert info["_actions"][i] and list(info["actions"][i]) == hist[i], (t, i)  # training.py:280
+            elif "actions" in info:
+                assert not info["_actions"][i]
+            if dn[i] or tr[i]:
+                n_solved += int(dn[i])
+                hist[i] = []
+    assert n_solved > 0
+
+
 def test_rollout_equals_repeated_step_and_fixture():
     from acx import VecACEnv
     d = _load("env_episodes.npz")
@@ -265,11 +303,11 @@ def _ms_starts(L, B):
 
 @pytest.mark.parametrize("L", [36, 128])
 def test_full_size_rollout_properties_and_sampled_parity(L):
-    """Full batch (2^20 envs at L=36, 2^17 at L=128): size-independent invariants on every env
-    (valid, freely + cyclically reduced, lengths = letter counts) and bit-exact oracle replay
-    of a sample of envs."""
+    """Full per-GPU batch (2^20 envs: config 3 at L=36, config 5's shard at L=128):
+    size-independent invariants on every env (valid, freely + cyclically reduced, lengths =
+    letter counts) and bit-exact oracle replay of a sample of envs."""
     from acx import VecACEnv
-    B = (1 << 20) if L == 36 else (1 << 17)
+    B = 1 << 20
     T, H = 24, 10
     init = _ms_starts(L, B)
     env = VecACEnv(init, horizon_length=H, device=DEV, track_final_obs=False)
