@@ -75,7 +75,7 @@ def run_greedy_device(p, max_nodes_to_explore, verbose, cyclical, device=None, b
     try:
         if st != _lib.OK:
             _lib.check(st, "acx_greedy_run")
-        stats = np.zeros(7, np.int64)
+        stats = np.zeros(13, np.int64)
         lib.acx_greedy_stats(h, stats.ctypes.data)
         budget = ctypes.c_int32(0)
         min_len = ctypes.c_int32(0)
@@ -84,7 +84,9 @@ def run_greedy_device(p, max_nodes_to_explore, verbose, cyclical, device=None, b
         LAST_STATS.clear()
         LAST_STATS.update(rounds=int(stats[0]), expanded=int(stats[1]), pops=int(stats[2]),
                           device_known_children=int(stats[3]), host_select_s=stats[4] / 1e9,
-                          gpu_roundtrip_s=stats[5] / 1e9, host_replay_s=stats[6] / 1e9, nodes=int(n_nodes.value),
+                          gpu_roundtrip_s=stats[5] / 1e9, host_replay_s=stats[6] / 1e9, stop_new=int(stats[7]),
+                          stop_old=int(stats[8]), stop_aged=int(stats[9]), gpu_wait_s=stats[10] / 1e9,
+                          host_cache_s=stats[11] / 1e9, retired_caches=int(stats[12]), nodes=int(n_nodes.value),
                           status=int(status), min_length=int(min_len.value), engine="device-visited-set")
         ntr = lib.acx_greedy_min_trace(h, None, 0)
         trace = np.zeros(max(ntr, 1), np.int32)

@@ -14,9 +14,9 @@
 //     round.
 // The host replays the reference's order exactly: pops while the frontier's top has cached
 // children; a child the device did not know is checked only against the nodes appended since
-// its round (the in-flight conflicts), kept in a host table of the last 2^20..2^21 appended
-// nodes; children cached before the last 2^20 appends are dropped and their parent re-expanded
-// when it comes up again, which bounds that table.
+// its round (the in-flight conflicts), kept in a host table of the last 2^16..2^17 appended
+// nodes (two generations of tagged entries); children cached before the last 2^16 appends are
+// retired and their parent re-expanded with a later batch, which bounds that table.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -44,8 +44,16 @@ constexpr int ACT = 12;
 constexpr int BUCKET = 8;
 constexpr uint32_t FP_MASK = 0xffffffu;
 constexpr int HDR = 40;  // priority-key header bits: total (9) | path length (31)
-constexpr int64_t AGE = 1 << 20;  // a cached expansion stays usable while fewer nodes than this have been
-                                  // appended since its probe (bounds the in-flight table)
+constexpr int64_t AGE = 1 << 16;  // a cached expansion stays usable while fewer nodes than this have been
+                                  // appended since its probe (bounds the in-flight table: two
+                                  // generations of AGE nodes, 2 x 1 MB of tagged entries, cache-
+                                  // resident).  Aged caches are retired at round starts, so their
+                                  // nodes are re-expanded with the next batches instead of costing
+                                  // a round each at the top of the frontier (r02u: ~40k rounds)
+static int64_t g_age_override = 0;  // tests only (acx_internal_greedy_age): a smaller AGE
+constexpr int DEFAULT_BATCH = 64;  // parents per round (tools/greedy_sweep.py: 64-128 best on AK(3) /
+                                   // Miller-Schupp at 10^6 nodes; larger rounds mostly expand nodes
+                                   // that are never popped)
 
 struct DevArgs {
     const uint64_t* parents;  // (n, kw) keys of the round's parents
@@ -150,7 +158,8 @@ static inline int64_t now_ns() {
 struct Engine {
     int L = 0, kw = 0, pk = 0, cyc = 0, dev = 0;
     int64_t max_nodes = 0, cap = 0;
-    int batch_cap = 512;
+    int batch_cap = DEFAULT_BATCH;
+    int64_t age = AGE;
     // nodes (ids in discovery order)
     std::vector<uint64_t> keys;
     std::vector<int64_t> parent;
@@ -163,10 +172,13 @@ struct Engine {
     std::vector<int64_t> c_known;
     std::vector<int32_t> c_round;
     std::vector<int32_t> free_slots;
-    // nodes appended in the last W rounds (the in-flight set): open addressing on the hash
-    std::vector<int64_t> recent;  // id + 1, 0 = empty
-    uint64_t rmask = 0;
-    int64_t recent_floor = 0;      // the table holds every id >= recent_floor
+    // the recently appended nodes (the in-flight set), two generations of up to AGE ids each:
+    // gen[cur] holds ids >= gen_lo[cur], gen[cur ^ 1] the AGE ids before them; open addressing
+    // with entries (id + 1) << 16 | 16-bit tag, so a probe reads a node's key only on a tag hit
+    std::vector<uint64_t> gen[2];
+    int64_t gen_lo[2] = {0, 0};
+    int cur = 0;
+    uint64_t gmask = 0;
     std::vector<int64_t> n_at_round;  // node count when round r's kernel probed the device table
     int64_t committed = 0;            // ids < committed are in the device table
     int round = 0;
@@ -180,16 +192,32 @@ struct Engine {
     int found_action = -1, last_action = -1, last_len = -1;
     uint64_t found_key[ACX_MAX_L / 16 + 2] = {0};
     int64_t st_rounds = 0, st_expanded = 0, ns_select = 0, ns_gpu = 0, ns_replay = 0, st_known = 0;
-    // device: one staging buffer each way per round (parents + committed keys in; child keys,
-    // hashes and known ids out), so a round is 1 H2D + 2 launches + 1 D2H + 1 sync
+    // why each round's replay stopped: the top node was appended during that replay / was an
+    // older node outside the round's batch / had children cached too long ago
+    int64_t st_stop_new = 0, st_stop_old = 0, st_stop_aged = 0;
+    int64_t ns_wait = 0, ns_cache = 0;
+    int64_t st_retired = 0;  // cached expansions retired unused because they aged  // inside the round trip: polling for the GPU / caching children
+    // staging: pinned host buffers the kernels read (parents + committed keys) and write (child
+    // keys, hashes, known ids) directly, so a round is 2 launches and a completion poll -- no
+    // copies, no blocking synchronisation
     hipStream_t stream = nullptr;
     DevArgs d{};
-    uint64_t *d_in = nullptr, *d_out = nullptr;
-    uint64_t *h_in = nullptr, *h_out = nullptr;  // pinned
+    uint64_t *h_in = nullptr, *h_out = nullptr;    // pinned, host view
+    uint64_t *hd_in = nullptr, *hd_out = nullptr;  // the same memory, device view
     int64_t commit_cap = 0;
 
+    // wait for the stream by polling (hipStreamSynchronize may sleep on an interrupt: tens of us
+    // per round at ~1500 rounds per 10^6-node search)
+    int wait() const {
+        hipError_t e;
+        while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+        }
+        return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+    }
+
     ~Engine() {
-        void* dp[] = {d_in, d_out, d.nkeys, d.table};
+        if (stream) (void)hipStreamSynchronize(stream);
+        void* dp[] = {d.nkeys, d.table};
         for (void* p : dp)
             if (p) (void)hipFree(p);
         void* hp[] = {h_in, h_out};
@@ -206,7 +234,8 @@ struct Engine {
         cyc = cyc_;
         max_nodes = max_nodes_;
         cap = max_nodes + 12;
-        batch_cap = batch > 0 ? batch : 512;
+        batch_cap = batch > 0 ? batch : DEFAULT_BATCH;
+        age = g_age_override > 0 ? g_age_override : AGE;  // a power of two
         if (hipGetDevice(&dev) != hipSuccess) return false;
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
         uint64_t ts = 1024;
@@ -214,12 +243,12 @@ struct Engine {
         commit_cap = 4 * (int64_t)batch_cap * ACT + 64;
         const size_t nb = (size_t)batch_cap;
         const size_t in_words = (nb + (size_t)commit_cap) * kw, out_words = nb * ACT * (kw + 2);
-        bool ok = hipMalloc((void**)&d_in, in_words * 8) == hipSuccess &&
-                  hipMalloc((void**)&d_out, out_words * 8) == hipSuccess &&
-                  hipMalloc((void**)&d.nkeys, (size_t)cap * kw * 8) == hipSuccess &&
+        bool ok = hipMalloc((void**)&d.nkeys, (size_t)cap * kw * 8) == hipSuccess &&
                   hipMalloc((void**)&d.table, ts * 8) == hipSuccess &&
-                  hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocDefault) == hipSuccess &&
+                  hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocMapped) == hipSuccess &&
+                  hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocMapped) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&hd_in, h_in, 0) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&hd_out, h_out, 0) == hipSuccess &&
                   hipMemsetAsync(d.table, 0, ts * 8, stream) == hipSuccess;
         if (!ok) {
             (void)hipGetLastError();
@@ -229,8 +258,6 @@ struct Engine {
         d.L = L;
         d.kw = kw;
         d.cyc = cyc;
-        recent.assign(1 << 12, 0);
-        rmask = recent.size() - 1;
         return true;
     }
 
@@ -304,6 +331,10 @@ struct Engine {
             return false;
         }
         bool empty() const { return id.empty(); }
+        void reserve(size_t n) {
+            id.reserve(n);
+            k.reserve(n * pk);
+        }
         size_t size() const { return id.size(); }
         int64_t top() const { return id[0]; }
         void push(const uint64_t* key, int64_t v) {
@@ -353,28 +384,38 @@ struct Engine {
         const uint64_t* top_key() const { return k.data(); }
     };
     Heap frontier;    // every node not popped yet: the reference's to_explore (pop order)
-    Heap unexpanded;  // the subset without usable cached children (expansion order)
+    // cached expansions in round order, to retire the ones that aged (their node then counts as
+    // unexpanded again and is picked up by select() with the other smallest unexpanded nodes)
+    std::vector<std::pair<int32_t, int64_t>> cache_fifo;
+    size_t fifo_head = 0;
+    Heap unexpanded;  // the frontier nodes without usable cached children (expansion order)
 
     // ---------------------------------------------------------------- in-flight table
+    static uint64_t tag_of(uint64_t h) { return (h >> 48) & 0xffffu; }
     void recent_insert(int64_t id, uint64_t h) {
-        uint64_t s = h & rmask;
-        while (recent[s]) s = (s + 1) & rmask;
-        recent[s] = id + 1;
+        if (id - gen_lo[cur] >= age) {  // the current generation is full: it becomes the older one
+            cur ^= 1;
+            std::fill(gen[cur].begin(), gen[cur].end(), 0ull);
+            gen_lo[cur] = id;
+        }
+        std::vector<uint64_t>& g = gen[cur];
+        uint64_t s = h & gmask;
+        while (g[s]) s = (s + 1) & gmask;
+        g[s] = ((uint64_t)(id + 1) << 16) | tag_of(h);
     }
-    void recent_rebuild(int64_t floor, size_t need) {
-        size_t sz = 1 << 12;
-        while (sz < 2 * need + 16) sz <<= 1;
-        recent.assign(sz, 0);
-        rmask = sz - 1;
-        recent_floor = floor;
-        const int64_t n = (int64_t)parent.size();
-        for (int64_t id = floor; id < n; ++id) recent_insert(id, host_hash(&keys[(size_t)id * kw], kw));
-    }
-    // a node with id >= from equal to key k, or -1
+    // a node with id >= from equal to key k, or -1 (from >= the older generation's first id:
+    // usable() admits only caches probed fewer than AGE appends ago)
     int64_t recent_find(const uint64_t* k, uint64_t h, int64_t from) const {
-        for (uint64_t s = h & rmask; recent[s]; s = (s + 1) & rmask) {
-            const int64_t id = recent[s] - 1;
-            if (id >= from && memcmp(&keys[(size_t)id * kw], k, 8 * kw) == 0) return id;
+        const uint64_t tag = tag_of(h);
+        for (int i = 0; i < 2; ++i) {
+            const int gi = cur ^ i;
+            if (i == 1 && gen_lo[cur] <= from) break;  // every id >= from is in the current one
+            const std::vector<uint64_t>& g = gen[gi];
+            for (uint64_t s = h & gmask; g[s]; s = (s + 1) & gmask) {
+                if ((g[s] & 0xffffu) != tag) continue;
+                const int64_t id = (int64_t)(g[s] >> 16) - 1;
+                if (id >= from && memcmp(&keys[(size_t)id * kw], k, 8 * kw) == 0) return id;
+            }
         }
         return -1;
     }
@@ -388,7 +429,6 @@ struct Engine {
         depth.push_back(dep);
         cache_slot.push_back(-1);
         recent_insert(id, h);
-        if ((int64_t)(id - recent_floor) * 2 + 16 > (int64_t)recent.size()) recent_rebuild(recent_floor, id - recent_floor + 1);
         uint64_t pkey[32];
         prio_key(k, tot, dep, pkey);
         frontier.push(pkey, id);
@@ -398,7 +438,7 @@ struct Engine {
 
     bool usable(int64_t id) const {
         const int32_t s = cache_slot[id];
-        return s >= 0 && (int64_t)parent.size() - n_at_round[c_round[s]] <= AGE;
+        return s >= 0 && (int64_t)parent.size() - n_at_round[c_round[s]] <= age;
     }
     void drop_cache(int64_t id) {
         const int32_t s = cache_slot[id];
@@ -459,8 +499,30 @@ struct Engine {
     }
 
     // the smallest frontier nodes without usable cached children (greedy expands them next)
+    void push_unexpanded(int64_t id) {
+        uint64_t pkey[32];
+        prio_key(&keys[(size_t)id * kw], total[id], depth[id], pkey);
+        unexpanded.push(pkey, id);
+    }
+
+    // the smallest frontier nodes without usable cached children (greedy expands them next)
     void select(std::vector<int64_t>& out) {
         out.clear();
+        // retire the caches that aged since the last round: their nodes are unexpanded again
+        const int64_t nn = (int64_t)parent.size();
+        while (fifo_head < cache_fifo.size() && nn - n_at_round[cache_fifo[fifo_head].first] > age) {
+            const auto [r, id] = cache_fifo[fifo_head++];
+            const int32_t sl = cache_slot[id];
+            if (sl >= 0 && c_round[sl] == r) {
+                ++st_retired;
+                drop_cache(id);
+                push_unexpanded(id);
+            }
+        }
+        if (fifo_head > 4096 && fifo_head * 2 > cache_fifo.size()) {
+            cache_fifo.erase(cache_fifo.begin(), cache_fifo.begin() + (ptrdiff_t)fifo_head);
+            fifo_head = 0;
+        }
         while (!unexpanded.empty() && (int)out.size() < batch_cap) {
             out.push_back(unexpanded.top());
             unexpanded.pop();
@@ -482,7 +544,21 @@ struct Engine {
         total.assign(1, (int16_t)tot0);
         depth.assign(1, 0);
         cache_slot.assign(1, -1);
-        recent_rebuild(0, 1);
+        // every per-node array at its final size up front (no reallocation copies mid-search)
+        const size_t nres = (size_t)std::min<int64_t>(cap, 1 << 26);
+        keys.reserve(nres * kw);
+        for (auto* v : {&parent}) v->reserve(nres);
+        action.reserve(nres);
+        total.reserve(nres);
+        depth.reserve(nres);
+        cache_slot.reserve(nres);
+        frontier.reserve(nres);
+        unexpanded.reserve(nres);
+        for (auto& g : gen) g.assign((size_t)2 * age, 0ull);
+        gmask = 2 * age - 1;
+        cur = 0;
+        gen_lo[0] = gen_lo[1] = 0;
+        recent_insert(0, host_hash(root, kw));
         uint64_t pkey[32];
         prio_key(root, tot0, 0, pkey);
         frontier.push(pkey, 0);
@@ -490,14 +566,11 @@ struct Engine {
         std::vector<int64_t> batch;
         while (status == 0) {
             const int64_t t0 = now_ns();
+            const int64_t n_sel = (int64_t)parent.size();
             if (frontier.empty()) {  // to_explore ran empty (greedy.py:71)
                 status = 2;
                 break;
             }
-            // the in-flight table must hold every id >= (nodes - AGE): the probes of usable caches
-            // saw everything below; refloored every AGE appended nodes, so it stays <= 2 AGE
-            const int64_t want_floor = (int64_t)parent.size() - AGE;
-            if (want_floor > recent_floor + AGE) recent_rebuild(want_floor, (size_t)AGE);
             select(batch);
             const int64_t t1 = now_ns();
             ns_select += t1 - t0;
@@ -515,8 +588,13 @@ struct Engine {
                 const int64_t id = frontier.top();
                 if (!usable(id)) {
                     if (cache_slot[id] >= 0) {  // expanded before the last AGE appends: expand again
+                        ++st_stop_aged;
                         drop_cache(id);
                         unexpanded.push(frontier.top_key(), id);
+                    } else if (id >= n_sel) {
+                        ++st_stop_new;
+                    } else {
+                        ++st_stop_old;
                     }
                     break;
                 }
@@ -557,10 +635,8 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
         const int64_t hi = std::min(n_nodes, lo + commit_cap);
         uint64_t* cst = h_in + (size_t)n * kw;
         if (hi > lo) memcpy(cst, &keys[(size_t)lo * kw], (size_t)(hi - lo) * kw * 8);
-        const size_t words = (size_t)(n + (hi - lo)) * kw;
-        if (hipMemcpyAsync(d_in, h_in, words * 8, hipMemcpyHostToDevice, stream) != hipSuccess) return ACX_E_LAUNCH;
         if (hi > lo) {
-            d.commit = d_in + (size_t)n * kw;
+            d.commit = hd_in + (size_t)n * kw;
             d.lo = lo;
             d.hi = hi;
             CommitLaunch cl{this};
@@ -568,22 +644,22 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
         }
         lo = hi;
         if (lo >= n_nodes) break;
-        if (hipStreamSynchronize(stream) != hipSuccess) return ACX_E_LAUNCH;  // h_in is reused
+        if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return ACX_E_LAUNCH;  // h_in is reused
     }
     committed = n_nodes;
     n_at_round.push_back(n_nodes);
-    if (n == 0) return hipStreamSynchronize(stream) == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+    if (n == 0) return hipGetLastError() == hipSuccess ? wait() : ACX_E_LAUNCH;
     d.n = n;
-    d.parents = d_in;
-    d.ckeys = d_out;
-    d.chash = d_out + (size_t)n * ACT * kw;
+    d.parents = hd_in;
+    d.ckeys = hd_out;
+    d.chash = hd_out + (size_t)n * ACT * kw;
     d.cknown = reinterpret_cast<int64_t*>(d.chash + (size_t)n * ACT);
     ExpandLaunch el{this};
     bfs::by_nw(L, el);
-    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
-    if (hipMemcpyAsync(h_out, d_out, (size_t)n * ACT * (kw + 2) * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
-        return ACX_E_LAUNCH;
+    const int64_t tw = now_ns();
+    if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return ACX_E_LAUNCH;
+    const int64_t tc = now_ns();
+    ns_wait += tc - tw;
     const uint64_t* ck = h_out;
     const uint64_t* ch = h_out + (size_t)n * ACT * kw;
     const int64_t* kn = reinterpret_cast<const int64_t*>(ch + (size_t)n * ACT);
@@ -604,7 +680,9 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
         memcpy(&c_known[(size_t)s * ACT], kn + (size_t)i * ACT, ACT * 8);
         c_round[s] = round;
         cache_slot[batch[i]] = s;
+        cache_fifo.emplace_back(round, batch[i]);
     }
+    ns_cache += now_ns() - tc;
     ++st_rounds;
     st_expanded += n;
     return ACX_OK;
@@ -634,6 +712,10 @@ int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, in
 }
 
 void acx_greedy_destroy(void* h) { delete static_cast<Engine*>(h); }
+
+// tests only (not in acx.h): searches started afterwards use 2^log2_age as the cache age limit
+// (0: the default 2^20), so the re-expansion of aged caches is exercised at test sizes
+void acx_internal_greedy_age(int32_t log2_age) { g_age_override = log2_age > 0 ? (int64_t)1 << log2_age : 0; }
 
 // 0 running, 1 success, 2 failed, 3 move error; budget_hit, min_length, nodes (len(tree_nodes))
 int32_t acx_greedy_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {
@@ -666,7 +748,10 @@ int64_t acx_greedy_path(void* h, int32_t* actions, int32_t* totals, int64_t cap)
 }
 
 // out[0] rounds, [1] parents expanded, [2] parents popped, [3] children the device knew,
-// [4..6] host ns selecting / in the GPU round trip / replaying
+// [4..6] host ns selecting / in the GPU round trip / replaying, [7..9] replays that stopped at a
+// node appended during the replay / at an older unexpanded node / at an aged cache, [10..11] ns
+// of the round trips spent polling for the GPU / caching children, [12] cached expansions
+// retired unused because they aged
 void acx_greedy_stats(void* h, int64_t* out) {
     Engine* E = static_cast<Engine*>(h);
     out[0] = E->st_rounds;
@@ -676,6 +761,12 @@ void acx_greedy_stats(void* h, int64_t* out) {
     out[4] = E->ns_select;
     out[5] = E->ns_gpu;
     out[6] = E->ns_replay;
+    out[7] = E->st_stop_new;
+    out[8] = E->st_stop_old;
+    out[9] = E->st_stop_aged;
+    out[10] = E->ns_wait;
+    out[11] = E->ns_cache;
+    out[12] = E->st_retired;
 }
 
 int64_t acx_greedy_min_trace(void* h, int32_t* out, int64_t cap) {

@@ -358,12 +358,16 @@ int32_t acx_search_found(void* h, int32_t* first_letters, int64_t* explored);
  * frontier nodes not yet expanded (lane per (parent, action)) and probes every child against the
  * HBM hash table of the committed nodes; the host replays the reference's pop / dedup / budget
  * order exactly, checking only the children the device did not know against the nodes appended
- * since (the in-flight conflicts).  batch = parents per round (<= 0: 512).
+ * since (the in-flight conflicts).  batch = parents per round (<= 0: 64).
  *   acx_greedy_run       searches from `presentation` (HOST pointer, 2L int32, letters +-1/+-2);
  *                        *out_handle receives the finished search (query it, then destroy)
  *   acx_greedy_status / _path / _min_trace / _popped / _node_keys / _found   as acx_search_*
  *   acx_greedy_stats     out[0] rounds, [1] parents expanded, [2] popped, [3] children the device
- *                        knew, [4..6] host ns selecting / GPU round trips / replaying
+ *                        knew, [4..6] host ns selecting / GPU round trips / replaying, [7..9] replays
+ *                        stopped at a node appended in that replay / an older unexpanded node / an
+ *                        aged cache, [10..11] ns of the round trips spent polling for the GPU /
+ *                        caching children, [12] cached expansions retired unused because they aged
+ *                        (13 int64)
  */
 int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, int32_t cyclical, int32_t batch,
                    void** out_handle);
