@@ -415,7 +415,7 @@ def gen_kat_search_extra(ref, n_cases=240):
     return cases
 
 
-SCALE_CHECKPOINTS = (1, 10, 100, 1000, 10000, 100000, 1000000)
+SCALE_CHECKPOINTS = (1, 10, 100, 1000, 10000, 100000, 1000000, 1500000)
 
 
 def run_recorded_search(ref, fn, pres, budget, cyclical):
@@ -662,6 +662,18 @@ if __name__ == "__main__":
         ap.add_argument("--reference", default="/root/reference")
         with open(os.path.join(HERE, "unit_cases.json"), "w") as f:
             json.dump(gen_unit_cases(load_reference(ap.parse_args().reference)), f)
+    elif "--search-scale-1e7" in sys.argv:  # only (re)generate search_scale_1e7.json (config 4 at full size)
+        sys.argv.remove("--search-scale-1e7")
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--reference", default="/root/reference")
+        root = ap.parse_args().reference
+        ref = load_reference(root)
+        ak3 = ref.utils.convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
+        out = [run_recorded_search(ref, "bfs", ak3, 10 ** 7, False)]
+        with open(os.path.join(HERE, "search_scale_1e7.json"), "w") as f:
+            json.dump(out, f)
+        for r in out:
+            print(r["search_fn"], r["L"], r["budget"], r["cyclical"], r["ok"], r["parents"], r["stdout"][-1:])
     elif "--search-scale" in sys.argv:  # only (re)generate search_scale.json
         sys.argv.remove("--search-scale")
         ap = argparse.ArgumentParser()

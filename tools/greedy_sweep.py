@@ -32,4 +32,14 @@ for name, p in cases.items():
               if k not in ("node_keys", "min_trace", "popped")}
         out[f"{name}_b{b}"] = {"wall_s": round(dt, 4), "path_len": len(path), **st}
         print(json.dumps({f"{name}_b{b}": out[f"{name}_b{b}"]}), file=sys.stderr, flush=True)
+    # the host-dedup engine (round 1's path: acx_expand12 launches + csrc/acx_search.cpp), warm
+    for rep in range(2):
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            ok, path = acx.greedy_search(presentation=p, max_nodes_to_explore=budget, engine="host")
+        dt = time.perf_counter() - t0
+    st = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in _engine.LAST_STATS.items()
+          if k not in ("node_keys", "min_trace", "popped")}
+    out[f"{name}_host"] = {"wall_s": round(dt, 4), "path_len": len(path), **st}
+    print(json.dumps({f"{name}_host": out[f"{name}_host"]}), file=sys.stderr, flush=True)
 print(json.dumps(out))

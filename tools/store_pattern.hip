@@ -112,6 +112,16 @@ __global__ __launch_bounds__(256, 8) void tile_pattern(int4* obs, int32_t* rew, 
     }
 }
 
+// tile_pattern<F_NT> with extra dynamic LDS per block, to cap the resident blocks per CU (and so
+// the write window: resident waves x 18 KB) -- occupancy vs placement sensitivity
+extern "C" int sp_tile_occ(void* obs, int64_t B, int T, int row_chunks, int lds_pad, void* stream) {
+    if (B <= 0 || B % 64 != 0 || T <= 0 || row_chunks <= 0 || lds_pad < 0) return -1;
+    dim3 grid((unsigned)((B + 255) / 256));
+    tile_pattern<F_NT><<<grid, 256, (size_t)lds_pad, (hipStream_t)stream>>>((int4*)obs, nullptr, nullptr, nullptr,
+                                                                           nullptr, B, T, row_chunks);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // each wave owns TWO 64-row tiles and writes both every step (4 waves/SIMD, so a 2^20-env batch
 // is resident in one round instead of two rounds of one-tile waves)
 __global__ __launch_bounds__(256, 4) void tile2_pattern(int4* obs, int64_t B, int T, int row_chunks) {
