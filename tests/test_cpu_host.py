@@ -253,3 +253,37 @@ def test_engine_matches_reference_scale_cases_at_L128_on_oracle_expansions():
         budget = [x for x in c["stdout"] if x.startswith("Exiting")]
         assert budget == [f"Exiting search as number of explored nodes = {n_nodes.value} has exceeded the limit "
                           f"{c['budget']}"]
+
+
+def test_on_disk_loaders_text_formats(tmp_path):
+    """read_presentations / to_batch / read_path on files in the reference's formats: one Python
+    list literal per line with each presentation at its own max length (the layout of
+    search/miller_schupp/data/*.txt read by agents/utils.py:10-34), and an AC path file
+    (notebooks/paths/*.txt, one list of move ids)."""
+    from acx import data
+    ms = data.load_initial_states("all")
+    rows = []
+    for p in ms[:40]:
+        L0 = len(p) // 2
+        a, b = p[:L0][p[:L0] != 0], p[L0:][p[L0:] != 0]
+        Lp = max(len(a), len(b))  # each line padded to its own length, as the reference files are
+        q = np.zeros(2 * Lp, np.int64)
+        q[: len(a)], q[Lp : Lp + len(b)] = a, b
+        rows.append(q)
+    f = tmp_path / "presentations.txt"
+    f.write_text("\n".join(str(list(map(int, q))) for q in rows) + "\n\n")
+    got = data.read_presentations(str(f))
+    assert [list(x) for x in got] == [list(map(int, q)) for q in rows]
+    batch = data.to_batch(got, 36)
+    assert batch.dtype == np.int32 and batch.shape == (40, 72)
+    assert np.array_equal(batch, data.load_initial_states("all", 36)[:40])
+    with pytest.raises(ValueError):
+        data.to_batch([[1, 1, 1, 2, 2, 2]], 2)
+    pth = tmp_path / "AC_path.txt"
+    pth.write_text("[3, 11, 0, 7, 5]\n")
+    assert data.read_path(str(pth)) == [3, 11, 0, 7, 5]
+    # the text is parsed, never executed
+    bad = tmp_path / "bad.txt"
+    bad.write_text("__import__('os').getcwd()\n")
+    with pytest.raises(ValueError):
+        data.read_presentations(str(bad))

@@ -4,7 +4,7 @@
 # steps are chained so a failure ends the session.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r02}
+TAG=${1:-r02}  # usage: bash tools/gpu_session.sh TAG  (PROFILE=0: skip the rocprofv3 passes)
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
