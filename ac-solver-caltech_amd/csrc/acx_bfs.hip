@@ -103,23 +103,6 @@ struct Args {
     int P, L, kw, cyc, ntiles;
 };
 
-__device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, WAVE));
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) v += (uint32_t)__shfl_xor((int)v, o, WAVE);
-    return v;
-}
-
 // (1) expand: one block per tile of 64 parents; wave w makes the children of actions 3w..3w+2
 // (4x the lanes of a lane-per-parent loop: the move chain is latency-bound, and a 2^19-parent
 // chunk is only ~8 waves per SIMD that way); keys staged through LDS, written coalesced

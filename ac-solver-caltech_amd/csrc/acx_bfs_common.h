@@ -56,6 +56,24 @@ __host__ __device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
     return fmix64(h);
 }
 
+// LDS written by the wave's lanes is visible to the whole wave after this
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, WAVE));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) v += (uint32_t)__shfl_xor((int)v, o, WAVE);
+    return v;
+}
+
 __device__ __forceinline__ uint64_t tload(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -77,6 +77,7 @@ struct Args {
     uint64_t* send;        // (nsend, kw + 1) records grouped by owner
     uint32_t* gmask;       // (P) survivor masks (this rank's, then all-reduced)
     int64_t* look;         // lookup result
+    uint32_t* xblk;        // (expand blocks, 2 + world) per-block min child total, parents, owner counts
     uint64_t mask;
     int64_t head, n_before, need, lcap, nloc, lo, nrecv;
     int P, Pr, L, kw, cyc, world;
@@ -87,77 +88,140 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
     return (uint32_t)(((h >> 32) * (uint64_t)world) >> 32);
 }
 
-// (1) lane per candidate local parent lo + j (j < Pr = min(P, nloc - lo)); the parents of the
-// chunk are the prefix with gid < head + P
+// (1) block per tile of 64 candidate local parents lo + j (j < Pr = min(P, nloc - lo); the
+// parents of the chunk are the prefix with gid < head + P); wave w makes the children of actions
+// 3w..3w+2 of the same 64 parents (as acx_bfs.hip's bfs_expand_kernel: 4x the lanes of a
+// lane-per-parent loop over 12 serial moves), child keys staged in LDS and written action-major
+// as coalesced runs, owners counted by ballots
+constexpr int STILE = 64;
+constexpr int SAPW = 12 / (TPB / WAVE);  // actions per wave (3)
 template <int NW>
 __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
+    __shared__ uint64_t kst[TPB / WAVE][STILE * (NW + 1)];
     __shared__ uint32_t hist[MAXW];
+    __shared__ uint32_t smin[STILE];
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     for (int i = threadIdx.x; i < a.world; i += TPB) hist[i] = 0;
-    __syncthreads();
-    const int j = blockIdx.x * TPB + threadIdx.x;
+    if (wid == 0) smin[lane] = 0xffffu;
+    const int j0 = blockIdx.x * STILE;
+    const int j = j0 + lane;
     const int64_t gid = j < a.Pr ? a.lgid[a.lo + j] : INT64_MAX;
     const bool live = gid < a.head + a.P;
-    uint8_t own[12];
-#pragma unroll
-    for (int act = 0; act < 12; ++act) own[act] = 0xff;
-    uint32_t mn_lane = NONE;
+    const int kw = a.kw;
+    const bool cyc = a.cyc != 0;
+    PresRegs<NW> pr;
+    bool clean = false;
     if (live) {
-        PresRegs<NW> pr;
-        load_key<NW>(a.lkeys + (a.lo + j) * a.kw, a.kw, a.L, pr);
-        const bool cyc = a.cyc != 0;
-        const bool clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, cyc);
-        const uint32_t p = (uint32_t)(gid - a.head);
-        uint32_t succ = NONE, err = NONE;
-        int mn = 0xffff;
-        for (int act = 0; act < 12; ++act) {
+        load_key<NW>(a.lkeys + (a.lo + j) * kw, kw, a.L, pr);
+        clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, cyc);
+    }
+    __syncthreads();
+    const uint32_t p = live ? (uint32_t)(gid - a.head) : 0u;
+    uint32_t succ = NONE, err = NONE, mn = 0xffffu;
+    uint32_t ownp = 0xffffffu;  // owner byte of action 3w + jj at bits 8 jj (a runtime-indexed
+                                // array here would live in scratch: the loop is not unrolled)
+    uint64_t* st = kst[wid];
+    const int nrow = min(STILE, a.Pr - j0);  // the tile's lanes with a local parent slot
+#pragma unroll 1
+    for (int jj = 0; jj < SAPW; ++jj) {
+        const int act = wid * SAPW + jj;
+        uint32_t own = 0xff;
+        if (live) {
             PresRegs<NW> q = pr;
             const int e = clean ? ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc)
                                 : ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, cyc);
             const uint32_t s = p * 12u + (uint32_t)act;
-            const int tot = q.n0 + q.n1;
             if (e != ACX_ERR_NONE) {
-                if (err == NONE) err = s;
+                err = min(err, s);
             } else {
-                if (tot == 2 && succ == NONE) succ = s;
-                mn = tot < mn ? tot : mn;
+                const uint32_t tot = (uint32_t)(q.n0 + q.n1);
+                if (tot == 2) succ = min(succ, s);
+                mn = min(mn, tot);
             }
             Key<NW + 1> key;
             make_key<NW>(a.L, q, key.w);
-            uint64_t* dst = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
+            own = owner_of(khash<NW + 1>(key, kw), a.world);
+            ownp = (ownp & ~(0xffu << (8 * jj))) | (own << (8 * jj));
 #pragma unroll
             for (int k = 0; k < NW + 1; ++k)
-                if (k < a.kw) dst[k] = key.w[k];
-            own[act] = (uint8_t)owner_of(khash<NW + 1>(key, a.kw), a.world);
-            a.cown[(int64_t)act * a.Pr + j] = own[act];
+                if (k < kw) st[lane * kw + k] = key.w[k];
         }
-        a.pmin[j] = (uint16_t)mn;
-        mn_lane = (uint32_t)mn;
-        if (succ != NONE) atomicMin(&a.ctl->succ_seq, succ);
-        if (err != NONE) atomicMin(&a.ctl->err_seq, err);
-    } else if (j < a.Pr) {
-        for (int act = 0; act < 12; ++act) a.cown[(int64_t)act * a.Pr + j] = 0xff;
+        wsync();
+        // the tile's keys of this action: one contiguous run (lanes past Pr have no slot; a lane
+        // whose parent is past the chunk writes a stale key its owner byte 0xff tells pack to skip)
+        uint64_t* o = a.ckeys + ((int64_t)act * a.Pr + j0) * kw;
+        for (int i = lane; i < nrow * kw; i += WAVE) o[i] = st[i];
+        if (j < a.Pr) a.cown[(int64_t)act * a.Pr + j] = (uint8_t)own;
+        wsync();
     }
-    // per-owner counts: one ballot per (action, owner) and one LDS add per wave, instead of a
-    // same-address LDS atomic per child
-    const int lane = threadIdx.x & (WAVE - 1);
+    // per-owner counts: one ballot per (action, owner) and one LDS add per wave
     for (int o = 0; o < a.world; ++o) {
         uint32_t c = 0;
 #pragma unroll
-        for (int act = 0; act < 12; ++act) c += __popcll(__ballot(own[act] == o));
-        if (lane == 0 && c) atomicAdd(&hist[o], c);
+        for (int jj = 0; jj < SAPW; ++jj) c += __popcll(__ballot(((ownp >> (8 * jj)) & 0xffu) == (uint32_t)o));
+        if (lane == 0 && c) atomicAdd(&hist[o], c);  // LDS
     }
-    // chunk min length and local parent count: one atomic per block (a same-address atomic per
-    // lane serialises in L2)
-    __shared__ uint32_t sh[TPB / WAVE];
-    const uint32_t bmin = block_min(mn_lane, sh);
+    if (live) atomicMin(&smin[lane], mn);
+    succ = wave_min(succ);
+    err = wave_min(err);
+    if (lane == 0) {  // rare: one global atomic per wave that has one
+        if (succ != NONE) atomicMin(&a.ctl->succ_seq, succ);
+        if (err != NONE) atomicMin(&a.ctl->err_seq, err);
+    }
     __syncthreads();
-    const uint32_t bpar = block_min(live ? NONE - (uint32_t)(j + 1) : NONE, sh);
-    if (threadIdx.x == 0) {
-        if (bmin != NONE) atomicMin(&a.ctl->min_len, bmin);
-        if (bpar != NONE) atomicMax(&a.ctl->npar, NONE - bpar);
+    // the block's min child total, parent count and owner counts go to its own record, reduced
+    // by sbfs_expand_reduce_kernel: a same-address atomic per block serialises in L2 (3 of them
+    // per block over the 8,192 blocks of a 2^19-parent chunk cost ~80 us)
+    uint32_t* x = a.xblk + (size_t)blockIdx.x * (2 + a.world);
+    if (wid == 0) {
+        const uint32_t m = smin[lane];
+        if (live) a.pmin[j] = (uint16_t)m;
+        const uint32_t bmin = wave_min(live ? m : NONE);
+        const uint32_t bpar = wave_min(live ? NONE - (uint32_t)(j + 1) : NONE);
+        if (lane == 0) {
+            x[0] = bmin;
+            x[1] = NONE - bpar;  // 1 + last live lane's j, 0 if none
+        }
     }
-    for (int i = threadIdx.x; i < a.world; i += TPB)
-        if (hist[i]) atomicAdd(&a.ctl->cnt[i], hist[i]);
+    for (int i = threadIdx.x; i < a.world; i += TPB) x[2 + i] = hist[i];
+}
+
+// (1b) the expand blocks' records -> the chunk's min child total, local parent count and
+// children per owner (one block)
+__global__ __launch_bounds__(1024) void sbfs_expand_reduce_kernel(Args a, int nblk) {
+    __shared__ uint32_t cnt[MAXW];
+    __shared__ uint32_t red[2][1024 / WAVE];
+    const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
+    const int rw = 2 + a.world;
+    for (int i = t; i < a.world; i += 1024) cnt[i] = 0;
+    __syncthreads();
+    uint32_t mn = NONE, np = 0;
+    for (int b = t; b < nblk; b += 1024) {
+        mn = min(mn, a.xblk[(size_t)b * rw]);
+        np = max(np, a.xblk[(size_t)b * rw + 1]);
+    }
+    for (int64_t i = t; i < (int64_t)nblk * a.world; i += 1024) {
+        const int b = (int)(i / a.world), o = (int)(i - (int64_t)b * a.world);
+        const uint32_t v = a.xblk[(size_t)b * rw + 2 + o];
+        if (v) atomicAdd(&cnt[o], v);
+    }
+    mn = wave_min(mn);
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) np = max(np, (uint32_t)__shfl_xor((int)np, o, WAVE));
+    if (lane == 0) {
+        red[0][wid] = mn;
+        red[1][wid] = np;
+    }
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < 1024 / WAVE; ++w) {
+            mn = min(mn, red[0][w]);
+            np = max(np, red[1][w]);
+        }
+        if (mn != NONE) a.ctl->min_len = min(a.ctl->min_len, mn);
+        a.ctl->npar = np;
+    }
+    for (int i = t; i < a.world; i += 1024) a.ctl->cnt[i] = cnt[i];
 }
 
 // (2) records into the send buffer, grouped by owner (order within a group is arbitrary:
@@ -336,47 +400,75 @@ __global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, int nb, ui
     if (t == 0) *total = tot;
 }
 
-// (4c) global ids, the budget cut, and the appends to this rank's store
+// (4c) global ids, the budget cut, and the appends to this rank's store.  A block's own
+// survivors take consecutive store slots (their global ids ascend with the slot), so each lane
+// stages its survivors in LDS at their block-local rank and the block then writes the slot range
+// cooperatively: keys as one coalesced run, ids / parents / moves as coalesced arrays (the
+// round-1 lane-per-parent loop wrote up to 12 scattered key copies per lane: 129 us per chunk).
+constexpr int CMAX = TPB * 12;  // own survivors a block can stage
 __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
+    __shared__ uint32_t srec[CMAX];  // received-record index of the k-th own survivor
+    __shared__ uint32_t sinf[CMAX];  // parent within the block (8 bits) | move (4) | id offset (12)
     const int p = blockIdx.x * TPB + threadIdx.x;
     const uint32_t m = p < a.P ? a.gmask[p] : 0u;
     const uint32_t mine = p < a.P ? own_bits(a, (uint32_t)p, m) : 0u;
     uint32_t tot;
-    const int64_t base = (int64_t)a.bsum[blockIdx.x] + block_excl_scan(__popc(m), sh, tot);
+    const uint32_t bex = block_excl_scan(__popc(m), sh, tot);  // survivors of the block before p
+    const int64_t base = (int64_t)a.bsum[blockIdx.x] + bex;
     __syncthreads();
-    const int64_t lbase = (int64_t)a.lbsum[blockIdx.x] + block_excl_scan(__popc(mine), sh, tot);
-    if (p >= a.P) return;
-    const int64_t incl = base + __popc(m);
-    if (incl >= a.need && (base < a.need || p == 0)) {
-        a.ctl->cut_p = (uint32_t)p;
-        a.ctl->nodes_at_cut = (uint64_t)(a.n_before + incl);
+    uint32_t ltot;
+    const uint32_t lrank = block_excl_scan(__popc(mine), sh, ltot);
+    if (p < a.P) {
+        const int64_t incl = base + __popc(m);
+        if (incl >= a.need && (base < a.need || p == 0)) {
+            a.ctl->cut_p = (uint32_t)p;
+            a.ctl->nodes_at_cut = (uint64_t)(a.n_before + incl);
+        }
     }
-    uint32_t mm = mine, stored = 0;
+    uint32_t mm = mine, k = lrank;
     while (mm) {
         const int act = __builtin_ctz(mm);
         mm &= mm - 1;
-        const uint32_t below = (1u << act) - 1u;
-        const int64_t gid = a.n_before + base + __popc(m & below);
-        // a node at or past max_nodes + 12 comes after the budget cut and is never used (the
-        // single-GPU queue drops it too); the ones kept are a prefix of this rank's appends
-        if (gid >= a.n_before + a.need + 12) continue;
-        const int64_t li = a.nloc + lbase + __popc(mine & below);
+        srec[k] = a.map[(uint32_t)p * 12u + act];
+        sinf[k] = (uint32_t)threadIdx.x << 16 | (uint32_t)act << 12 | (bex + __popc(m & ((1u << act) - 1u)));
+        ++k;
+    }
+    __syncthreads();
+    // a node at or past max_nodes + 12 comes after the budget cut and is never used (the
+    // single-GPU queue drops it too): the stored ones are a prefix of the slot range
+    const int64_t g0 = a.n_before + (int64_t)a.bsum[blockIdx.x];  // id of the block's first survivor
+    const int64_t keep_below = a.n_before + a.need + 12;
+    const int64_t li0 = a.nloc + (int64_t)a.lbsum[blockIdx.x];
+    const int rw = a.kw + 1;
+    uint32_t stored = 0;
+    for (uint32_t i = threadIdx.x; i < ltot; i += TPB) {
+        const uint32_t inf = sinf[i];
+        const int64_t gid = g0 + (inf & 0xfffu);
+        const int64_t li = li0 + i;
+        if (gid >= keep_below) continue;
         if (li >= a.lcap) {
             atomicOr(&a.ctl->overflow, 2u);
             continue;
         }
         ++stored;
-        const uint32_t i = a.map[(uint32_t)p * 12u + act];
-        const uint64_t* rec = a.recv + (int64_t)i * (a.kw + 1);
-        for (int k = 0; k < a.kw; ++k) a.lkeys[li * a.kw + k] = rec[k];
         a.lgid[li] = gid;
-        a.lpar[li] = a.head + p;
-        a.lact[li] = (uint8_t)act;
-        const uint32_t si = a.rslot[i];
+        a.lpar[li] = a.head + (int64_t)blockIdx.x * TPB + (inf >> 16);
+        a.lact[li] = (uint8_t)((inf >> 12) & 0xfu);
+        const uint32_t r = srec[i];
+        const uint32_t si = a.rslot[r];
         a.table[si] = ((uint64_t)(li + 1) << 32) | (uint32_t)a.table[si];
     }
-    if (stored) atomicAdd(&a.ctl->stored, stored);
+    // keys: word w of the block's slot range comes from word w % kw of record srec[w / kw]
+    for (uint32_t w = threadIdx.x; w < ltot * (uint32_t)a.kw; w += TPB) {
+        const uint32_t i = w / (uint32_t)a.kw, c = w - i * (uint32_t)a.kw;
+        const int64_t li = li0 + i;
+        if (g0 + (sinf[i] & 0xfffu) >= keep_below || li >= a.lcap) continue;
+        a.lkeys[li * a.kw + c] = a.recv[(int64_t)srec[i] * rw + c];
+    }
+    uint32_t bs;
+    block_excl_scan(stored, sh, bs);
+    if (threadIdx.x == 0 && bs) atomicAdd(&a.ctl->stored, bs);
 }
 
 // min child total over the local parents of the chunk with p <= last
@@ -432,7 +524,7 @@ struct Shard {
 
     ~Shard() {
         void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.map,
-                        a.rslot, a.bsum, a.lbsum, a.table, a.ctl, a.look};
+                        a.rslot, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
@@ -451,7 +543,7 @@ struct ExpandLaunch {
     Shard* S;
     hipStream_t st;
     template <int NW>
-    void go() { sbfs_expand_kernel<NW><<<dim3(nblocks(S->Pr)), dim3(TPB), 0, st>>>(S->a); }
+    void go() { sbfs_expand_kernel<NW><<<dim3((unsigned)((S->Pr + STILE - 1) / STILE)), dim3(TPB), 0, st>>>(S->a); }
 };
 struct InsertLaunch {
     Shard* S;
@@ -518,6 +610,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
               dalloc(a.pmin, (size_t)pl) && dalloc(a.map, (size_t)S->rcap) && dalloc(a.rslot, (size_t)S->rcap) &&
               dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
+              dalloc(a.xblk, (size_t)((pl + STILE - 1) / STILE + 1) * (2 + world)) &&
               hipHostMalloc((void**)&S->ctl_host, sizeof(Ctl), hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void**)&S->look_host, 4 * sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
     if (!ok) {
@@ -597,6 +690,7 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream
     if (S->Pr > 0) {
         ExpandLaunch el{S, st};
         by_nw(S->L, el);
+        sbfs_expand_reduce_kernel<<<dim3(1), dim3(1024), 0, st>>>(a, (S->Pr + STILE - 1) / STILE);
     }
     const int r = sync_ctl(S, st);
     if (r != ACX_OK) return r;
