@@ -186,24 +186,40 @@ __global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
     for (int i = threadIdx.x; i < a.world; i += TPB) x[2 + i] = hist[i];
 }
 
+// exclusive scan over a 1024-thread block (sh: 16 words)
+__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t* sh, uint32_t& tot) {
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    if (lane == WAVE - 1) sh[wid] = x;
+    __syncthreads();
+    uint32_t off = 0;
+    tot = 0;
+#pragma unroll
+    for (int i = 0; i < 1024 / WAVE; ++i) {
+        off += i < wid ? sh[i] : 0u;
+        tot += sh[i];
+    }
+    return off + x - v;
+}
+
 // (1b) the expand blocks' records -> the chunk's min child total, local parent count and
-// children per owner (one block)
+// children per owner (one block); each block's per-owner count is replaced by its exclusive
+// prefix over the blocks, and ctl->cur[o] set to owner o's first send slot, so pack places
+// every record without a global atomic
 __global__ __launch_bounds__(1024) void sbfs_expand_reduce_kernel(Args a, int nblk) {
-    __shared__ uint32_t cnt[MAXW];
     __shared__ uint32_t red[2][1024 / WAVE];
+    __shared__ uint32_t tot[MAXW];
     const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
     const int rw = 2 + a.world;
-    for (int i = t; i < a.world; i += 1024) cnt[i] = 0;
-    __syncthreads();
     uint32_t mn = NONE, np = 0;
     for (int b = t; b < nblk; b += 1024) {
         mn = min(mn, a.xblk[(size_t)b * rw]);
         np = max(np, a.xblk[(size_t)b * rw + 1]);
-    }
-    for (int64_t i = t; i < (int64_t)nblk * a.world; i += 1024) {
-        const int b = (int)(i / a.world), o = (int)(i - (int64_t)b * a.world);
-        const uint32_t v = a.xblk[(size_t)b * rw + 2 + o];
-        if (v) atomicAdd(&cnt[o], v);
     }
     mn = wave_min(mn);
 #pragma unroll
@@ -221,56 +237,64 @@ __global__ __launch_bounds__(1024) void sbfs_expand_reduce_kernel(Args a, int nb
         if (mn != NONE) a.ctl->min_len = min(a.ctl->min_len, mn);
         a.ctl->npar = np;
     }
-    for (int i = t; i < a.world; i += 1024) a.ctl->cnt[i] = cnt[i];
+    // per owner: thread t scans blocks [b0, b1) of a contiguous split
+    const int per = (nblk + 1023) / 1024;
+    const int b0 = min(nblk, t * per), b1 = min(nblk, b0 + per);
+    for (int o = 0; o < a.world; ++o) {
+        uint32_t loc = 0;
+        for (int b = b0; b < b1; ++b) loc += a.xblk[(size_t)b * rw + 2 + o];
+        __syncthreads();  // red reuse
+        uint32_t total;
+        uint32_t run = block_excl_scan_1024(loc, &red[0][0], total);
+        for (int b = b0; b < b1; ++b) {
+            uint32_t* x = a.xblk + (size_t)b * rw + 2 + o;
+            const uint32_t c = *x;
+            *x = run;
+            run += c;
+        }
+        if (t == 0) tot[o] = total;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int o = 0; o < a.world; ++o) {
+            a.ctl->cnt[o] = tot[o];
+            a.ctl->cur[o] = run;
+            run += tot[o];
+        }
+    }
 }
 
 // (2) records into the send buffer, grouped by owner (order within a group is arbitrary:
-// the owner indexes records by seq).  Positions are wave-aggregated: per (action, owner) a
-// ballot ranks the lanes and lane 0 reserves the wave's run with one LDS add (broadcast by shfl).
+// the owner indexes records by seq).  Same tiling as the expansion (block per 64 local parents,
+// wave w: actions 3w..3w+2): the block's run for owner o starts at cur[o] + its prefix (1b);
+// inside the block, per (action, owner) a ballot ranks the lanes and lane 0 reserves the wave's
+// run with one LDS add.
 __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
-    __shared__ uint32_t hist[MAXW], base[MAXW], off[MAXW];
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int i = 0; i < a.world; ++i) {
-            off[i] = run;
-            run += a.ctl->cnt[i];
-        }
-    }
+    __shared__ uint32_t hist[MAXW];
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     for (int i = threadIdx.x; i < a.world; i += TPB) hist[i] = 0;
     __syncthreads();
-    const int j = blockIdx.x * TPB + threadIdx.x;
-    const int lane = threadIdx.x & (WAVE - 1);
+    const int j = blockIdx.x * STILE + lane;
     const uint64_t below = (1ull << lane) - 1ull;
-    uint8_t own[12];
-    uint32_t loc[12];
-#pragma unroll
-    for (int act = 0; act < 12; ++act) {
-        own[act] = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : (uint8_t)0xff;
-        loc[act] = 0;
-    }
-    // each (action, owner) run of the wave gets a block-local offset in hist[owner]
-    for (int o = 0; o < a.world; ++o) {
-#pragma unroll
-        for (int act = 0; act < 12; ++act) {
-            const uint64_t m = __ballot(own[act] == o);
-            if (!m) continue;
-            uint32_t b = lane == 0 ? atomicAdd(&hist[o], (uint32_t)__popcll(m)) : 0u;
-            b = (uint32_t)__shfl((int)b, 0, WAVE);
-            if (own[act] == o) loc[act] = b + (uint32_t)__popcll(m & below);
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.world; i += TPB) base[i] = hist[i] ? atomicAdd(&a.ctl->cur[i], hist[i]) : 0u;
-    __syncthreads();
-    if (j >= a.Pr || own[0] == 0xff) return;
-    const uint32_t p = (uint32_t)(a.lgid[a.lo + j] - a.head);
+    const uint32_t* x = a.xblk + (size_t)blockIdx.x * (2 + a.world) + 2;
+    const uint32_t p = j < a.Pr ? (uint32_t)(a.lgid[a.lo + j] - a.head) : 0u;
     const int rw = a.kw + 1;
-#pragma unroll
-    for (int act = 0; act < 12; ++act) {
-        const int o = own[act];
-        const int64_t pos = (int64_t)off[o] + base[o] + loc[act];
+#pragma unroll 1
+    for (int jj = 0; jj < SAPW; ++jj) {
+        const int act = wid * SAPW + jj;
+        const uint32_t o = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : 0xffu;
+        uint32_t pos = 0;
+        for (uint32_t w = 0; w < (uint32_t)a.world; ++w) {
+            const uint64_t m = __ballot(o == w);
+            if (!m) continue;
+            uint32_t b = lane == 0 ? atomicAdd(&hist[w], (uint32_t)__popcll(m)) : 0u;  // LDS
+            b = (uint32_t)__shfl((int)b, 0, WAVE);
+            if (o == w) pos = a.ctl->cur[w] + x[w] + b + (uint32_t)__popcll(m & below);
+        }
+        if (o == 0xffu) continue;
         const uint64_t* src = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
-        uint64_t* dst = a.send + pos * rw;
+        uint64_t* dst = a.send + (int64_t)pos * rw;
         for (int k = 0; k < a.kw; ++k) dst[k] = src[k];
         dst[a.kw] = (uint64_t)(p * 12u + (uint32_t)act);
     }
@@ -710,7 +734,7 @@ int acx_sbfs_pack(void* h, uint64_t* send, void* stream) {
     if (!S || !send) return ACX_E_ARG;
     if (S->Pr == 0) return ACX_OK;
     S->a.send = send;
-    sbfs_pack_kernel<<<dim3(nblocks(S->Pr)), dim3(TPB), 0, (hipStream_t)stream>>>(S->a);
+    sbfs_pack_kernel<<<dim3((unsigned)((S->Pr + STILE - 1) / STILE)), dim3(TPB), 0, (hipStream_t)stream>>>(S->a);
     return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 

@@ -171,3 +171,39 @@ def test_greedy_device_engine_aged_caches():
     assert st["stop_aged"] > 0
     assert [bool(ok), [list(x) for x in path]] == [c["ok"], c["path"]]
     _check_order(unpack_keys_np(st["node_keys"][st["popped"]], c["L"]), c)
+
+
+with open(os.path.join(GOLDEN, "search_scale_1e7.json")) as _f:
+    CONFIG4 = json.load(_f)[0]
+
+
+@pytest.mark.parametrize("engine", ["device", "sharded"])
+def test_config4_full_frontier_matches_reference(engine, capsys):
+    """BASELINE configs[3] at its full size, pinned to the reference itself: the reference bfs
+    from AK(3), L = 36, to 10^7 nodes (make_golden.py --search-scale-1e7: 1,589,594 parents
+    expanded, every parent state in the rolling sha256) against the device BFS and the
+    owner-partitioned BFS at one rank -- same printed budget message, result, parent count and
+    parent order."""
+    c = CONFIG4
+    assert c["budget"] == 10 ** 7 and c["L"] == 36 and c["parents"] == 1589594
+    if engine == "device":
+        from acx.search import _device_bfs as D
+        res = D.device_bfs(np.array(c["presentation"]), c["budget"], verbose=True,
+                           cyclically_reduce_after_moves=c["cyclical"], device=DEV, keep_node_keys=True)
+        st = D.LAST_STATS
+        keys = st["node_keys"][: c["parents"]]
+        D.release_workspaces()
+    else:
+        from acx.search import _sharded_bfs as SB
+        res = SB.sharded_bfs(np.array(c["presentation"]), c["budget"], cyclically_reduce_after_moves=c["cyclical"],
+                             device=DEV, keep_node_keys=True)
+        st = SB.LAST_STATS
+        order = np.argsort(st["node_ids"], kind="stable")
+        keys = st["node_keys"][order][: c["parents"]]
+        SB.release_workspaces()
+    out = capsys.readouterr().out.splitlines()
+    # the sharded search prints the budget message but not the verbose new-minimum lines
+    assert out == (c["stdout"] if engine == "device" else [ln for ln in c["stdout"] if ln.startswith("Exiting")])
+    assert _result(*res) == [c["ok"], c["path"]]
+    assert st["parents"] == c["parents"]
+    _check_order(unpack_keys_np(keys, c["L"]), c)
