@@ -89,6 +89,7 @@ SIGNATURES = {
     "acx_sbfs_commit": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),
     "acx_sbfs_min_len": ([_P, _I64, _P], ctypes.c_int64),
     "acx_sbfs_lookup": ([_P, _I64, _P, _P], ctypes.c_int),
+    "acx_sbfs_trace": ([_P, _I64, _I64, _P, _I64, _P], ctypes.c_int64),
     "acx_sbfs_node_keys": ([_P, _P, _P, _I64], ctypes.c_int64),
 }
 

@@ -114,6 +114,30 @@ def local_capacity(max_nodes: int, world: int) -> int:
     return min(n, (n + world - 1) // world * 5 // 4 + 4096)
 
 
+TRACE_CAP = 512  # (seq, total) records per rank per chunk (acx_sbfs_trace; <= 2L + 1 in practice)
+
+
+def _trace_chunk(lib, h, comm, buf, running, end_seq, stream, ok, agree, lines):
+    """The verbose new-minimum lines of the last chunk (breadth_first.py:79-82): every rank reports
+    its prefix minima among the chunk's children before end_seq; merged in sequence order they
+    give the reference's sequence.  Returns the running minimum after the chunk."""
+    n_raw = int(lib.acx_sbfs_trace(h, int(running), int(end_seq), buf.ctypes.data, TRACE_CAP, stream))
+    ok(n_raw, "acx_sbfs_trace")
+    n = min(max(n_raw, 0), TRACE_CAP)
+    row = np.zeros(2 + 2 * TRACE_CAP, np.int64)
+    row[0] = n
+    row[1] = n_raw < 0 or n_raw > TRACE_CAP  # agreed on by every rank through the gathered rows
+    row[2: 2 + 2 * n] = buf[: 2 * n]
+    rows = comm.all_gather_rows(row)
+    agree(int(rows[:, 1].sum()), "acx_sbfs_trace (or more than TRACE_CAP records)")
+    recs = sorted((int(r[2 + 2 * i]), int(r[3 + 2 * i])) for r in rows for i in range(int(r[0])))
+    for _, tot in recs:
+        if tot < running:
+            running = tot
+            lines.append(tot)
+    return running
+
+
 def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
                 device=None, chunk=0, group=None, keep_node_keys=False):
     """(True, path) | (False, None), as breadth_first.py:15-97; SPMD over the ranks of `group`
@@ -153,6 +177,9 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     W = comm.world
     exp_out = np.zeros(6 + W, np.int64)  # acx_sbfs_expand's 5 + W values, then this rank's failure flag
     com_out = np.zeros(5, np.int64)
+    trace_buf = np.zeros(2 * TRACE_CAP, np.int64)
+    trace_min = total0  # breadth_first.py:59,79-82: the running minimum the verbose lines follow
+    trace_lines = []
     failed = []  # (call, status) of failed C calls on this rank
 
     def ok(st, what):
@@ -203,6 +230,13 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
             suc_p = succ_seq // 12 if succ_seq != NONE else None
             err_first = err_p is not None and err_seq < succ_seq and (cut is None or err_p <= cut)
             succ_first = not err_first and suc_p is not None and (cut is None or suc_p <= cut)
+            if verbose and chunk_min < trace_min:
+                # the chunk's children the reference visits: up to (not incl.) the raising one, incl.
+                # the successful one, through the cut parent, or all of them
+                end_seq = (err_seq if err_first else succ_seq + 1 if succ_first else
+                           12 * (cut + 1) if cut is not None else 12 * P)
+                trace_min = _trace_chunk(lib, h, comm, trace_buf, trace_min, end_seq, stream, ok, agree,
+                                         trace_lines)
             if err_first or succ_first or cut is not None:
                 last = err_p if err_first else suc_p if succ_first else cut
                 if succ_first:
@@ -251,10 +285,12 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
         if n > 0:
             lib.acx_sbfs_node_keys(h, nk.ctypes.data, ng.ctypes.data, n)
         LAST_STATS["node_keys"], LAST_STATS["node_ids"] = nk, ng
+    LAST_STATS["min_trace"] = list(trace_lines)
+    if verbose and comm.rank == 0:
+        for v in trace_lines:  # breadth_first.py:79-82 (printed before a raising move, as there)
+            print(f"New minimal length found: {v}")
     if status == _lib.BFS_MOVE_ERROR:
         raise AssertionError("bfs: a move produced an invalid presentation (utils.py:264-266)")
-    if verbose and comm.rank == 0:
-        print(f"Minimal total length found: {min_len}")
     if status == _lib.BFS_BUDGET and comm.rank == 0:
         print(f"Exiting search as number of explored nodes = {n_nodes} has exceeded the limit "
               f"{max_nodes_to_explore}")

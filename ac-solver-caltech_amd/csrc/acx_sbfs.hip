@@ -505,6 +505,83 @@ __global__ __launch_bounds__(TPB) void sbfs_minlen_kernel(Args a, int64_t last) 
     if (threadIdx.x == 0 && v != NONE) atomicMin(&a.ctl->min_len, v);
 }
 
+// the total length stored in a packed child key (n0 at bit 4L, n1 at bit 4L + 8)
+__device__ __forceinline__ uint32_t key_total(const uint64_t* k, int L) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int bit = 4 * L + 8 * h, w = bit >> 6, o = bit & 63;
+        uint64_t v = k[w] >> o;
+        if (o > 56) v |= k[w + 1] << (64 - o);
+        t += (uint32_t)(v & 0xffu);
+    }
+    return t;
+}
+
+// verbose trace (breadth_first.py:79-82): this rank's chunk children with seq < end whose total
+// is below every earlier child of this rank and below `running` -- the rank's prefix minima, a
+// superset of the global new minima that lie on this rank (<= 2L of them).  One block: a min
+// scan over contiguous parent ranges (pmin, or the children below `end` for the boundary
+// parent), then every range whose running min drops walks its parents' children in order.
+constexpr int TRACE_MAX = 512;
+__global__ __launch_bounds__(1024) void sbfs_trace_kernel(Args a, int npar, uint32_t running, uint32_t end,
+                                                          int64_t* out, int32_t* n_out) {
+    __shared__ uint32_t red[1024 / WAVE];
+    __shared__ uint32_t cnt;
+    const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
+    if (t == 0) cnt = 0;
+    const int per = (npar + 1023) / 1024;
+    const int j0 = min(npar, t * per), j1 = min(npar, j0 + per);
+    auto child_total = [&](int j, int act) -> uint32_t {
+        return key_total(a.ckeys + ((int64_t)act * a.Pr + j) * a.kw, a.L);
+    };
+    auto parent_seq = [&](int j) -> uint32_t { return (uint32_t)(a.lgid[a.lo + j] - a.head) * 12u; };
+    uint32_t mn = NONE;
+    for (int j = j0; j < j1; ++j) {
+        const uint32_t s0 = parent_seq(j);
+        if (s0 >= end) break;
+        if (s0 + 12u <= end) {
+            mn = min(mn, (uint32_t)a.pmin[j]);
+        } else {
+            for (int act = 0; s0 + act < end; ++act) mn = min(mn, child_total(j, act));
+        }
+    }
+    // exclusive prefix min over the threads' ranges (in parent order = seq order)
+    uint32_t x = mn;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, WAVE);
+        if (lane >= o) x = min(x, y);
+    }
+    if (lane == WAVE - 1) red[wid] = x;
+    __syncthreads();
+    uint32_t before = running;
+    for (int i = 0; i < wid; ++i) before = min(before, red[i]);
+    const uint32_t xe = (uint32_t)__shfl_up((int)x, 1, WAVE);
+    if (lane > 0) before = min(before, xe);
+    if (mn < before) {  // this range holds prefix minima: walk it in order
+        uint32_t run = before;
+        for (int j = j0; j < j1; ++j) {
+            const uint32_t s0 = parent_seq(j);
+            if (s0 >= end) break;
+            if (s0 + 12u <= end && (uint32_t)a.pmin[j] >= run) continue;
+            for (int act = 0; act < 12 && s0 + act < end; ++act) {
+                const uint32_t tt = child_total(j, act);
+                if (tt < run) {
+                    run = tt;
+                    const uint32_t k = atomicAdd(&cnt, 1u);  // LDS
+                    if (k < TRACE_MAX) {
+                        out[2 * k] = (int64_t)(s0 + act);
+                        out[2 * k + 1] = (int64_t)tt;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) *n_out = (int32_t)cnt;
+}
+
 // the stored node with global id g: found, parent id, action, total length
 template <int NW>
 __global__ void sbfs_lookup_kernel(Args a, int64_t g) {
@@ -805,6 +882,41 @@ int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream) {
     const int r = sync_ctl(S, st);
     if (r != ACX_OK) return r;
     return S->ctl_host->min_len == NONE ? 255 : (int64_t)S->ctl_host->min_len;
+}
+
+// verbose trace of the last chunk (call after acx_sbfs_commit): this rank's children with seq <
+// end whose total is below `running` and below every earlier child of this rank, as (seq, total)
+// int64 pairs into out (HOST, 2 * cap); returns their count (<= 2L + 1 in practice)
+int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int64_t cap, void* stream) {
+    Shard* S = static_cast<Shard*>(h);
+    if (!S || !out || cap < 0) return ACX_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    Args a = S->a;
+    const int npar = (int)S->ctl_host->npar;
+    a.lo = S->lo - npar;  // commit advanced lo past the chunk's local parents
+    if (npar == 0) return 0;
+    int64_t* d_out = nullptr;
+    int32_t* d_n = nullptr;
+    if (hipMalloc((void**)&d_out, 2 * TRACE_MAX * sizeof(int64_t)) != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMalloc((void**)&d_n, sizeof(int32_t)) != hipSuccess) {
+        (void)hipFree(d_out);
+        return ACX_E_LAUNCH;
+    }
+    const uint32_t run = running < 0 ? 0u : running > (int64_t)NONE ? NONE : (uint32_t)running;
+    const uint32_t e = end < 0 ? 0u : end > (int64_t)NONE ? NONE : (uint32_t)end;
+    sbfs_trace_kernel<<<dim3(1), dim3(1024), 0, st>>>(a, npar, run, e, d_out, d_n);
+    int32_t n = 0;
+    int64_t res = ACX_E_LAUNCH;
+    if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&n, d_n, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipStreamSynchronize(st) == hipSuccess) {
+        const int64_t m = n < cap ? n : cap;
+        const int64_t mm = m < TRACE_MAX ? m : TRACE_MAX;
+        if (mm == 0 || hipMemcpy(out, d_out, (size_t)(2 * mm) * sizeof(int64_t), hipMemcpyDeviceToHost) == hipSuccess)
+            res = n;
+    }
+    (void)hipFree(d_out);
+    (void)hipFree(d_n);
+    return res;
 }
 
 // node with global id g if this rank stores it: out (int64[4]) = found, parent id, action, total

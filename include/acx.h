@@ -305,6 +305,11 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
 int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t need, int64_t* out, void* stream);
 int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream);
 int acx_sbfs_lookup(void* h, int64_t g, int64_t* out, void* stream);
+/* verbose trace of the last chunk (after acx_sbfs_commit; breadth_first.py:79-82): this rank's
+ * children with seq < end whose total is below `running` and below every earlier child of this
+ * rank, as (seq, total) int64 pairs into out (HOST, 2 * cap); returns their count.  The caller
+ * merges every rank's records in seq order to print the reference's new-minimum lines. */
+int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int64_t cap, void* stream);
 int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap);
 
 /*

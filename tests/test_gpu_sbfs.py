@@ -23,6 +23,13 @@ def _ak3(L):
     return convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], L)
 
 
+def _ms17():
+    """The Miller-Schupp start of tests/golden/search_scale.json's non-AK(3) cases (L = 36)."""
+    with open(os.path.join(GOLDEN, "search_scale.json")) as f:
+        return next(c["presentation"] for c in json.load(f)
+                    if c["L"] == 36 and c["presentation"] != _ak3(36).tolist())
+
+
 def _extra_cases(n=None):
     with open(os.path.join(GOLDEN, "kat_search_extra.json")) as f:
         cases = [c for c in json.load(f) if c["search_fn"] == "bfs"]
@@ -108,9 +115,10 @@ def _worker(rank, world, port, jobs, q):
         from acx.search import _sharded_bfs as S
         out = {}
         for name, (pres, budget, cyc, chunk) in jobs["orders"].items():
-            r = S.sharded_bfs(np.array(pres), budget, cyclically_reduce_after_moves=cyc, device=DEV, chunk=chunk,
-                              keep_node_keys=True)
-            out[name] = (r, S.LAST_STATS["nodes"], S.LAST_STATS["node_ids"], S.LAST_STATS["node_keys"])
+            r = S.sharded_bfs(np.array(pres), budget, verbose=True, cyclically_reduce_after_moves=cyc, device=DEV,
+                              chunk=chunk, keep_node_keys=True)
+            out[name] = (r, S.LAST_STATS["nodes"], S.LAST_STATS["node_ids"], S.LAST_STATS["node_keys"],
+                         S.LAST_STATS["min_trace"])
         out["cases"] = _run_cases(jobs["cases"], jobs["case_chunk"], _sbfs)
         q.put((rank, out))
     except Exception as e:  # report instead of hanging the other ranks' queue reads
@@ -128,7 +136,9 @@ def test_sharded_bfs_multi_rank(world):
     orders = {"ak3_36": (_ak3(36).tolist(), 150_000, False, 4096),
               "ak3_36_cyc": (_ak3(36).tolist(), 60_000, True, 777),
               "ak3_128": (_ak3(128).tolist(), 30_000, False, 0),
-              "ak2": ([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0], 10 ** 6, False, 64)}
+              "ak2": ([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0], 10 ** 6, False, 64),
+              # a start whose search finds new minima (the verbose trace crosses the ranks)
+              "ms17": (_ms17(), 60_000, False, 3000)}
     cases = _extra_cases(40)
     jobs = {"orders": orders, "cases": cases, "case_chunk": 3}
     ctx = mp.get_context("spawn")
@@ -149,6 +159,8 @@ def test_sharded_bfs_multi_rank(world):
         ref = D.device_bfs(np.array(pres), budget, cyclically_reduce_after_moves=cyc, device=DEV, chunk=chunk,
                            keep_node_keys=True)
         nd = D.LAST_STATS["nodes"]
+        for r in range(world):  # the verbose new-minimum sequence, merged over the ranks
+            assert res[r][name][4] == D.LAST_STATS["min_trace"], name
         dk = D.LAST_STATS["node_keys"]
         ids = np.concatenate([res[r][name][2] for r in range(world)])
         keys = np.concatenate([res[r][name][3] for r in range(world)])
