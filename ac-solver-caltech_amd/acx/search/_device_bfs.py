@@ -44,7 +44,7 @@ def release_workspaces() -> None:
 def device_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
                device=None, chunk=0, keep_node_keys=False):
     """(True, path) | (False, None), as breadth_first.py:15-97.  chunk = parents per kernel
-    round (0: up to 2^19).  keep_node_keys: LAST_STATS["node_keys"] = the packed keys of all
+    round (0: up to 2^20).  keep_node_keys: LAST_STATS["node_keys"] = the packed keys of all
     discovered nodes in discovery (FIFO) order."""
     p = np.asarray(presentation)
     assert is_array_valid_presentation(p), f"{p} is not a valid presentation"

@@ -535,7 +535,7 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     S->cyc = cyclical != 0;
     S->max_nodes = max_nodes;
     S->qcap = max_nodes + 12;
-    if (chunk_parents <= 0) chunk_parents = 1 << 19;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
+    if (chunk_parents <= 0) chunk_parents = 1 << 20;  // tools/bfs_chunk_probe.py (r02ak): 2^20 fastest at 10^7 / 10^8 nodes
     S->pmax = chunk_parents < S->qcap ? chunk_parents : S->qcap;
     S->tiles_max = S->pmax / TILE + 2;
     // every parent that can be expanded (< qcap) has its 12 child slots; one spare tile

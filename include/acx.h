@@ -237,7 +237,7 @@ int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out,
  * with identical results): FIFO queue of packed node keys and the visited set (open-addressing
  * hash table) in HBM; the 12-way expansion, dedup against the visited set and within the chunk
  * (first occurrence in (parent, action) order wins), the success test and the per-parent node
- * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^19).
+ * budget run as kernels over chunks of up to `chunk_parents` parents (<= 0: 2^20).
  *   acx_bfs_create   allocates the device workspace on the current device for searches of
  *                    up to max_nodes nodes (<= 2^30) at max_relator_length L; NULL on failure
  *                    (every child key of every expanded parent is kept: ~12 * 8 * kw bytes

@@ -1,3 +1,7 @@
+"""Device BFS wall time on AK(3), L = 36, at several chunk sizes (parents per round of kernels),
+10^7 and 10^8 nodes, best of 3 after a warmup: what sets acx_bfs_create's default chunk.
+
+    python tools/bfs_chunk_probe.py"""
 import sys, time, json, torch, contextlib, io
 sys.path.insert(0, "ac-solver-caltech_amd")
 from acx.envs.utils import convert_relators_to_presentation
