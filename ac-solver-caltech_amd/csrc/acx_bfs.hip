@@ -108,7 +108,7 @@ struct Args {
 // chunk is only ~8 waves per SIMD that way); keys staged through LDS, written coalesced
 constexpr int APW = 12 / (TPB / WAVE);  // actions per wave (3)
 template <int NW>
-__global__ __launch_bounds__(TPB) void bfs_expand_kernel(Args a) {
+__global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void bfs_expand_kernel(Args a) {
     __shared__ uint64_t kst[TPB / WAVE][TILE * (NW + 1)];
     __shared__ uint32_t smin[TILE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
@@ -190,7 +190,7 @@ __device__ __forceinline__ int64_t local_pos(const Args& a, uint64_t c) {
 
 // (2) lane per child: probe the visited set; claim an empty slot or join the state's entry
 template <int KWM>
-__global__ __launch_bounds__(TPB) void bfs_insert_kernel(Args a) {
+__global__ __launch_bounds__(TPB, 8) void bfs_insert_kernel(Args a) {  // 8 waves/SIMD: latency-bound, SGPRs capped at 96
     const int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (c >= (int64_t)a.ntiles * TILE_CH) return;
     const int t = (int)(c / TILE_CH);

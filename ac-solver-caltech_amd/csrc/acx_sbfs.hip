@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
 constexpr int STILE = 64;
 constexpr int SAPW = 12 / (TPB / WAVE);  // actions per wave (3)
 template <int NW>
-__global__ __launch_bounds__(TPB) void sbfs_expand_kernel(Args a) {
+__global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void sbfs_expand_kernel(Args a) {
     __shared__ uint64_t kst[TPB / WAVE][STILE * (NW + 1)];
     __shared__ uint32_t hist[MAXW];
     __shared__ uint32_t smin[STILE];
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(TPB) void sbfs_map_kernel(Args a) {
 
 // (3b) probe / claim / join, one lane per received child (acx_bfs.hip bfs_insert_kernel)
 template <int KWM>
-__global__ __launch_bounds__(TPB) void sbfs_insert_kernel(Args a) {
+__global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 waves/SIMD (latency-bound)
     const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (i >= a.nrecv) return;
     const int rw = a.kw + 1;
