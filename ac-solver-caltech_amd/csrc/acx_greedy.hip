@@ -714,7 +714,7 @@ int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, in
 void acx_greedy_destroy(void* h) { delete static_cast<Engine*>(h); }
 
 // tests only (not in acx.h): searches started afterwards use 2^log2_age as the cache age limit
-// (0: the default 2^20), so the re-expansion of aged caches is exercised at test sizes
+// (0: the default AGE), so the retirement of aged caches is exercised harder at test sizes
 void acx_internal_greedy_age(int32_t log2_age) { g_age_override = log2_age > 0 ? (int64_t)1 << log2_age : 0; }
 
 // 0 running, 1 success, 2 failed, 3 move error; budget_hit, min_length, nodes (len(tree_nodes))
