@@ -360,6 +360,25 @@ __global__ __launch_bounds__(TPB) void bfs_commit_kernel(Args a) {
         if (n0 + i < a.qcap) a.queue[n0 + i] = st[i];
 }
 
+// the chunk's control block to its initial values (a kernel, so the reset is asynchronous on
+// the stream: a host-to-device copy from pageable memory blocks the host for its duration)
+__global__ void bfs_ctl_reset_kernel(Ctl* c) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Ctl z;
+    memset(&z, 0, sizeof(z));
+    z.succ = z.err = z.cut_p = z.min_len = NONE;
+    *c = z;
+}
+
+// wait for the stream by polling (hipStreamSynchronize may sleep and wake late: one wait per
+// chunk is on the search's critical path)
+static int stream_wait(hipStream_t st) {
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+}
+
 // root: node 0 (code 1) and its table entry
 template <int KWM>
 __global__ void bfs_root_kernel(Args a) {
@@ -594,9 +613,6 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     int64_t min_len = total0, path_len = 0;
     int status = ACX_BFS_EXHAUSTED;
     int64_t succ_node = -1, succ_act = -1;
-    Ctl init;
-    memset(&init, 0, sizeof(init));
-    init.succ = init.err = init.cut_p = init.min_len = NONE;
     while (head < n_nodes) {
         const int64_t avail = n_nodes - head;
         const int P = (int)(avail < S->pmax ? avail : S->pmax);
@@ -606,13 +622,13 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
         a.ntiles = (int)((head + P - 1) / TILE - a.tile0 + 1);
         a.n_before = n_nodes;
         a.need = max_nodes - n_nodes;
-        if (hipMemcpyAsync(a.ctl, &init, sizeof(Ctl), hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+        bfs_ctl_reset_kernel<<<dim3(1), dim3(64), 0, st>>>(a.ctl);
         ChunkLaunch cl{S, st};
         by_nw(L, cl);
         if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
         if (hipMemcpyAsync(S->ctl_host, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess)
             return ACX_E_LAUNCH;
-        if (hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+        if (stream_wait(st) != ACX_OK) return ACX_E_LAUNCH;
         const Ctl c = *S->ctl_host;
         ++chunks;
         if (c.overflow) return ACX_E_LAUNCH;

@@ -670,8 +670,12 @@ static int sync_ctl(Shard* S, hipStream_t st) {
     if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
     if (hipMemcpyAsync(S->ctl_host, S->a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess)
         return ACX_E_LAUNCH;
-    if (hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
-    return ACX_OK;
+    // poll: hipStreamSynchronize may sleep and wake late, and two waits per chunk are on the
+    // search's critical path
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 
 }  // namespace sbfs
