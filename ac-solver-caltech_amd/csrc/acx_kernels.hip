@@ -158,9 +158,10 @@ struct FastTile {
 
     uint32_t* lds;
     uint8_t* flags;
+    uint8_t* dirty;         // per row: bit h = relator h differs from the loaded row (store_dirty)
     bool tile_bad = false;  // wave-uniform: some row of the last load was flagged
 
-    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
     // per-row out-of-domain flags as of the tile's FIRST load (a later load of other rows
     // replaced them); the fallback rows of store<true> follow these
     __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
@@ -176,6 +177,7 @@ struct FastTile {
     __device__ __forceinline__ FastTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
+        dirty = flags + WAVE;
     }
     __device__ __forceinline__ int Lr() const { return L; }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(lds + r * S); }
@@ -390,6 +392,67 @@ struct FastTile {
         asm volatile("" : "+v"(ln));
         uint32_t* dst = lds + ln * S;
         uint32_t d[CPR];
+        image(p, d);
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
+    }
+
+    // unpack, and return which relators differ from the row it overwrites (bit h = relator h):
+    // the int8 image is canonical (zero letters past the length), so equal relators compare equal
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        uint32_t d[CPR];
+        image(p, d);
+        uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) {
+            const uint2 o = *reinterpret_cast<const uint2*>(dst + k);
+            if (k < HALF) x0 |= o.x ^ d[k];
+            else x1 |= o.x ^ d[k];
+            if (k + 1 < HALF) x0 |= o.y ^ d[k + 1];
+            else x1 |= o.y ^ d[k + 1];
+            *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
+        }
+        return (x0 != 0u ? 1u : 0u) | (x1 != 0u ? 2u : 0u);
+    }
+
+    __device__ __forceinline__ void set_dirty(int lane, uint32_t m) const { dirty[lane] = (uint8_t)m; }
+
+    // In-place state store (g is the row block the tile was loaded from): only the 16-byte
+    // chunks of relators marked in dirty[] are written; every other chunk already holds its
+    // value in HBM (a gated move, an unchanged relator, a failed env).  Needs set_dirty for every
+    // row of the tile and a wave_sync after it.
+    template <bool NT>
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        int4* dst = reinterpret_cast<int4*>(g);
+#pragma unroll
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+            bool wr[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                wr[u] = false;
+                const int c = ln + (u0 + u) * WAVE;
+                if (u0 + u < CPR && c < nc) {
+                    const int r = c / CPR;
+                    const int k = c - r * CPR;
+                    wr[u] = (dirty[r] >> (k >= HALF ? 1 : 0)) & 1u;
+                    if (wr[u]) p[u] = lds[r * S + k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u)
+                if (wr[u]) out16<NT, false>(dst + ln + (u0 + u) * WAVE, widen4(p[u]));
+        }
+    }
+
+  private:
+    __device__ __forceinline__ static void image(const PresRegs<NW>& p, uint32_t (&d)[CPR]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const Word<NW>& w = h ? p.w1 : p.w0;
@@ -399,8 +462,6 @@ struct FastTile {
             for (int k = 0; k < HALF; ++k)
                 d[h * HALF + k] = codes_to_i8x4((w.w[k >> 2] >> (8 * (k & 3))) & 0xffu, clamp_bits(n8 - 32 * k));
         }
-#pragma unroll
-        for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
     }
 };
 
@@ -423,9 +484,10 @@ struct CodeTile {
 
     uint32_t* lds;
     uint8_t* flags;
+    uint8_t* dirty;  // see FastTile
     bool tile_bad = false;
 
-    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + WAVE; }
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
     __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
         flags[lane] = flagged;
         tile_bad = __any(flagged);
@@ -438,6 +500,7 @@ struct CodeTile {
     __device__ __forceinline__ CodeTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
+        dirty = flags + WAVE;
     }
     __device__ __forceinline__ int Lr() const { return L; }
     __device__ __forceinline__ uint16_t* slots(int r) const { return reinterpret_cast<uint16_t*>(lds + r * S); }
@@ -592,10 +655,52 @@ struct CodeTile {
         return bad;
     }
 
-    __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const {
+    __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const { unpack_impl<false>(lane, p); }
+    // see FastTile::unpack_dirty; the slots compared are canonical (codes of absent letters
+    // masked to 0, as load writes them)
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
+        return unpack_impl<true>(lane, p);
+    }
+    __device__ __forceinline__ void set_dirty(int lane, uint32_t m) const { dirty[lane] = (uint8_t)m; }
+
+    // see FastTile::store_dirty
+    template <bool NT>
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        int4* dst = reinterpret_cast<int4*>(g);
+        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+            uint32_t p[STAGE_UNROLL];
+            bool wr[STAGE_UNROLL];
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                wr[u] = false;
+                const int c = ln + (u0 + u) * WAVE;
+                if (c < nc) {
+                    const int r = c / CPR;
+                    const int k = c - r * CPR;
+                    wr[u] = (dirty[r] >> (k >= HALF ? 1 : 0)) & 1u;
+                    if (wr[u]) p[u] = slots(r)[k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                if (!wr[u]) continue;
+                const uint32_t nz4 = (p[u] >> 8) & 0xfu;
+                out16<NT, false>(dst + ln + (u0 + u) * WAVE,
+                                 widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
+            }
+        }
+    }
+
+  private:
+    template <bool CMP>
+    __device__ __forceinline__ uint32_t unpack_impl(int lane, const PresRegs<NW>& p) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         uint32_t* dst = lds + ln * S;
+        uint32_t x[2] = {0u, 0u};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const Word<NW>& w = h ? p.w1 : p.w0;
@@ -608,13 +713,20 @@ struct CodeTile {
                     const int kk = k + j;
                     const int nin = n - 4 * kk;
                     const uint32_t nz4 = nin >= 4 ? 0xfu : (nin <= 0 ? 0u : ((1u << nin) - 1u));
-                    const uint32_t c8 = (w.w[kk >> 2] >> (8 * (kk & 3))) & 0xffu;
+                    uint32_t c8 = (w.w[kk >> 2] >> (8 * (kk & 3))) & 0xffu;
+                    if constexpr (CMP) c8 &= nin >= 4 ? 0xffu : (nin <= 0 ? 0u : ((1u << (2 * nin)) - 1u));
                     sl[j] = c8 | (nz4 << 8);
                 }
-                *reinterpret_cast<uint2*>(dst + (h * HALF + k) / 2) =
-                    make_uint2(sl[0] | (sl[1] << 16), sl[2] | (sl[3] << 16));
+                uint2* q = reinterpret_cast<uint2*>(dst + (h * HALF + k) / 2);
+                const uint2 v = make_uint2(sl[0] | (sl[1] << 16), sl[2] | (sl[3] << 16));
+                if constexpr (CMP) {
+                    const uint2 o = *q;
+                    x[h] |= (o.x ^ v.x) | (o.y ^ v.y);
+                }
+                *q = v;
             }
         }
+        return (x[0] != 0u ? 1u : 0u) | (x[1] != 0u ? 2u : 0u);
     }
 };
 
@@ -799,6 +911,16 @@ struct GenericTile {
         unpack_relator(r, p.w0, p.n0);
         unpack_relator(r + L, p.w1, p.n1);
     }
+    // runtime-L tiles (parity tests at any L) track no dirty relators: every row is written
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
+        unpack(lane, p);
+        return 3u;
+    }
+    __device__ __forceinline__ void set_dirty(int, uint32_t) const {}
+    template <bool NT>
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
+        store<true>(g, twoL, R, g, twoL, lane);
+    }
 };
 
 template <int NW, int LC, int VEC>
@@ -923,6 +1045,8 @@ struct StepArgs {
     uint8_t* fin_wave;
     const int32_t* next_index;
     int32_t* next_base;
+    // state_out == state_in (set by the launcher): the state store writes changed relators only
+    int in_place;
 };
 
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path)
@@ -943,6 +1067,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     bool keep = false;   // the env's row is left as loaded (out of domain, or its move failed)
     PresRegs<NW> p;
     int cnt0 = 0, cnt = 0, e = ACX_ERR_NONE;
+    uint32_t dm = 0;     // relators of the row that differ from state_in (in-place store)
     if (w.active) {
         int act;
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
@@ -964,7 +1089,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
-        if (!keep) tile.unpack(w.lane, p);
+        if (!keep) dm = tile.unpack_dirty(w.lane, p);
         const bool triv = !keep && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
         const bool trunc = !keep && a.step_count && cnt >= a.horizon;
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
@@ -995,6 +1120,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             wave_sync();
             keep = keep || rbad;
             if (w.active && !keep) tile.unpack(w.lane, p);
+            dm = (w.active && !keep) ? 3u : 0u;  // the tile now holds starting rows: write every kept-moving row
             tile.restore_flags(w.lane, w.active && keep);
         } else {
             // a few lanes: the wave loads just their rows (scattered resets cost their rows only)
@@ -1002,6 +1128,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             if (reset) {
                 rbad = tile.pack(w.lane, p);
                 if (!rbad) tile.unpack(w.lane, p);
+                dm = rbad ? 0u : 3u;
             }
             keep = keep || rbad;
             tile.flag_rows(w.lane, rbad);
@@ -1030,8 +1157,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             if (w.r0 == 0 && w.lane == 0) *a.next_base = *a.next_index;
         }
     }
-    wave_sync();
-    tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
+    if (a.in_place) {
+        // state_out == state_in: write only the relators that changed (a gated move, a
+        // cyclic conjugation that is a no-op and a failed env leave their row as it is in HBM)
+        tile.set_dirty(w.lane, dm);
+        wave_sync();
+        if (__ballot(dm != 0u)) tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane);
+    } else {
+        wave_sync();
+        tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
+    }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane);
@@ -1554,6 +1689,7 @@ struct StepLaunch {
     template <int NW, int LC, int VEC>
     int go() {
         const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+        a.in_place = a.state_in == a.state_out;
         if (learn) step_kernel<NW, LC, VEC, true><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         else step_kernel<NW, LC, VEC, false><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();

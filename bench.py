@@ -310,6 +310,7 @@ def main():
                              "(generate_trivial_states, utils.py:91-114) with step_count[i] = i mod H, so dones "
                              "and resets fire on a large share of env-steps")
         del tstarts, desync
+    chg_rate = None  # changed relators per env-step of the in-place step (step_api variant)
     if not args.no_step_api:
         # per-call acx_step API: one launch per env step, state in/out of HBM each step
         rew1 = torch.empty(B, dtype=torch.int32, device=dev)
@@ -335,17 +336,33 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         s_api = e0.elapsed_time(e1) / 1e3
-        # per env-step: state in 8L + action 4 + count in 4 + state out 8L + lengths 8 +
-        # reward 4 + done 1 + truncated 1 + count out 4 + err 1
-        sb = 16 * L + 27
+        n_err_api = int(err_count.item())
+        # The in-place step writes back only the relators that changed (gated moves, no-op
+        # cyclic conjugations and failed envs leave their rows as they are in HBM), so the bytes
+        # it must move depend on the walk: measured off the clock over the next 8 steps of the
+        # same walk as the mean number of changed relators per env-step.
+        chg = 0.0
+        for t in range(8):
+            before = st1.clone()
+            step(actions[(W + K + t) % actions.shape[0]])
+            chg += float(((before.view(B, 2, L) != st1.view(B, 2, L)).any(2)).sum().item()) / B
+            del before
+        chg /= 8
+        chg_rate = chg
+        # per env-step: state in 8L + action 4 + count in 4 + changed relators x 4L + lengths 8 +
+        # reward 4 + done 1 + truncated 1 + count out 4 + err 1; full rows: state out 8L
+        sb_full = 16 * L + 27
+        sb = 8 * L + 27 + 4 * L * chg
         variants["step_api"] = {
             "value": world * B * K / s_api if world == 1 else None,
             "unit": "env-steps/s",
             "ms_per_step": s_api / K * 1e3,
             "roofline": {"bound": "hbm", "achieved": B * sb / (s_api / K) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS,
-                         "bytes_per_env_step": sb},
-            "env_errors": int(err_count.item()),
+                         "bytes_per_env_step": sb, "changed_relators_per_env_step": chg,
+                         "bytes_per_env_step_full_rows": sb_full,
+                         "frac_on_full_row_bytes": B * sb_full / (s_api / K) / 1e9 / HBM_PEAK_GBS},
+            "env_errors": n_err_api,
         }
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
@@ -370,7 +387,7 @@ def main():
                 "value": B * K / s_g if world == 1 else None, "unit": "env-steps/s", "ms_per_step": s_g / K * 1e3,
                 "roofline": {"bound": "hbm", "achieved": B * sb / (s_g / K) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": B * sb / (s_g / K) / 1e9 / HBM_PEAK_GBS,
-                             "bytes_per_env_step": sb},
+                             "bytes_per_env_step": sb, "bytes_per_env_step_full_rows": sb_full},
             }
             del graph
 
@@ -400,11 +417,17 @@ def main():
         # per env-step: state in/out 16L + action 8 + count in/out 8 + obs f32 8L + reward f32 4
         # + done f32 4 + done/trunc u8 2 + history 1 + episode_len 4 + err 1 + curriculum
         # (done/trunc re-read 2, needs_host 1)
-        lb = 24 * L + 35
+        # The state store is in place (changed relators only, see step_api): the same walk
+        # distribution as the step_api variant (Miller-Schupp starts, uniform moves, horizon H),
+        # so its measured changed-relator rate prices the state write-back.
+        lb_full = 24 * L + 35
+        lb = lb_full if chg_rate is None else lb_full - 8 * L + 4 * L * chg_rate
         variants["learner_step"] = {
             "value": B * KL / s_l, "unit": "env-steps/s", "steps": KL, "ms_per_step": s_l / KL * 1e3,
             "roofline": {"bound": "hbm", "achieved": B * lb / (s_l / KL) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb},
+                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb,
+                         "bytes_per_env_step_full_rows": lb_full,
+                         "frac_on_full_row_bytes": B * lb_full / (s_l / KL) / 1e9 / HBM_PEAK_GBS},
         }
         del lobs, lrew, ldone, lenv
 

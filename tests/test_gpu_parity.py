@@ -55,6 +55,64 @@ def test_transitions_fixture(L, cyc):
     assert np.array_equal(out[~ok], d[k + "state_in"][~ok].astype(np.int32))
 
 
+@pytest.mark.parametrize("L", [7, 18, 36, 128])
+@pytest.mark.parametrize("cyc", [1, 0])
+def test_transitions_fixture_in_place(L, cyc):
+    """In place (state_out == state_in) the step kernel writes back only the relators that
+    changed: every row must still end as the reference's output, failed rows as their input."""
+    import acx
+    d = _load("transitions.npz")
+    k = f"L{L}_c{cyc}_"
+    st = torch.as_tensor(d[k + "state_in"].astype(np.int32)).to(DEV)
+    a = torch.as_tensor(d[k + "action"].astype(np.int32)).to(DEV)
+    err = torch.empty((st.shape[0],), dtype=torch.uint8, device=DEV)
+    acx.ops.step(st, a, state_out=st, cyclical=bool(cyc), err=err)
+    out, e = st.cpu().numpy(), err.cpu().numpy()
+    ok = e == 0
+    assert np.array_equal(e, d[k + "err"].astype(np.uint8))
+    assert np.array_equal(out[ok], d[k + "state_out"][ok].astype(np.int32))
+    assert np.array_equal(out[~ok], d[k + "state_in"][~ok].astype(np.int32))
+
+
+@pytest.mark.parametrize("L", [36, 128])
+def test_in_place_random_walk_with_bad_rows(L):
+    """In-place steps over a random walk where some rows are out of the packed domain (letter 3),
+    some moves are invalid ids and many envs reset together (horizon 4, synchronised counts:
+    whole-tile reloads), every step against the oracle."""
+    import acx
+    B, T, H = 64 * 9 + 13, 10, 4
+    rng = np.random.default_rng(L)
+    ms = np.load(os.path.join(os.path.dirname(acx.__file__), "data", "all_presentations.npy"))
+    s = np.zeros((B, 2 * L), np.int32)
+    for i in range(B):
+        p = ms[(7 * i) % len(ms)]
+        s[i, :18], s[i, L : L + 18] = p[:18], p[18:]
+    bad_rows = rng.choice(B, size=17, replace=False)
+    s[bad_rows, 0] = 3
+    st = torch.as_tensor(s).to(DEV)
+    rs = torch.as_tensor(s).to(DEV)
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    o_st, o_cnt = s.copy(), np.zeros(B, np.int32)
+    is_bad = np.zeros(B, bool)
+    is_bad[bad_rows] = True
+    for t in range(T):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        a[rng.choice(B, size=5, replace=False)] = 12  # invalid move id
+        acx.ops.step(st, torch.as_tensor(a).to(DEV), state_out=st, reset_state=rs, step_count=cnt, horizon=H,
+                     cyclical=True, err=err)
+        # failed envs (out-of-domain row: err 3, bad move id: err 4) keep state and count
+        fail = is_bad | (a == 12)
+        g = ~fail
+        sub, sub_cnt = np.ascontiguousarray(o_st[g]), np.ascontiguousarray(o_cnt[g])
+        O.env_step(sub, a[g], L, H, sub_cnt, reset_state=np.ascontiguousarray(s[g]), cyclical=True)
+        o_st[g], o_cnt[g] = sub, sub_cnt
+        e = err.cpu().numpy()
+        assert (e[is_bad] == 3).all() and (e[~is_bad & (a == 12)] == 4).all() and (e[g] == 0).all(), t
+        assert np.array_equal(st.cpu().numpy(), o_st), t
+        assert np.array_equal(cnt.cpu().numpy(), o_cnt), t
+
+
 @pytest.mark.parametrize("L", range(1, 10))
 def test_smallL_fixture_including_errors(L):
     d = _load("smallL_random.npz")
