@@ -36,6 +36,7 @@ SIGNATURES = {
     "acx_packed_actions_words": ([_I32, _I64], ctypes.c_int64),
     "acx_pack_actions": ([_P, _P, _I32, _I64, _P], ctypes.c_int),
     "acx_rollout_packed": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_rollout_obs8": ([_P] * 11 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_expand12": ([_P] * 6 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_canonicalize": ([_P] * 5 + [_I64, _I32, _I32, _P], ctypes.c_int),
     "acx_unpack_keys": ([_P] * 3 + [_I64, _I32, _P], ctypes.c_int),

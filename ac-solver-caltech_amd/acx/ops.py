@@ -119,7 +119,10 @@ def rollout(
     pack_actions (default): acx_pack_actions + acx_rollout_packed -- one streaming pass packs
     the (T, B) int32 move ids 8 per word (0.5 B per env-step) into `packed_workspace`
     ((ceil(T/8), B) int32, allocated if not given), then the rollout reads those; identical
-    results to acx_rollout (pack_actions=False)."""
+    results to acx_rollout (pack_actions=False).
+
+    obs_traj may be int32 or int8 (T, B, 2L): int8 is the reference's observation dtype
+    (ac_env.py:64-70) and goes to acx_rollout_obs8 (a quarter of the trajectory bytes)."""
     lib = _lib.load()
     _need_gpu(state, "state")
     L = _L_of(state)
@@ -130,7 +133,8 @@ def rollout(
     _check(actions, "actions", _INT32, (T, B), dev)
     _check(reset_state, "reset_state", _INT32, (B, 2 * L), dev)
     _check(step_count, "step_count", _INT32, (B,), dev)
-    _check(obs_traj, "obs_traj", _INT32, (T, B, 2 * L), dev)
+    obs8 = obs_traj is not None and obs_traj.dtype == torch.int8
+    _check(obs_traj, "obs_traj", torch.int8 if obs8 else _INT32, (T, B, 2 * L), dev)
     _check(reward_traj, "reward_traj", _INT32, (T, B), dev)
     _check(done_traj, "done_traj", _UINT8, (T, B), dev)
     _check(trunc_traj, "trunc_traj", _UINT8, (T, B), dev)
@@ -145,12 +149,28 @@ def rollout(
             raise ValueError(f"packed_workspace must be a contiguous int32 tensor of >= {words * B} elements on {dev}")
         st = lib.acx_pack_actions(_ptr(actions), _ptr(packed_workspace), T, B, _stream(dev))
         _lib.check(st, "acx_pack_actions")
+        if obs8:
+            st = lib.acx_rollout_obs8(
+                _ptr(state), None, _ptr(packed_workspace), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj),
+                _ptr(reward_traj), _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L,
+                int(horizon), int(bool(cyclical)), _stream(dev),
+            )
+            _lib.check(st, "acx_rollout_obs8")
+            return
         st = lib.acx_rollout_packed(
             _ptr(state), _ptr(packed_workspace), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj),
             _ptr(reward_traj), _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon),
             int(bool(cyclical)), _stream(dev),
         )
         _lib.check(st, "acx_rollout_packed")
+        return
+    if obs8:
+        st = lib.acx_rollout_obs8(
+            _ptr(state), _ptr(actions), None, _ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj),
+            _ptr(done_traj), _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon),
+            int(bool(cyclical)), _stream(dev),
+        )
+        _lib.check(st, "acx_rollout_obs8")
         return
     st = lib.acx_rollout(
         _ptr(state), _ptr(actions), _ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj),

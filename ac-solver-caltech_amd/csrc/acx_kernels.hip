@@ -315,6 +315,39 @@ struct FastTile {
         }
     }
 
+    // LDS -> R contiguous global rows as int8 letters (the observation_space dtype,
+    // ac_env.py:64-70): the tile's LDS image IS the int8 tile, so a 16-byte LDS read is a
+    // 16-byte global store; 2L bytes per row, (R * 2L) / 16 stores per wave (4.5 per lane at L = 36)
+    template <bool NT>
+    __device__ __forceinline__ void store_rows_i8(int8_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nd = R * CPR;  // dwords of the int8 tile
+        uint32_t* dst = reinterpret_cast<uint32_t*>(g);
+        // rows are 2L = 8m bytes: a tile starts 16-byte aligned unless m and the row index are
+        // both odd (L = 36 with an odd batch), then dword stores (wave-uniform branch)
+        const bool al = (reinterpret_cast<uintptr_t>(g) & 15u) == 0;
+#pragma unroll
+        for (int u = 0; u < (WAVE * CPR + 4 * WAVE - 1) / (4 * WAVE); ++u) {
+            const int d0 = 4 * (ln + u * WAVE);
+            if (d0 >= nd) continue;
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int d = d0 + j < nd ? d0 + j : d0;
+                const int r = d / CPR;
+                v[j] = lds[r * S + (d - r * CPR)];
+            }
+            if (al && d0 + 4 <= nd) {
+                const v4i_t x = {(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+                if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(dst + d0));
+                else *reinterpret_cast<v4i_t*>(dst + d0) = x;
+            } else {
+                for (int j = 0; j < 4 && d0 + j < nd; ++j) dst[d0 + j] = v[j];
+            }
+        }
+    }
+
     // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from fallback
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
@@ -595,6 +628,29 @@ struct CodeTile {
         }
     }
 
+    // see FastTile::store_rows_i8: slot c of the tile is int8 dword c of the global tile
+    template <bool NT>
+    __device__ __forceinline__ void store_rows_i8(int8_t* g, int R, int lane) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int nc = R * CPR;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(g);
+#pragma unroll
+        for (int u = 0; u < (WAVE * CPR) / (4 * WAVE); ++u) {
+            const int c0 = 4 * (ln + u * WAVE);
+            if (c0 >= nc) continue;  // nc is a multiple of 4 (CPR % 4 == 0)
+            int x[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t p = get(c0 + j);
+                x[j] = (int)codes_to_i8x4(p & 0xffu, 8u * __builtin_popcount((p >> 8) & 0xfu));
+            }
+            const v4i_t v = {x[0], x[1], x[2], x[3]};
+            if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4i_t*>(dst + c0));
+            else *reinterpret_cast<v4i_t*>(dst + c0) = v;
+        }
+    }
+
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
                                           int64_t fpitch, int lane) const {
@@ -754,6 +810,11 @@ struct GenericTile {
     template <bool NT>
     __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
         store<false, NT>(g, 2 * L, R, nullptr, 0, lane);
+    }
+    // int8 rows, byte by byte (parity instantiations)
+    template <bool NT>
+    __device__ __forceinline__ void store_rows_i8(int8_t* g, int R, int lane) const {
+        for (int i = lane; i < R * twoL; i += WAVE) g[i] = row(i / twoL)[i % twoL];
     }
     __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
         flags[lane] = flagged;
@@ -1186,9 +1247,11 @@ struct RolloutArgs {
     int32_t* err_count;
     int64_t B;
     int T, L, horizon, cyclical;
+    int8_t* obs_traj8;  // acx_rollout_obs8: the trajectory as int8 letters (obs_traj unused)
 };
 
-template <int NW, int LC, int VEC, bool OBS>
+// OBS: 0 no trajectory, 1 int32 obs trajectory (obs_traj), 2 int8 obs trajectory (obs_traj8)
+template <int NW, int LC, int VEC, int OBS>
 __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_kernel(RolloutArgs a) {
     using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1264,10 +1327,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 if (rbad && first_err == ACX_ERR_NONE) first_err = ACX_ERR_DOMAIN;
             }
         }
-        if constexpr (OBS) {
+        if constexpr (OBS != 0) {
             if (w.active && !bad) tile.unpack(w.lane, p);
             wave_sync();
-            tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
+            if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
+            else tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, w.lane);
             wave_sync();
         }
     };
@@ -1280,7 +1344,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     // compiler waits vmcnt(0)): a drain of the wave's write queue.  8-step batches cost 8 %
     // of the rollout in drains (tools/store_pattern.py, ACT8 vs none); with obs stores the
     // batch is 32 steps, loaded as four groups of 8 (only the first wait finds stores).
-    constexpr int ACT_BLOCK = OBS ? 32 : 8;
+    constexpr int ACT_BLOCK = OBS != 0 ? 32 : 8;
     constexpr int ACT_GROUP = 8;
     constexpr int QW = ACT_BLOCK / 8;
     uint32_t q[QW];
@@ -1701,8 +1765,9 @@ struct RolloutLaunch {
     template <int NW, int LC, int VEC>
     int go() {
         const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        if (a.obs_traj) rollout_kernel<NW, LC, VEC, true><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        else rollout_kernel<NW, LC, VEC, false><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        if (a.obs_traj8) rollout_kernel<NW, LC, VEC, 2><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        else if (a.obs_traj) rollout_kernel<NW, LC, VEC, 1><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        else rollout_kernel<NW, LC, VEC, 0><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
     }
 };
@@ -1871,6 +1936,20 @@ int acx_rollout_packed(int32_t* state, const uint32_t* packed_actions, const int
     if (!aligned16(state) || !aligned16(reset_state) || (obs_traj && !aligned16(obs_traj))) return ACX_E_ARG;
     RolloutArgs a{state, nullptr, packed_actions, reset_state, step_count, obs_traj, reward_traj, done_traj,
                   trunc_traj, err, err_count, B, T, L, horizon, cyclical};
+    RolloutLaunch f{a, (hipStream_t)stream};
+    return dispatch(L, f);
+}
+
+int acx_rollout_obs8(int32_t* state, const int32_t* actions, const uint32_t* packed_actions, const int32_t* reset_state,
+                     int32_t* step_count, int8_t* obs_traj8, int32_t* reward_traj, uint8_t* done_traj,
+                     uint8_t* trunc_traj, uint8_t* err, int32_t* err_count, int32_t T, int64_t B, int32_t L,
+                     int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || T < 0 || L < 1 || L > ACX_MAX_L) return ACX_E_ARG;
+    if (B == 0 || T == 0) return ACX_OK;
+    if (!state || !reset_state || !step_count || !obs_traj8 || (!actions == !packed_actions)) return ACX_E_ARG;
+    if (!aligned16(state) || !aligned16(reset_state) || !aligned16(obs_traj8)) return ACX_E_ARG;
+    RolloutArgs a{state, actions, packed_actions, reset_state, step_count, nullptr, reward_traj, done_traj,
+                  trunc_traj, err, err_count, B, T, L, horizon, cyclical, obs_traj8};
     RolloutLaunch f{a, (hipStream_t)stream};
     return dispatch(L, f);
 }

@@ -154,6 +154,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-bfs", action="store_true")
     ap.add_argument("--no-desync", action="store_true")
+    ap.add_argument("--no-obs8", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -295,6 +296,43 @@ def main():
                 "workload": what,
                 "roofline": {"bound": "hbm", "achieved": nb / s_d / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": nb / s_d / 1e9 / HBM_PEAK_GBS, "launch_bytes": nb}}
+
+    if not args.no_obs8:
+        # the headline rollout (same starts, counts from 0, same actions) with the observation
+        # trajectory in the reference's observation dtype, int8 (ac_env.py:64-70: Box(int8); the
+        # observations SyncVectorEnv returns): 2L bytes per env-step instead of 8L
+        obs8 = torch.zeros((T_buf, B, 2 * L), dtype=torch.int8, device=dev)
+        st8, cnt8 = starts.clone(), torch.zeros(B, dtype=torch.int32, device=dev)
+        err_count.zero_()
+
+        def go8(a, T):
+            for t0 in range(0, T, T_buf):
+                t1 = min(T, t0 + T_buf)
+                ops.rollout(st8, a[t0:t1], starts, cnt8, horizon=H, cyclical=True, obs_traj=obs8[: t1 - t0],
+                            reward_traj=rew[: t1 - t0], done_traj=done[: t1 - t0], trunc_traj=trunc[: t1 - t0],
+                            err=err, err_count=err_count)
+
+        if W > 0:
+            go8(actions[:W], W)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        go8(actions[W : W + K], K)
+        e1.record()
+        torch.cuda.synchronize()
+        s8 = e0.elapsed_time(e1) / 1e3
+        nres = count_resets(K)
+        nb8 = rollout_bytes(nres) - K * B * 6 * L  # obs 2L instead of 8L bytes per env-step
+        variants["rollout_obs_int8"] = {
+            "value": B * K / s8, "unit": "env-steps/s", "kernel_ms": s8 * 1e3, "ms_per_step": s8 / K * 1e3,
+            "env_errors": int(err_count.item()),
+            "workload": "the headline rollout writing the (K,B,2L) observation trajectory as int8 (the reference's "
+                        "observation_space dtype) instead of int32",
+            "roofline": {"bound": "hbm", "achieved": nb8 / s8 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": nb8 / s8 / 1e9 / HBM_PEAK_GBS, "launch_bytes": nb8,
+                         "bytes_per_env_step": step_bytes - 6 * L}}
+        del obs8, st8, cnt8
 
     if not args.no_desync:
         desync = torch.arange(B, dtype=torch.int32, device=dev) % H

@@ -179,6 +179,18 @@ int acx_rollout_packed(int32_t* state, const uint32_t* packed_actions, const int
                        int32_t L, int32_t horizon, int32_t cyclical, void* stream);
 
 /*
+ * The rollout with the observation trajectory as int8 letters, obs_traj8 (T,B,2L) int8: the
+ * dtype of the reference's observation_space (ac_env.py:64-70, Box(int8)) and of the
+ * observations gymnasium's SyncVectorEnv returns (environment.py:70-72), a quarter of the
+ * int32 trajectory's bytes.  Exactly one of actions ((T,B) int32) / packed_actions
+ * (acx_pack_actions) is given; everything else as acx_rollout.
+ */
+int acx_rollout_obs8(int32_t* state, const int32_t* actions, const uint32_t* packed_actions,
+                     const int32_t* reset_state, int32_t* step_count, int8_t* obs_traj8, int32_t* reward_traj,
+                     uint8_t* done_traj, uint8_t* trunc_traj, uint8_t* err, int32_t* err_count, int32_t T,
+                     int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+
+/*
  * 12-way neighbour expansion: for every parent (N,2L) and every move id a in [0,12)
  * the child ACMove(a, parent, L, cyclical) (greedy/bfs call it with cyclical=0).
  *   children   (N,12,2L) int32 or NULL

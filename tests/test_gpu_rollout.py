@@ -29,14 +29,14 @@ def _starts(L, B, seed=0):
     return out
 
 
-def _roll(starts, acts, L, H, cyc, pack, count0=None, resets=None):
+def _roll(starts, acts, L, H, cyc, pack, count0=None, resets=None, obs_dtype=torch.int32):
     from acx import ops
     T, B = acts.shape
     st = torch.as_tensor(starts).to(DEV)
     rs = st.clone() if resets is None else torch.as_tensor(resets).to(DEV)
     cnt = (torch.zeros(B, dtype=torch.int32, device=DEV) if count0 is None
            else torch.as_tensor(count0.astype(np.int32)).to(DEV))
-    obs = torch.full((T, B, 2 * L), -7, dtype=torch.int32, device=DEV)
+    obs = torch.full((T, B, 2 * L), -7, dtype=obs_dtype, device=DEV)
     rew = torch.zeros((T, B), dtype=torch.int32, device=DEV)
     dn = torch.zeros((T, B), dtype=torch.uint8, device=DEV)
     tr = torch.zeros((T, B), dtype=torch.uint8, device=DEV)
@@ -200,3 +200,23 @@ def test_step_api_desynchronised_resets_equal_oracle(L, H):
         fin = (d | trn).astype(bool)
         assert np.array_equal(fo.cpu().numpy()[fin], o_fo[fin]), t
         assert (err.cpu().numpy() == 0).all()
+
+
+@pytest.mark.parametrize("L,B,T", [(36, 1000, 13), (36, 333, 11), (36, 4096, 40), (128, 200, 21), (17, 333, 9),
+                                   (36, 64, 1)])
+@pytest.mark.parametrize("pack", [True, False])
+def test_int8_obs_trajectory_equals_int32(L, B, T, pack):
+    """acx_rollout_obs8 (the observation trajectory in the reference's int8 observation dtype,
+    ac_env.py:64-70): the same episodes as the int32 trajectory, letter for letter, including an
+    odd batch at L = 36 (tiles not 16-byte aligned: dword stores), partial tiles, the generic-L
+    tile and desynchronised resets."""
+    rng = np.random.default_rng(L * 7 + T + B)
+    starts = _starts(L, B, seed=B)
+    acts = rng.integers(0, 12, size=(T, B)).astype(np.int32)
+    count0 = (np.arange(B) % 5).astype(np.int32)
+    a = _roll(starts, acts, L, 5, True, pack=pack, count0=count0)
+    b = _roll(starts, acts, L, 5, True, pack=pack, count0=count0, obs_dtype=torch.int8)
+    assert b[2].dtype == np.int8
+    assert np.array_equal(a[2], b[2].astype(np.int32))
+    for i in (0, 1, 3, 4, 5, 6, 7):
+        assert np.array_equal(a[i], b[i]), i
