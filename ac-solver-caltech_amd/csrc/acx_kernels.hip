@@ -332,11 +332,23 @@ struct FastTile {
             const int d0 = 4 * (ln + u * WAVE);
             if (d0 >= nd) continue;
             uint32_t v[4];
+            if constexpr (S == CPR) {
+                // flat image: one 16-byte LDS read per lane, consecutive lanes consecutive
+                // 16 bytes (per-dword reads at a 16-byte lane stride were 8-way bank conflicts)
+                if (d0 + 4 <= nd) {
+                    const uint4 x = *reinterpret_cast<const uint4*>(lds + d0);
+                    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+                } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int d = d0 + j < nd ? d0 + j : d0;
-                const int r = d / CPR;
-                v[j] = lds[r * S + (d - r * CPR)];
+                    for (int j = 0; j < 4; ++j) v[j] = lds[d0 + j < nd ? d0 + j : d0];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int d = d0 + j < nd ? d0 + j : d0;
+                    const int r = d / CPR;
+                    v[j] = lds[r * S + (d - r * CPR)];
+                }
             }
             if (al && d0 + 4 <= nd) {
                 const v4i_t x = {(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
@@ -639,12 +651,14 @@ struct CodeTile {
         for (int u = 0; u < (WAVE * CPR) / (4 * WAVE); ++u) {
             const int c0 = 4 * (ln + u * WAVE);
             if (c0 >= nc) continue;  // nc is a multiple of 4 (CPR % 4 == 0)
+            // 4 slots of one row (CPR % 4 == 0): one 8-byte LDS read
+            const int r = c0 / CPR;
+            const uint2 q = *reinterpret_cast<const uint2*>(slots(r) + (c0 - r * CPR));
+            const uint32_t sl[4] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16};
             int x[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t p = get(c0 + j);
-                x[j] = (int)codes_to_i8x4(p & 0xffu, 8u * __builtin_popcount((p >> 8) & 0xfu));
-            }
+            for (int j = 0; j < 4; ++j)
+                x[j] = (int)codes_to_i8x4(sl[j] & 0xffu, 8u * __builtin_popcount((sl[j] >> 8) & 0xfu));
             const v4i_t v = {x[0], x[1], x[2], x[3]};
             if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4i_t*>(dst + c0));
             else *reinterpret_cast<v4i_t*>(dst + c0) = v;
