@@ -518,8 +518,8 @@ def main():
     # and per-launch terms at any K, so the ratio is K-independent) and labelled as scaled.
     traffic, traffic_src = None, None
     cands = []
-    for tag in ("r02_k20", "r02", "r01"):
-        prof = os.path.join(REPO, "profiles", tag.split("_")[0], f"{tag}_summary.json")
+    for tag in ("r02h_k20", "r02h", "r02_k20", "r02", "r01"):
+        prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
         with open(prof) as f:
@@ -530,7 +530,7 @@ def main():
             cands.append((ps["bench_line"].get("steps") != K, tag, ps["bench_line"].get("steps"), td))
     if cands:
         scaled, tag, kp, td = min(cands, key=lambda c: c[0])
-        where = f"profiles/{tag.split('_')[0]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE"
+        where = f"profiles/{tag.split('_')[0][:3]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE"
         if not scaled:
             traffic, traffic_src = td["pmc_hbm_bytes"], f"{where} of this command (K={K})"
         else:
@@ -572,7 +572,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": f"acx::pack_actions_kernel + acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,true>",
+            "kernel": f"acx::pack_actions_kernel + acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,1>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
             "resets_in_launch": resets,

@@ -61,7 +61,9 @@ if bench:
     # the timed launch = the last (in time) of the longest rollout_kernel dispatches (the warmup
     # launch comes first) plus, when ops.rollout packed the move ids first, the matching
     # pack_actions_kernel dispatch
-    timed = [v for n, v in summary["kernels"].items() if "rollout_kernel" in n]
+    # the int32-trajectory instantiation (rollout_kernel<.., 1>; `true` before round 2's int8 mode)
+    timed = [v for n, v in summary["kernels"].items()
+             if "rollout_kernel" in n and (n.split("(")[0].endswith(", 1>") or n.split("(")[0].endswith("true>"))]
     packs = [v for n, v in summary["kernels"].items() if "pack_actions_kernel" in n]
 
     def hbm(k, i):
