@@ -1643,6 +1643,121 @@ __global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
     if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
 }
 
+// expand12 with int32 children (acx_expand12 children != NULL): one block of 4 waves per tile
+// of 64 parents, as expand12_keys_kernel -- wave 0 stages and packs the parents, wave w then
+// makes the children of actions 3w..3w+2, one action at a time: unpack into its own LDS tile,
+// then a tile store with row pitch 12 * 2L (child (p, a) is row 12p + a).  The block's 64 x 12
+// child rows are one contiguous 221 KB region at L = 36, written as 3-row runs per parent and
+// wave (the lane-per-parent loop it replaces made 12 serial moves per lane and wrote each child
+// row as its own 288-byte run).  Lengths and error codes go through LDS and out as one
+// contiguous run per block.  Out-of-domain parents' children are copies of the parent row (the
+// fallback rows of the tile store), as in expand12_kernel.
+template <int NW, int LC, int VEC>
+struct ExpandChildrenSmem {
+    static __host__ __device__ size_t tile_bytes(int L) {
+        return (TileFor<NW, LC, VEC>::wave_bytes(L) + 15) & ~(size_t)15;
+    }
+    static __host__ __device__ size_t packed_off(int L) { return WPB * tile_bytes(L); }
+    static __host__ __device__ size_t lens_off(int L) {
+        return packed_off(L) + (size_t)WAVE * packed_words<NW>() * 4;
+    }
+    static __host__ __device__ size_t err_off(int L) { return lens_off(L) + (size_t)WAVE * 12 * 2 * 4; }
+    static __host__ __device__ size_t bytes(int L) { return err_off(L) + (size_t)WAVE * 12; }
+};
+
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) {
+    using Tile = TileFor<NW, LC, VEC>;
+    using Smem = ExpandChildrenSmem<NW, LC, VEC>;
+    constexpr int PW = packed_words<NW>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t r0 = (int64_t)blockIdx.x * WAVE;
+    if (r0 >= a.N) return;  // block-uniform
+    const int R = (int)((a.N - r0) < WAVE ? (a.N - r0) : WAVE);
+    const bool active = lane < R;
+    Tile tile(smem + wid * Smem::tile_bytes(a.L), a.L);
+    const int L = tile.Lr(), twoL = 2 * L;
+    uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::packed_off(a.L));
+    int32_t* lens_st = reinterpret_cast<int32_t*>(smem + Smem::lens_off(a.L));
+    uint8_t* err_st = reinterpret_cast<uint8_t*>(smem + Smem::err_off(a.L));
+    const bool cyc = a.cyclical != 0;
+    if (wid == 0) {
+        tile.load(a.parents + r0 * twoL, R, lane);
+        if (active) {
+            PresRegs<NW> p;
+            const bool bad = tile.pack(lane, p);
+            const bool clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+            uint32_t* d = packed + lane * PW;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                d[k] = p.w0.w[k];
+                d[NW + k] = p.w1.w[k];
+            }
+            d[2 * NW] = (uint32_t)p.n0 | ((uint32_t)p.n1 << 8);
+            d[2 * NW + 1] = (uint32_t)bad | ((uint32_t)clean << 1);
+        }
+    }
+    __syncthreads();
+    PresRegs<NW> p;
+    bool bad = false, clean = false;
+    if (active) {
+        const uint32_t* d = packed + lane * PW;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            p.w0.w[k] = d[k];
+            p.w1.w[k] = d[NW + k];
+        }
+        p.n0 = (int)(d[2 * NW] & 0xffu);
+        p.n1 = (int)((d[2 * NW] >> 8) & 0xffu);
+        bad = (d[2 * NW + 1] & 1u) != 0;
+        clean = (d[2 * NW + 1] & 2u) != 0;
+    }
+    // every wave's tile flags its out-of-domain rows (their children copy the parent row)
+    tile.restore_flags(lane, active && bad);
+    int nerr = 0;
+    const int64_t par = r0 + lane;
+#pragma unroll 1
+    for (int j = 0; j < KEYS_APW; ++j) {
+        const int act = wid * KEYS_APW + j;
+        if (active) {
+            PresRegs<NW> q = p;
+            int e;
+            if (bad) e = ACX_ERR_DOMAIN;
+            else if (clean) e = ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            else e = ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            nerr += e != ACX_ERR_NONE;
+            err_st[lane * 12 + act] = (uint8_t)e;
+            lens_st[(lane * 12 + act) * 2] = q.n0;
+            lens_st[(lane * 12 + act) * 2 + 1] = q.n1;
+            if (a.child_key) {  // keys as well (not the search path): per lane, unstaged
+                PresRegs<NW> kq = q;
+                if (e != ACX_ERR_NONE) {
+                    kq.n0 = 0xff;
+                    kq.n1 = 0xff;
+                }
+                store_key<NW>(a.child_key + (par * 12 + act) * a.kw64, a.kw64, L, kq);
+            }
+            if (!bad) tile.unpack(lane, q);
+        }
+        wave_sync();
+        tile.template store<true>(a.children + (r0 * 12 + act) * twoL, (int64_t)12 * twoL, R,
+                                  a.parents + r0 * twoL, twoL, lane);
+        wave_sync();
+    }
+    __syncthreads();
+    if (a.child_len) {
+        int32_t* dst = a.child_len + r0 * 24;
+        for (int i = threadIdx.x; i < R * 24; i += BLOCK) dst[i] = lens_st[i];
+    }
+    if (a.err) {
+        uint8_t* dst = a.err + r0 * 12;
+        for (int i = threadIdx.x; i < R * 12; i += BLOCK) dst[i] = err_st[i];
+    }
+    if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
+}
+
 struct CanonArgs {
     const int32_t* state_in;
     int32_t* state_out;
@@ -1790,6 +1905,11 @@ struct ExpandLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
+        const size_t cshm = ExpandChildrenSmem<NW, LC, VEC>::bytes(a.L);
+        if (a.children && cshm <= 64 * 1024) {
+            expand12_children_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), cshm, s>>>(a);
+            return finish_launch();
+        }
         const size_t kshm = ExpandKeysSmem<NW, LC, VEC>::bytes(a.L);
         if (!a.children && a.child_key && kshm <= 40 * 1024) {  // the search path
             expand12_keys_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), kshm, s>>>(a);

@@ -211,6 +211,33 @@ def test_expand12_vs_oracle(L, cyc):
     assert np.array_equal(res["lengths"].cpu().numpy()[ok], lens[ok])
 
 
+@pytest.mark.parametrize("L,N", [(36, 64 * 5 + 17), (128, 64 * 3 + 1), (17, 333), (36, 64)])
+def test_expand12_children_with_bad_parents(L, N):
+    """Block-per-tile children kernel: children, lengths and error codes of every (parent,
+    action) against the oracle, partial tiles, children without keys, and out-of-domain parents
+    (a letter 3: every child is err 3 and a copy of the parent row)."""
+    import acx
+    rng = np.random.default_rng(L * 31 + N)
+    s = np.zeros((N, 2 * L), np.int32)
+    for b in range(N):
+        for h in range(2):
+            n = int(rng.integers(1, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    bad = rng.choice(N, size=max(1, N // 40), replace=False)
+    s[bad, 0] = 3
+    good = np.ones(N, bool)
+    good[bad] = False
+    ch, lens, err = O.expand12(np.ascontiguousarray(s[good]), L, False)
+    res = acx.ops.expand12(torch.as_tensor(s).to(DEV), cyclical=False)
+    g_ch, g_len, g_err = (res[k].cpu().numpy() for k in ("children", "lengths", "err"))
+    assert np.array_equal(g_err[good], err)
+    assert np.array_equal(g_ch[good], ch)
+    ok = err == 0
+    assert np.array_equal(g_len[good][ok], lens[ok])
+    assert (g_err[bad] == 3).all()
+    assert np.array_equal(g_ch[bad], np.repeat(s[bad][:, None, :], 12, axis=1))
+
+
 @pytest.mark.parametrize("L", [3, 36, 128])
 def test_canonicalize_vs_oracle(L):
     import acx

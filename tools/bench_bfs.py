@@ -64,4 +64,26 @@ best = min(times)
 bpp = 8 * L + 12 * kw * 8  # parent row in + 12 packed child keys out
 res["expand12_keys"] = {"parents": N, "kernel_ms": best * 1e3, "children_per_s": 12 * N / best,
                         "bytes_per_parent": bpp, "GBps": N * bpp / best / 1e9, "frac": N * bpp / best / 8e12}
+del kout
+
+# children mode (full int32 children + lengths + error codes) over the first 10^6 parents:
+# parent row 8L in, 12 x (8L + 8 + 1) out
+M = min(N, 10 ** 6)
+cout = {"children": torch.empty((M, 12, 2 * L), dtype=torch.int32, device=dev),
+        "lengths": torch.empty((M, 12, 2), dtype=torch.int32, device=dev),
+        "err": torch.empty((M, 12), dtype=torch.uint8, device=dev)}
+ops.expand12(parents[:M], cyclical=False, children=True, lengths=True, keys=False, err=True, out=cout)
+torch.cuda.synchronize()
+times = []
+for _ in range(5):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ops.expand12(parents[:M], cyclical=False, children=True, lengths=True, keys=False, err=True, out=cout)
+    e1.record()
+    torch.cuda.synchronize()
+    times.append(e0.elapsed_time(e1) / 1e3)
+best = min(times)
+bpp = 8 * L + 12 * (8 * L + 9)
+res["expand12_children"] = {"parents": M, "kernel_ms": best * 1e3, "children_per_s": 12 * M / best,
+                            "bytes_per_parent": bpp, "GBps": M * bpp / best / 1e9, "frac": M * bpp / best / 8e12}
 print(json.dumps(res))
