@@ -1644,7 +1644,7 @@ __global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
 }
 
 // expand12 with int32 children (acx_expand12 children != NULL): one block of 4 waves per tile
-// of 64 parents, as expand12_keys_kernel -- wave 0 stages and packs the parents, wave w then
+// of 64 parents, as expand12_keys_kernel -- every wave stages and packs the parents, wave w
 // makes the children of actions 3w..3w+2, one action at a time: unpack into its own LDS tile,
 // then a tile store with row pitch 12 * 2L (child (p, a) is row 12p + a).  The block's 64 x 12
 // child rows are one contiguous 221 KB region at L = 36, written as 3-row runs per parent and
@@ -1657,10 +1657,7 @@ struct ExpandChildrenSmem {
     static __host__ __device__ size_t tile_bytes(int L) {
         return (TileFor<NW, LC, VEC>::wave_bytes(L) + 15) & ~(size_t)15;
     }
-    static __host__ __device__ size_t packed_off(int L) { return WPB * tile_bytes(L); }
-    static __host__ __device__ size_t lens_off(int L) {
-        return packed_off(L) + (size_t)WAVE * packed_words<NW>() * 4;
-    }
+    static __host__ __device__ size_t lens_off(int L) { return WPB * tile_bytes(L); }
     static __host__ __device__ size_t err_off(int L) { return lens_off(L) + (size_t)WAVE * 12 * 2 * 4; }
     static __host__ __device__ size_t bytes(int L) { return err_off(L) + (size_t)WAVE * 12; }
 };
@@ -1669,7 +1666,6 @@ template <int NW, int LC, int VEC>
 __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) {
     using Tile = TileFor<NW, LC, VEC>;
     using Smem = ExpandChildrenSmem<NW, LC, VEC>;
-    constexpr int PW = packed_words<NW>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
@@ -1679,43 +1675,20 @@ __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) 
     const bool active = lane < R;
     Tile tile(smem + wid * Smem::tile_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
-    uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::packed_off(a.L));
     int32_t* lens_st = reinterpret_cast<int32_t*>(smem + Smem::lens_off(a.L));
     uint8_t* err_st = reinterpret_cast<uint8_t*>(smem + Smem::err_off(a.L));
     const bool cyc = a.cyclical != 0;
-    if (wid == 0) {
-        tile.load(a.parents + r0 * twoL, R, lane);
-        if (active) {
-            PresRegs<NW> p;
-            const bool bad = tile.pack(lane, p);
-            const bool clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
-            uint32_t* d = packed + lane * PW;
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                d[k] = p.w0.w[k];
-                d[NW + k] = p.w1.w[k];
-            }
-            d[2 * NW] = (uint32_t)p.n0 | ((uint32_t)p.n1 << 8);
-            d[2 * NW + 1] = (uint32_t)bad | ((uint32_t)clean << 1);
-        }
-    }
-    __syncthreads();
+    // every wave stages and packs the parent tile itself (the block's other three reads of the
+    // 18 KB tile are L2 hits): no block-wide wait on one wave's load before the moves start;
+    // the tile's flags mark the out-of-domain rows, whose children copy the parent row
+    tile.load(a.parents + r0 * twoL, R, lane);
     PresRegs<NW> p;
     bool bad = false, clean = false;
     if (active) {
-        const uint32_t* d = packed + lane * PW;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            p.w0.w[k] = d[k];
-            p.w1.w[k] = d[NW + k];
-        }
-        p.n0 = (int)(d[2 * NW] & 0xffu);
-        p.n1 = (int)((d[2 * NW] >> 8) & 0xffu);
-        bad = (d[2 * NW + 1] & 1u) != 0;
-        clean = (d[2 * NW + 1] & 2u) != 0;
+        bad = tile.pack(lane, p);
+        clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
     }
-    // every wave's tile flags its out-of-domain rows (their children copy the parent row)
-    tile.restore_flags(lane, active && bad);
+
     int nerr = 0;
     const int64_t par = r0 + lane;
 #pragma unroll 1
