@@ -109,14 +109,20 @@ class ACEnv:
         self.device = torch.device(device if device is not None else "cuda")
         self._dtype = self.initial_state.dtype
         dev = self.device
-        self._state = torch.empty((1, 2 * L), dtype=torch.int32, device=dev)
+        # one int32 device block holds everything a step returns -- state 2L | lengths 2 | reward |
+        # done, truncated, err as bytes of one slot -- so a step is one launch plus one D2H copy
+        # into a pinned host block (no per-step allocations or conversion kernels)
+        self._blk = torch.zeros(2 * L + 4, dtype=torch.int32, device=dev)
+        self._host = torch.empty(2 * L + 4, dtype=torch.int32, pin_memory=True)
+        b8 = self._blk.view(torch.uint8)
+        self._state = self._blk[: 2 * L].view(1, 2 * L)
+        self._lens = self._blk[2 * L : 2 * L + 2].view(1, 2)
+        self._reward = self._blk[2 * L + 2 : 2 * L + 3]
+        self._done = b8[4 * (2 * L + 3) : 4 * (2 * L + 3) + 1]
+        self._trunc = b8[4 * (2 * L + 3) + 1 : 4 * (2 * L + 3) + 2]
+        self._err = b8[4 * (2 * L + 3) + 2 : 4 * (2 * L + 3) + 3]
         self._action = torch.empty((1,), dtype=torch.int32, device=dev)
         self._count = torch.zeros((1,), dtype=torch.int32, device=dev)
-        self._reward = torch.empty((1,), dtype=torch.int32, device=dev)
-        self._done = torch.empty((1,), dtype=torch.uint8, device=dev)
-        self._trunc = torch.empty((1,), dtype=torch.uint8, device=dev)
-        self._lens = torch.empty((1, 2), dtype=torch.int32, device=dev)
-        self._err = torch.empty((1,), dtype=torch.uint8, device=dev)
         self._set_state(np.copy(self.initial_state))
         self.actions = []
 
@@ -145,13 +151,14 @@ class ACEnv:
                  horizon=self.horizon_length, cyclical=True, reward=self._reward, done=self._done,
                  truncated=self._trunc, lengths=self._lens, err=self._err)
         L = self.max_relator_length
-        host = torch.cat([self._state.reshape(-1), self._lens.reshape(-1), self._reward,
-                          self._done.to(torch.int32), self._trunc.to(torch.int32), self._err.to(torch.int32)]).cpu()
-        h = host.numpy()
-        raise_for_err(int(h[-1]), "ACEnv.step")
+        self._host.copy_(self._blk, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        h = self._host.numpy()
+        flags = int(h[2 * L + 3])  # little-endian bytes: done, truncated, err
+        raise_for_err((flags >> 16) & 0xff, "ACEnv.step")
         self.state = h[: 2 * L].astype(self._dtype)
         self.lengths = [int(h[2 * L]), int(h[2 * L + 1])]
-        reward, done, truncated = int(h[2 * L + 2]), bool(h[2 * L + 3]), bool(h[2 * L + 4])
+        reward, done, truncated = int(h[2 * L + 2]), bool(flags & 0xff), bool((flags >> 8) & 0xff)
         self.count_steps += 1
         return self.state, reward, done, truncated, ({"actions": self.actions.copy()} if done else {})
 

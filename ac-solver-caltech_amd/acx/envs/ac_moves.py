@@ -15,10 +15,34 @@ the host<->device copies; batched callers use acx.ops directly.
 
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 import torch
 
 from .. import _lib, ops
+
+# Per-thread staging for the per-call ACMove (B = 1): one pinned host block in, one device block
+# holding the kernel's outputs (state | lengths | error byte), one pinned host block out -- so a
+# call is one H2D copy, one step launch and one D2H copy, with no allocations and no extra
+# conversion kernels.  Thread-local: ACMove is re-entrant in the reference.
+_TLS = threading.local()
+
+
+def _stage(dev: torch.device, L: int):
+    cache = getattr(_TLS, "stage", None)
+    if cache is None:
+        cache = _TLS.stage = {}
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device(), L)
+    st = cache.get(key)
+    if st is None:
+        n = 2 * L + 3  # state 2L, lengths 2, error byte (in an int32 slot)
+        h_in = torch.empty(2 * L + 1, dtype=torch.int32, pin_memory=True)
+        d_in = torch.empty(2 * L + 1, dtype=torch.int32, device=dev)
+        d_out = torch.zeros(n, dtype=torch.int32, device=dev)
+        h_out = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        st = cache[key] = (h_in, d_in, d_out, h_out)
+    return st
 
 
 def raise_for_err(code: int, where: str = "ACMove") -> None:
@@ -66,14 +90,25 @@ def ACMove(move_id, presentation, max_relator_length, lengths=None, cyclical=Tru
     L = int(max_relator_length)
     assert p.shape == (2 * L,), f"presentation must have length 2*max_relator_length = {2 * L}"
     dev = _device(device)
+    if in_packed_domain(p, L):
+        h_in, d_in, d_out, h_out = _stage(dev, L)
+        hv = h_in.numpy()
+        hv[: 2 * L] = p
+        hv[2 * L] = int(move_id)
+        d_in.copy_(h_in, non_blocking=True)
+        # the kernel always writes the error byte; the slot's other bytes stay 0 from allocation
+        err = d_out.view(torch.uint8)[4 * (2 * L + 2) : 4 * (2 * L + 2) + 1]
+        ops.step(d_in[: 2 * L].view(1, 2 * L), d_in[2 * L :], state_out=d_out[: 2 * L].view(1, 2 * L),
+                 cyclical=bool(cyclical), lengths=d_out[2 * L : 2 * L + 2].view(1, 2), err=err)
+        h_out.copy_(d_out, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        host = h_out.numpy()
+        # the error byte is the low byte of the last int32 slot (little-endian)
+        raise_for_err(int(host[2 * L + 2]) & 0xff)
+        return host[: 2 * L].astype(_out_dtype(p)), [int(host[2 * L]), int(host[2 * L + 1])]
     s = torch.as_tensor(p.astype(np.int32)).reshape(1, 2 * L).to(dev)
     a = torch.tensor([int(move_id)], dtype=torch.int32, device=dev)
-    if in_packed_domain(p, L):
-        lens = torch.empty((1, 2), dtype=torch.int32, device=dev)
-        err = torch.empty((1,), dtype=torch.uint8, device=dev)
-        out = ops.step(s, a, cyclical=bool(cyclical), lengths=lens, err=err)
-    else:
-        out, lens, _, err = ops.word_move(s, a, cyclical=bool(cyclical))
+    out, lens, _, err = ops.word_move(s, a, cyclical=bool(cyclical))
     host = torch.cat([out.reshape(-1), lens.reshape(-1), err.to(torch.int32)]).cpu().numpy()
     raise_for_err(int(host[-1]))
     return host[: 2 * L].astype(_out_dtype(p)), [int(host[2 * L]), int(host[2 * L + 1])]

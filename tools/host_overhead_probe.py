@@ -55,4 +55,21 @@ g.replay()
 e1.record()
 torch.cuda.synchronize()
 res["graph_replay_us_per_step"] = e0.elapsed_time(e1) / 100 * 1e3
+# the reference's per-call APIs at B = 1: ACMove (ac_moves.py:159) and ACEnv.step (ac_env.py:91)
+import numpy as np  # noqa: E402
+
+p = np.zeros(72, np.int64)
+p[:7] = [1, 1, 1, -2, -2, -2, -2]
+p[36:42] = [1, 2, 1, -2, -1, -2]
+acx.ACMove(5, p, 36)
+t0 = time.perf_counter()
+for i in range(2000):
+    acx.ACMove(4 + i % 8, p, 36)
+res["acmove_us"] = (time.perf_counter() - t0) / 2000 * 1e6
+e = acx.ACEnv(acx.ACEnvConfig(initial_state=p))
+e.step(5)
+t0 = time.perf_counter()
+for i in range(2000):
+    e.step(4 + i % 8)
+res["acenv_step_us"] = (time.perf_counter() - t0) / 2000 * 1e6
 print(json.dumps(res))
