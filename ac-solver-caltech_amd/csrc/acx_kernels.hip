@@ -463,6 +463,20 @@ struct FastTile {
         return (x0 != 0u ? 1u : 0u) | (x1 != 0u ? 2u : 0u);
     }
 
+    // relator h1 of the lane's row only: a clean move changes just its target relator, so the
+    // rollout keeps the LDS tile as the int8 image of the current states and re-images one half
+    // per step (the trajectory store then reads the whole tile)
+    __device__ __forceinline__ void unpack_half(int lane, const PresRegs<NW>& p, bool h1) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const Word<NW> w = wsel<NW>(h1, p.w1, p.w0);
+        const int n8 = 8 * (h1 ? p.n1 : p.n0);
+        uint32_t* dst = lds + ln * S + (h1 ? HALF : 0);
+#pragma unroll
+        for (int k = 0; k < HALF; ++k)
+            dst[k] = codes_to_i8x4((w.w[k >> 2] >> (8 * (k & 3))) & 0xffu, clamp_bits(n8 - 32 * k));
+    }
+
     __device__ __forceinline__ void set_dirty(int lane, uint32_t m) const { dirty[lane] = (uint8_t)m; }
 
     // In-place state store (g is the row block the tile was loaded from): only the 16-byte
@@ -726,6 +740,26 @@ struct CodeTile {
     }
 
     __device__ __forceinline__ void unpack(int lane, const PresRegs<NW>& p) const { unpack_impl<false>(lane, p); }
+    // see FastTile::unpack_half
+    __device__ __forceinline__ void unpack_half(int lane, const PresRegs<NW>& p, bool h1) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const Word<NW> w = wsel<NW>(h1, p.w1, p.w0);
+        const int n = h1 ? p.n1 : p.n0;
+        uint32_t* dst = lds + ln * S + (h1 ? HALF / 2 : 0);
+#pragma unroll
+        for (int k = 0; k < HALF; k += 4) {
+            uint32_t sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kk = k + j;
+                const int nin = n - 4 * kk;
+                const uint32_t nz4 = nin >= 4 ? 0xfu : (nin <= 0 ? 0u : ((1u << nin) - 1u));
+                sl[j] = ((w.w[kk >> 2] >> (8 * (kk & 3))) & 0xffu) | (nz4 << 8);
+            }
+            *reinterpret_cast<uint2*>(dst + k / 2) = make_uint2(sl[0] | (sl[1] << 16), sl[2] | (sl[3] << 16));
+        }
+    }
     // see FastTile::unpack_dirty; the slots compared are canonical (codes of absent letters
     // masked to 0, as load writes them)
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
@@ -985,6 +1019,10 @@ struct GenericTile {
         int8_t* r = row(lane);
         unpack_relator(r, p.w0, p.n0);
         unpack_relator(r + L, p.w1, p.n1);
+    }
+    // relator h1 of the lane's row only (the rollout's clean moves change one relator)
+    __device__ __forceinline__ void unpack_half(int lane, const PresRegs<NW>& p, bool h1) const {
+        unpack_relator(row(lane) + (h1 ? L : 0), wsel<NW>(h1, p.w1, p.w0), h1 ? p.n1 : p.n0);
     }
     // runtime-L tiles (parity tests at any L) track no dirty relators: every row is written
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
@@ -1307,9 +1345,13 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         int ln = w.lane;
         asm volatile("" : "+v"(ln));
         bool reset = false;
+        bool both = false;  // the LDS image needs both relators (general move: both reduced)
+        bool h1 = false;    // the moved relator (ac_moves.py:167-179: i = (id + 1) & 1)
         if (w.active) {
             const int act = (int)id;
             int e;
+            both = !clean;
+            h1 = ((act + 1) & 1) != 0;
             if (bad) e = ACX_ERR_DOMAIN;
             else if (clean) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
             else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
@@ -1325,12 +1367,14 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             if (reset) cnt = 0;
         }
         const uint64_t rb = __ballot(reset);
+        bool reloaded = false;  // wave-uniform: the whole tile now holds starting rows
         if (rb) {  // same-step autoreset to the starting states
             bool rbad = false;
             if (__popcll(rb) > RESET_TILE_MIN) {  // many lanes: one coalesced tile reload
                 tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
                 if (reset) rbad = tile.pack(w.lane, p);
                 wave_sync();
+                reloaded = true;
             } else {  // a few lanes: the wave loads just their rows
                 tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
                 if (reset) rbad = tile.pack(w.lane, p);
@@ -1342,7 +1386,13 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             }
         }
         if constexpr (OBS != 0) {
-            if (w.active && !bad) tile.unpack(w.lane, p);
+            // the LDS tile stays the int8 image of the current states: a clean move re-images
+            // its target relator, a general move both; a row reset by load_rows already holds its
+            // starting row; after a whole-tile reload every row is re-imaged
+            if (w.active && !bad) {
+                if (reloaded || both) tile.unpack(w.lane, p);
+                else if (!reset) tile.unpack_half(w.lane, p, h1);
+            }
             wave_sync();
             if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
             else tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, w.lane);
