@@ -337,7 +337,9 @@ class VecACEnv:
 
     def rollout(self, actions: torch.Tensor, obs_traj: Optional[torch.Tensor] = None, reward_traj=None,
                 done_traj=None, trunc_traj=None):
-        """T = actions.shape[0] steps in one launch; trajectories optional (T, B, ...)."""
+        """T = actions.shape[0] steps in one launch; trajectories optional (T, B, ...).  obs_traj
+        is int32, or int8 -- the observation_space dtype (ac_env.py:64-70) and what
+        SyncVectorEnv returns -- at a quarter of the bytes."""
         ops.rollout(self.state, actions, self.reset_state, self.step_count, horizon=self.horizon_length,
                     cyclical=self.cyclical, obs_traj=obs_traj, reward_traj=reward_traj, done_traj=done_traj,
                     trunc_traj=trunc_traj, err=self.err, err_count=self.err_count)
