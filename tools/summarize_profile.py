@@ -61,9 +61,11 @@ if bench:
     # the timed launch = the last (in time) of the longest rollout_kernel dispatches (the warmup
     # launch comes first) plus, when ops.rollout packed the move ids first, the matching
     # pack_actions_kernel dispatch
-    # the int32-trajectory instantiation (rollout_kernel<.., 1>; `true` before round 2's int8 mode)
+    # the int32-trajectory instantiation: rollout_kernel<NW, LC, VEC, 1, PK> (round 2's int8 mode is
+    # OBS = 2; before it the parameter was `true`, and before the PK parameter it ended there)
+    import re
     timed = [v for n, v in summary["kernels"].items()
-             if "rollout_kernel" in n and (n.split("(")[0].endswith(", 1>") or n.split("(")[0].endswith("true>"))]
+             if re.search(r"rollout_kernel<\d+, \d+, \d+, (1|true)(, (true|false))?>", n)]
     packs = [v for n, v in summary["kernels"].items() if "pack_actions_kernel" in n]
 
     def hbm(k, i):
