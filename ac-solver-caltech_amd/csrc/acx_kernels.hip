@@ -1781,6 +1781,130 @@ __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) 
     if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
 }
 
+// expand12 with int32 children for compile-time L % 4 == 0 (L = 36 and 128): the block makes its
+// 64 x 12 children exactly as expand12_keys_kernel (wave 0 packs the parents, wave w the actions
+// 3w..3w+2), stages each child in LDS as packed words (both relators' 2-bit codes and the two
+// lengths: 2 NW + 1 dwords), then all 256 threads expand the staged children into the block's
+// contiguous 64 x 12 x 2L int32 region with 16-byte stores, consecutive threads on consecutive
+// chunks -- the whole 221 KB (L = 36) as one linear stream per block.  Out-of-domain parents'
+// children are copies of the parent row; lengths come from the staged words, error codes from LDS.
+template <int NW, int LC, int VEC>
+struct ExpandRowsSmem {
+    static constexpr int SW = 2 * NW + 1;  // staged dwords per child
+    static __host__ __device__ size_t region_a(int L) {
+        const size_t t = TileFor<NW, LC, VEC>::wave_bytes(L);
+        const size_t k = (size_t)WAVE * 12 * SW * 4;
+        return ((t > k ? t : k) + 15) & ~(size_t)15;
+    }
+    static __host__ __device__ size_t err_off(int L) { return region_a(L) + (size_t)WAVE * packed_words<NW>() * 4; }
+    static __host__ __device__ size_t bytes(int L) { return err_off(L) + (size_t)WAVE * 12; }
+};
+
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK) void expand12_rows_kernel(ExpandArgs a) {
+    static_assert(LC > 0 && LC % 4 == 0, "compile-time L, whole 16-byte chunks per relator");
+    using Tile = TileFor<NW, LC, VEC>;
+    using Smem = ExpandRowsSmem<NW, LC, VEC>;
+    constexpr int PW = packed_words<NW>();
+    constexpr int SW = Smem::SW;
+    constexpr int L = LC, CPR = LC / 2, HC = LC / 4;  // 16-byte chunks per row / per relator
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t r0 = (int64_t)blockIdx.x * WAVE;
+    if (r0 >= a.N) return;  // block-uniform
+    const int R = (int)((a.N - r0) < WAVE ? (a.N - r0) : WAVE);
+    uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::region_a(a.L));
+    uint8_t* err_st = reinterpret_cast<uint8_t*>(smem + Smem::err_off(a.L));
+    const bool cyc = a.cyclical != 0;
+    if (wid == 0) {
+        Tile tile(smem, a.L);
+        tile.load(a.parents + r0 * 2 * L, R, lane);
+        if (lane < R) {
+            PresRegs<NW> p;
+            const bool bad = tile.pack(lane, p);
+            const bool clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+            uint32_t* d = packed + lane * PW;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                d[k] = p.w0.w[k];
+                d[NW + k] = p.w1.w[k];
+            }
+            d[2 * NW] = (uint32_t)p.n0 | ((uint32_t)p.n1 << 8);
+            d[2 * NW + 1] = (uint32_t)bad | ((uint32_t)clean << 1);
+        }
+    }
+    __syncthreads();  // the tile is dead from here: region a holds the staged children
+    uint32_t* stw = reinterpret_cast<uint32_t*>(smem);
+    int nerr = 0;
+    if (lane < R) {
+        PresRegs<NW> p;
+        const uint32_t* d = packed + lane * PW;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            p.w0.w[k] = d[k];
+            p.w1.w[k] = d[NW + k];
+        }
+        p.n0 = (int)(d[2 * NW] & 0xffu);
+        p.n1 = (int)((d[2 * NW] >> 8) & 0xffu);
+        const bool bad = (d[2 * NW + 1] & 1u) != 0, clean = (d[2 * NW + 1] & 2u) != 0;
+        const int64_t par = r0 + lane;
+#pragma unroll 1
+        for (int j = 0; j < KEYS_APW; ++j) {
+            const int act = wid * KEYS_APW + j;
+            PresRegs<NW> q = p;
+            int e;
+            if (bad) e = ACX_ERR_DOMAIN;
+            else if (clean) e = ac_move_clean<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            else e = ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, L, cyc);
+            nerr += e != ACX_ERR_NONE;
+            err_st[lane * 12 + act] = (uint8_t)e;
+            if (a.child_key) {  // keys as well (not the search path): per lane, unstaged
+                PresRegs<NW> kq = q;
+                if (e != ACX_ERR_NONE) {
+                    kq.n0 = 0xff;
+                    kq.n1 = 0xff;
+                }
+                store_key<NW>(a.child_key + (par * 12 + act) * a.kw64, a.kw64, L, kq);
+            }
+            uint32_t* c = stw + (lane * 12 + act) * SW;  // odd stride: conflict-free
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                c[k] = q.w0.w[k];
+                c[NW + k] = q.w1.w[k];
+            }
+            c[2 * NW] = (uint32_t)q.n0 | ((uint32_t)q.n1 << 8);
+        }
+    }
+    __syncthreads();
+    int4* dst = reinterpret_cast<int4*>(a.children + r0 * 12 * 2 * L);
+    const int nch = R * 12 * CPR;
+    for (int i = threadIdx.x; i < nch; i += BLOCK) {
+        const int ci = i / CPR, k = i - ci * CPR;  // child (parent-major), 16-byte chunk of its row
+        const int pp = ci / 12;
+        int4 v;
+        if (packed[pp * PW + 2 * NW + 1] & 1u) {  // out-of-domain parent: its row, as is
+            v = reinterpret_cast<const int4*>(a.parents + (r0 + pp) * 2 * L)[k];
+        } else {
+            const uint32_t* c = stw + ci * SW;
+            const int h = k >= HC ? 1 : 0, m = k - h * HC;
+            const uint32_t c8 = (c[h * NW + (m >> 2)] >> (8 * (m & 3))) & 0xffu;
+            const int n = (int)((c[2 * NW] >> (8 * h)) & 0xffu);
+            v = widen4(codes_to_i8x4(c8, clamp_bits(8 * n - 32 * m)));
+        }
+        dst[i] = v;
+    }
+    if (a.child_len) {
+        int32_t* ld = a.child_len + r0 * 24;
+        for (int i = threadIdx.x; i < R * 24; i += BLOCK) ld[i] = (int32_t)((stw[(i >> 1) * SW + 2 * NW] >> (8 * (i & 1))) & 0xffu);
+    }
+    if (a.err) {
+        uint8_t* ed = a.err + r0 * 12;
+        for (int i = threadIdx.x; i < R * 12; i += BLOCK) ed[i] = err_st[i];
+    }
+    if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
+}
+
 struct CanonArgs {
     const int32_t* state_in;
     int32_t* state_out;
@@ -1928,6 +2052,13 @@ struct ExpandLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
+        if constexpr (LC > 0 && LC % 4 == 0) {
+            const size_t rshm = ExpandRowsSmem<NW, LC, VEC>::bytes(a.L);
+            if (a.children && rshm <= 64 * 1024) {
+                expand12_rows_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), rshm, s>>>(a);
+                return finish_launch();
+            }
+        }
         const size_t cshm = ExpandChildrenSmem<NW, LC, VEC>::bytes(a.L);
         if (a.children && cshm <= 64 * 1024) {
             expand12_children_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), cshm, s>>>(a);
