@@ -239,6 +239,36 @@ struct FastTile {
         wave_sync();
     }
 
+    // all BLOCK threads load R rows into this tile (the block's one): consecutive threads on
+    // consecutive 16-byte chunks, every load issued before any conversion; flags as load().
+    // Block-wide barriers before and after (the expand kernels' shared parent tile: a quarter of
+    // the per-lane round trips of one wave loading all 64 rows while three wait).
+    __device__ __forceinline__ void load_block(const int32_t* __restrict__ g, int R) {
+        constexpr int U = (WAVE * CPR + BLOCK - 1) / BLOCK;
+        if (threadIdx.x < WAVE) flags[threadIdx.x] = 0;
+        __syncthreads();
+        const int nc = R * CPR;
+        const int4* src = reinterpret_cast<const int4*>(g);
+        int4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = (int)threadIdx.x + u * BLOCK;
+            if (c < nc) v[u] = src[c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = (int)threadIdx.x + u * BLOCK;
+            if (c >= nc) continue;
+            bool bad = false;
+            const uint32_t q = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) | (to_i8(v[u].z, bad) << 16) |
+                               (to_i8(v[u].w, bad) << 24);
+            const int r = c / CPR;
+            lds[r * S + (c - r * CPR)] = q;
+            if (bad) flags[r] = 1;
+        }
+        __syncthreads();
+    }
+
     // the rows of the lanes in the wave-uniform mask `rows` only (a few resetting envs),
     // cooperatively: lane l loads 16-byte chunk l % CPR of the (l / CPR)-th selected row, so a
     // wave-instruction fetches 64 / CPR whole rows (3 at L = 36) with one round trip per group
@@ -603,6 +633,34 @@ struct CodeTile {
         }
         tile_bad = __any(any_bad);
         wave_sync();
+    }
+
+    // see FastTile::load_block
+    __device__ __forceinline__ void load_block(const int32_t* __restrict__ g, int R) {
+        constexpr int U = (WAVE * CPR + BLOCK - 1) / BLOCK;
+        if (threadIdx.x < WAVE) flags[threadIdx.x] = 0;
+        __syncthreads();
+        const int nc = R * CPR;
+        const int4* src = reinterpret_cast<const int4*>(g);
+        int4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = (int)threadIdx.x + u * BLOCK;
+            if (c < nc) v[u] = src[c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = (int)threadIdx.x + u * BLOCK;
+            if (c >= nc) continue;
+            bool bad = false;
+            const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) | (to_i8(v[u].z, bad) << 16) |
+                               (to_i8(v[u].w, bad) << 24);
+            uint32_t c8, nz4;
+            swar_pack4(d, c8, nz4);
+            put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+            if (bad) flags[c / CPR] = 1;
+        }
+        __syncthreads();
     }
 
     // the rows of the lanes in `rows` only (see FastTile::load_rows); a row is >= one
@@ -1629,9 +1687,10 @@ __global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
     char* region = smem;
     uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::region_a(a.L));
     const bool cyc = a.cyclical != 0;
+    Tile tile(region, a.L);
+    if constexpr (LC > 0 && LC % 4 == 0) tile.load_block(a.parents + r0 * 2 * L, R);
+    else if (wid == 0) tile.load(a.parents + r0 * 2 * L, R, lane);
     if (wid == 0) {
-        Tile tile(region, a.L);
-        tile.load(a.parents + r0 * 2 * L, R, lane);
         if (lane < R) {
             PresRegs<NW> p;
             const bool bad = tile.pack(lane, p);
@@ -1817,9 +1876,9 @@ __global__ __launch_bounds__(BLOCK) void expand12_rows_kernel(ExpandArgs a) {
     uint32_t* packed = reinterpret_cast<uint32_t*>(smem + Smem::region_a(a.L));
     uint8_t* err_st = reinterpret_cast<uint8_t*>(smem + Smem::err_off(a.L));
     const bool cyc = a.cyclical != 0;
+    Tile tile(smem, a.L);
+    tile.load_block(a.parents + r0 * 2 * L, R);
     if (wid == 0) {
-        Tile tile(smem, a.L);
-        tile.load(a.parents + r0 * 2 * L, R, lane);
         if (lane < R) {
             PresRegs<NW> p;
             const bool bad = tile.pack(lane, p);
