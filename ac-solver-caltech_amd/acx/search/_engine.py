@@ -128,6 +128,8 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
     L = len(p) // 2
     if np.any(np.abs(p) > 2):
         raise ValueError("acx presentations use letters +-1 (x) and +-2 (y) only")
+    if engine not in (None, "device", "host"):
+        raise ValueError(f"engine must be 'device' or 'host', not {engine!r}")
     if mode == GREEDY and engine in (None, "device") and not isinstance(device, (list, tuple)):
         return run_greedy_device(p, max_nodes_to_explore, verbose, cyclical, device, batch, keep_node_keys)
     devs = _devices(device)

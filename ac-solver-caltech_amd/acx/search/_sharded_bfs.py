@@ -24,14 +24,14 @@ from .. import _lib
 from ..envs.utils import is_array_valid_presentation
 
 LAST_STATS = {}  # statistics of the most recent sharded search on this rank
-_HANDLES = {}  # (device, L, cyclical, chunk, local_cap, rank, world) -> handle
+_HANDLES = {}  # (device, L, cyclical, chunk, local_cap, rank, world, exchange) -> handle
 NONE = 0xFFFFFFFF
 
 
 class _Comm:
     """The three exchanges of a chunk over a process group (or none)."""
 
-    def __init__(self, group, dev):
+    def __init__(self, group, dev, always=False):
         self.group = group
         self.dev = dev
         if dist.is_available() and dist.is_initialized():
@@ -40,10 +40,13 @@ class _Comm:
             self.device_collectives = dist.get_backend(group) == "nccl"
         else:
             self.rank, self.world, self.device_collectives = 0, 1, True
+        # `always`: run the collectives even in a one-rank group (which needs none), so the RCCL
+        # device-tensor branch executes on a single GPU (tests/test_gpu_sbfs.py)
+        self.local = self.world == 1 and not (always and dist.is_available() and dist.is_initialized())
 
     def all_gather_rows(self, row: np.ndarray) -> np.ndarray:
         """(world, n) int64: every rank's row."""
-        if self.world == 1:
+        if self.local:
             return row[None, :].copy()
         dev = self.dev if self.device_collectives else torch.device("cpu")
         t = torch.as_tensor(row, dtype=torch.int64, device=dev)
@@ -52,7 +55,7 @@ class _Comm:
         return torch.stack(out).cpu().numpy()
 
     def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits) -> None:
-        if self.world == 1:
+        if self.local:
             n = int(send_splits[0])
             recv[:n].copy_(send[:n])
             return
@@ -64,7 +67,7 @@ class _Comm:
         recv.copy_(r)
 
     def all_reduce_sum_(self, t: torch.Tensor) -> None:
-        if self.world == 1:
+        if self.local:
             return
         if self.device_collectives:
             dist.all_reduce(t, group=self.group)
@@ -80,8 +83,8 @@ class _Comm:
         return self.all_gather_rows(np.asarray(row, dtype=np.int64)).min(axis=0)
 
 
-def _handle(lib, dev, L, cyc, chunk, lcap, rank, world):
-    key = (dev.index, L, bool(cyc), int(chunk), int(lcap), rank, world)
+def _handle(lib, dev, L, cyc, chunk, lcap, rank, world, exchange):
+    key = (dev.index, L, bool(cyc), int(chunk), int(lcap), rank, world, bool(exchange))
     h = _HANDLES.get(key)
     if h is not None:
         return h
@@ -93,7 +96,7 @@ def _handle(lib, dev, L, cyc, chunk, lcap, rank, world):
     nrec = lib.acx_sbfs_max_records(ptr)
     kw = _lib.key_words(L)
     send = torch.empty(nrec * (kw + 1), dtype=torch.int64, device=dev)
-    recv = torch.empty(nrec * (kw + 1) if world > 1 else 0, dtype=torch.int64, device=dev)
+    recv = torch.empty(nrec * (kw + 1) if exchange else 0, dtype=torch.int64, device=dev)
     mask = torch.empty(max(int(chunk), 1), dtype=torch.int32, device=dev)
     h = (ptr, send, recv, mask)
     _HANDLES[key] = h
@@ -139,10 +142,11 @@ def _trace_chunk(lib, h, comm, buf, running, end_seq, stream, ok, agree, lines):
 
 
 def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclically_reduce_after_moves=False,
-                device=None, chunk=0, group=None, keep_node_keys=False):
+                device=None, chunk=0, group=None, keep_node_keys=False, always_exchange=False):
     """(True, path) | (False, None), as breadth_first.py:15-97; SPMD over the ranks of `group`
     (default: the default process group, if initialised).  chunk = parents per round (0: 2^19).
-    keep_node_keys: LAST_STATS["node_keys"] / ["node_ids"] = this rank's nodes (ascending id)."""
+    keep_node_keys: LAST_STATS["node_keys"] / ["node_ids"] = this rank's nodes (ascending id).
+    always_exchange: run the exchanges through torch.distributed even in a one-rank group."""
     p = np.asarray(presentation)
     assert is_array_valid_presentation(p), f"{p} is not a valid presentation"
     if np.any(np.abs(p) > 2):
@@ -154,7 +158,7 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     dev = torch.device(device if device is not None else "cuda")
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
-    comm = _Comm(group, dev)
+    comm = _Comm(group, dev, always=always_exchange)
     chunk = int(chunk) if chunk else 1 << 19
     lcap = local_capacity(max_nodes, comm.world)
     lib = _lib.load()
@@ -164,7 +168,7 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     local_err = None
     try:
         h, send, recv, gmask = _handle(lib, dev, L, cyclically_reduce_after_moves, chunk, lcap, comm.rank,
-                                       comm.world)
+                                       comm.world, not comm.local)
     except _lib.ACXError as e:
         local_err = e
     if comm.sum_rows([local_err is not None])[0]:
@@ -210,10 +214,10 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
             recv_counts = rows[:, 5 + comm.rank]
             nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
             ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
-            if W > 1:
+            if not comm.local:
                 comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
                                 [int(c) * rw for c in send_counts])
-            src = recv if W > 1 else send  # one rank: the records it sent are the ones it owns
+            src = send if comm.local else recv  # one rank alone: the records it sent are the ones it owns
             end = min(succ_seq, err_seq)
             ok(lib.acx_sbfs_insert(h, src.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
             comm.all_reduce_sum_(gmask[:P])
@@ -277,7 +281,8 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
 
     LAST_STATS.clear()
     LAST_STATS.update(nodes=int(n_nodes), parents=int(parents), chunks=int(chunks), min_length=int(min_len),
-                      status=int(status), rank=comm.rank, world=W)
+                      status=int(status), rank=comm.rank, world=W,
+                      exchange="local" if comm.local else "device" if comm.device_collectives else "host")
     if keep_node_keys:
         n = lib.acx_sbfs_node_keys(h, None, None, 0)
         nk = np.zeros((max(n, 0), kw), np.uint64)

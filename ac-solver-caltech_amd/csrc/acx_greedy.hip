@@ -51,6 +51,8 @@ constexpr int64_t AGE = 1 << 16;  // a cached expansion stays usable while fewer
                                   // nodes are re-expanded with the next batches instead of costing
                                   // a round each at the top of the frontier (r02u: ~40k rounds)
 static int64_t g_age_override = 0;  // tests only (acx_internal_greedy_age): a smaller AGE
+static int64_t g_dcap_override = 0;  // tests only (acx_internal_greedy_init_cap): a smaller INIT_DCAP
+constexpr int64_t INIT_DCAP = (int64_t)1 << 22;  // nodes of the first device store (doubled as needed)
 constexpr int DEFAULT_BATCH = 64;  // parents per round (tools/greedy_sweep.py: 64-128 best on AK(3) /
                                    // Miller-Schupp at 10^6 nodes; larger rounds mostly expand nodes
                                    // that are never popped)
@@ -158,6 +160,8 @@ static inline int64_t now_ns() {
 struct Engine {
     int L = 0, kw = 0, pk = 0, cyc = 0, dev = 0;
     int64_t max_nodes = 0, cap = 0;
+    int64_t dcap = 0;  // nodes the device key store / visited set hold now (grown by doubling)
+    uint64_t tsize = 0;
     int batch_cap = DEFAULT_BATCH;
     int64_t age = AGE;
     // nodes (ids in discovery order)
@@ -238,28 +242,61 @@ struct Engine {
         age = g_age_override > 0 ? g_age_override : AGE;  // a power of two
         if (hipGetDevice(&dev) != hipSuccess) return false;
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
-        uint64_t ts = 1024;
-        while (ts < 2 * (uint64_t)cap) ts <<= 1;
         commit_cap = 4 * (int64_t)batch_cap * ACT + 64;
         const size_t nb = (size_t)batch_cap;
         const size_t in_words = (nb + (size_t)commit_cap) * kw, out_words = nb * ACT * (kw + 2);
-        bool ok = hipMalloc((void**)&d.nkeys, (size_t)cap * kw * 8) == hipSuccess &&
-                  hipMalloc((void**)&d.table, ts * 8) == hipSuccess &&
-                  hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocMapped) == hipSuccess &&
-                  hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocMapped) == hipSuccess &&
-                  hipHostGetDevicePointer((void**)&hd_in, h_in, 0) == hipSuccess &&
-                  hipHostGetDevicePointer((void**)&hd_out, h_out, 0) == hipSuccess &&
-                  hipMemsetAsync(d.table, 0, ts * 8, stream) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
-            return false;
-        }
-        d.bmask = ts / BUCKET - 1;
         d.L = L;
         d.kw = kw;
         d.cyc = cyc;
+        bool ok = hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocMapped) == hipSuccess &&
+                  hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocMapped) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&hd_in, h_in, 0) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&hd_out, h_out, 0) == hipSuccess;
+        // the device store starts at min(budget, INIT_DCAP) nodes and doubles as the search grows
+        // (the reference's set grows with the search: a large budget on a search that ends early
+        // must not fail on an up-front allocation)
+        ok = ok && grow(std::min<int64_t>(cap, g_dcap_override > 0 ? g_dcap_override : INIT_DCAP));
+        if (!ok) (void)hipGetLastError();
+        return ok;
+    }
+
+    // (re)allocate the device key store for n >= dcap nodes and a visited set of load <= 1/2,
+    // keeping the committed nodes: their keys are copied and re-entered in the new table
+    bool grow(int64_t n) {
+        uint64_t ts = 1024;
+        while (ts < 2 * (uint64_t)n) ts <<= 1;
+        uint64_t *nk = nullptr, *tb = nullptr;
+        if (hipMalloc((void**)&nk, (size_t)n * kw * 8) != hipSuccess) return false;
+        if (hipMalloc((void**)&tb, ts * 8) != hipSuccess) {
+            (void)hipFree(nk);
+            return false;
+        }
+        bool ok = hipMemsetAsync(tb, 0, ts * 8, stream) == hipSuccess;
+        if (ok && committed > 0)
+            ok = hipMemcpyAsync(nk, d.nkeys, (size_t)committed * kw * 8, hipMemcpyDeviceToDevice, stream) == hipSuccess;
+        if (ok && wait() == ACX_OK) {
+            if (d.nkeys) (void)hipFree(d.nkeys);
+            if (d.table) (void)hipFree(d.table);
+        } else {
+            (void)hipFree(nk);
+            (void)hipFree(tb);
+            return false;
+        }
+        d.nkeys = nk;
+        d.table = tb;
+        d.bmask = ts / BUCKET - 1;
+        dcap = n;
+        tsize = ts;
+        if (committed > 0) {  // re-enter every committed node (the commit kernel rewrites its own key)
+            d.commit = d.nkeys;
+            d.lo = 0;
+            d.hi = committed;
+            commit_launch();
+            if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return false;
+        }
         return true;
     }
+    void commit_launch();
 
     // ---------------------------------------------------------------- key helpers
     int len_field(const uint64_t* k, int h) const {
@@ -436,9 +473,13 @@ struct Engine {
         return id;
     }
 
+    // A cached expansion is usable while the whole visit stays inside the in-flight table's
+    // reach: the visit appends up to ACT nodes, and an append that starts a new generation
+    // keeps only the `age` ids before it (recent_insert), so every id >= `from` must still be
+    // there after the visit's last append: parent.size() + ACT - from <= age.
     bool usable(int64_t id) const {
         const int32_t s = cache_slot[id];
-        return s >= 0 && (int64_t)parent.size() - n_at_round[c_round[s]] <= age;
+        return s >= 0 && (int64_t)parent.size() + ACT - n_at_round[c_round[s]] <= age;
     }
     void drop_cache(int64_t id) {
         const int32_t s = cache_slot[id];
@@ -510,7 +551,7 @@ struct Engine {
         out.clear();
         // retire the caches that aged since the last round: their nodes are unexpanded again
         const int64_t nn = (int64_t)parent.size();
-        while (fifo_head < cache_fifo.size() && nn - n_at_round[cache_fifo[fifo_head].first] > age) {
+        while (fifo_head < cache_fifo.size() && nn + ACT - n_at_round[cache_fifo[fifo_head].first] > age) {
             const auto [r, id] = cache_fifo[fifo_head++];
             const int32_t sl = cache_slot[id];
             if (sl >= 0 && c_round[sl] == r) {
@@ -624,9 +665,15 @@ struct CommitLaunch {
     }
 };
 
+void Engine::commit_launch() {
+    CommitLaunch cl{this};
+    bfs::by_nw(L, cl);
+}
+
 int Engine::expand_round(const std::vector<int64_t>& batch) {
     const int n = (int)batch.size();
     const int64_t n_nodes = (int64_t)parent.size();
+    if (n_nodes > dcap && !grow(std::min<int64_t>(cap, std::max<int64_t>(2 * dcap, n_nodes)))) return ACX_E_LAUNCH;
     // staging in: the batch's parent keys, then the keys of the nodes appended since the last
     // round (committed to the device visited set before the expansion probes it)
     for (int i = 0; i < n; ++i) memcpy(h_in + (size_t)i * kw, &keys[(size_t)batch[i] * kw], 8 * kw);
@@ -639,8 +686,7 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
             d.commit = hd_in + (size_t)n * kw;
             d.lo = lo;
             d.hi = hi;
-            CommitLaunch cl{this};
-            bfs::by_nw(L, cl);
+            commit_launch();
         }
         lo = hi;
         if (lo >= n_nodes) break;
@@ -697,7 +743,7 @@ extern "C" {
 
 int acx_greedy_run(const int32_t* presentation, int32_t L, int64_t max_nodes, int32_t cyclical, int32_t batch,
                    void** out_handle) {
-    if (!presentation || !out_handle || L < 1 || L > ACX_MAX_L || max_nodes < 1 || max_nodes > (1ll << 31))
+    if (!presentation || !out_handle || L < 1 || L > ACX_MAX_L || max_nodes < 1 || max_nodes > (1ll << 38))
         return ACX_E_ARG;
     *out_handle = nullptr;
     Engine* E = new (std::nothrow) Engine();
@@ -716,6 +762,9 @@ void acx_greedy_destroy(void* h) { delete static_cast<Engine*>(h); }
 // tests only (not in acx.h): searches started afterwards use 2^log2_age as the cache age limit
 // (0: the default AGE), so the retirement of aged caches is exercised harder at test sizes
 void acx_internal_greedy_age(int32_t log2_age) { g_age_override = log2_age > 0 ? (int64_t)1 << log2_age : 0; }
+// tests only: searches started afterwards begin with a 2^log2_cap-node device store (0: INIT_DCAP),
+// so the store's regrowth mid-search is exercised at test sizes
+void acx_internal_greedy_init_cap(int32_t log2_cap) { g_dcap_override = log2_cap > 0 ? (int64_t)1 << log2_cap : 0; }
 
 // 0 running, 1 success, 2 failed, 3 move error; budget_hit, min_length, nodes (len(tree_nodes))
 int32_t acx_greedy_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {

@@ -145,6 +145,16 @@ __device__ __forceinline__ uint32_t codes_to_i8x4(uint32_t c8, uint32_t s) {
 }
 __device__ __forceinline__ uint32_t clamp_bits(int s) { return (uint32_t)(s < 0 ? 0 : (s > 32 ? 32 : s)); }
 
+// Rows outside the packed domain (a letter not in {-2..2}, a zero inside a relator) cannot be
+// held in the LDS image; the stores copy their exact int32 values from a fallback row instead,
+// chosen per row by its code in the tile's flags[]:
+//   FB_IN     the row the kernel loaded (state_in / the rollout's input state)
+//   FB_RESET  the env's starting row (reset_state): an autoreset to an out-of-domain row
+constexpr uint32_t FB_IN = 1u, FB_RESET = 2u;
+__device__ __forceinline__ const int32_t* fb_src(uint32_t code, const int32_t* fb_in, const int32_t* fb_reset) {
+    return code == FB_RESET ? fb_reset : fb_in;
+}
+
 template <int NW, int LC>
 struct FastTile {
     static_assert(LC > 0 && LC % 4 == 0, "FastTile needs a compile-time L multiple of 4");
@@ -162,18 +172,20 @@ struct FastTile {
     bool tile_bad = false;  // wave-uniform: some row of the last load was flagged
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
-    // per-row out-of-domain flags as of the tile's FIRST load (a later load of other rows
-    // replaced them); the fallback rows of store<true> follow these
-    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
-        flags[lane] = flagged;
-        tile_bad = __any(flagged);
+    // per-row fallback codes (FB_* below) replacing whatever the loads left in flags[]; the
+    // flagged rows of store<true> / store_dirty / store_rows_i8_fb copy their fallback row
+    __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
+        flags[lane] = (uint8_t)code;
+        tile_bad = __any(code != 0u);
         wave_sync();
     }
-    // additionally flag the rows of lanes with f (their store copies the fallback row)
-    __device__ __forceinline__ void flag_rows(int lane, bool f) {
-        if (f) flags[lane] = 1;
-        tile_bad = tile_bad || __any(f);
+    // additionally flag the rows of lanes with code != 0
+    __device__ __forceinline__ void flag_rows(int lane, uint32_t code) {
+        if (code) flags[lane] = (uint8_t)code;
+        tile_bad = tile_bad || __any(code != 0u);
     }
+    // int8 letter k of row r of the LDS image (the rare fallback stores)
+    __device__ __forceinline__ int32_t letter(int r, int k) const { return row(r)[k]; }
     __device__ __forceinline__ FastTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
@@ -390,10 +402,11 @@ struct FastTile {
         }
     }
 
-    // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from fallback
+    // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from their
+    // fallback row (fb_src: `fallback`, or `fallback2` for FB_RESET rows; both pitch fpitch)
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -418,7 +431,8 @@ struct FastTile {
                     const int r = c / CPR;
                     const int pos = 4 * (c - r * CPR);
                     int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
-                    if (FB && flags[r]) out16<false, F32>(dst, *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos));
+                    const uint32_t fc = FB ? flags[r] : 0u;
+                    if (fc) out16<false, F32>(dst, *reinterpret_cast<const int4*>(fb_src(fc, fallback, fallback2) + (int64_t)r * fpitch + pos));
                     else out16<NT, F32>(dst, widen4(p[u]));
                 }
             }
@@ -512,13 +526,24 @@ struct FastTile {
     // In-place state store (g is the row block the tile was loaded from): only the 16-byte
     // chunks of relators marked in dirty[] are written; every other chunk already holds its
     // value in HBM (a gated move, an unchanged relator, a failed env).  Needs set_dirty for every
-    // row of the tile and a wave_sync after it.
+    // row of the tile and a wave_sync after it.  Dirty rows flagged FB_RESET (an autoreset to an
+    // out-of-domain starting row) are copied from fallback2 (same row pitch).
     template <bool NT>
-    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
         int4* dst = reinterpret_cast<int4*>(g);
+        if (tile_bad) {  // rare (wave-uniform): per-chunk fallback test
+            for (int c = ln; c < nc; c += WAVE) {
+                const int r = c / CPR;
+                const int k = c - r * CPR;
+                if (!((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u)) continue;
+                if (flags[r] == FB_RESET) dst[c] = reinterpret_cast<const int4*>(fallback2)[c];
+                else dst[c] = widen4(lds[r * S + k]);
+            }
+            return;
+        }
 #pragma unroll
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
@@ -577,14 +602,19 @@ struct CodeTile {
     bool tile_bad = false;
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
-    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
-        flags[lane] = flagged;
-        tile_bad = __any(flagged);
+    __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
+        flags[lane] = (uint8_t)code;
+        tile_bad = __any(code != 0u);
         wave_sync();
     }
-    __device__ __forceinline__ void flag_rows(int lane, bool f) {
-        if (f) flags[lane] = 1;
-        tile_bad = tile_bad || __any(f);
+    __device__ __forceinline__ void flag_rows(int lane, uint32_t code) {
+        if (code) flags[lane] = (uint8_t)code;
+        tile_bad = tile_bad || __any(code != 0u);
+    }
+    __device__ __forceinline__ int32_t letter(int r, int k) const {
+        const uint32_t sl = slots(r)[k >> 2];
+        const uint32_t d = codes_to_i8x4(sl & 0xffu, 8u * __builtin_popcount((sl >> 8) & 0xfu));
+        return (int32_t)(int8_t)(d >> (8 * (k & 3)));
     }
     __device__ __forceinline__ CodeTile(char* base, int) {
         lds = reinterpret_cast<uint32_t*>(base);
@@ -739,7 +769,7 @@ struct CodeTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -756,7 +786,8 @@ struct CodeTile {
                 const int pos = 4 * (c - r * CPR);
                 int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
                 if (FB && tile_bad && flags[r]) {
-                    out16<false, F32>(dst, *reinterpret_cast<const int4*>(fallback + (int64_t)r * fpitch + pos));
+                    out16<false, F32>(dst, *reinterpret_cast<const int4*>(fb_src(flags[r], fallback, fallback2) +
+                                                                          (int64_t)r * fpitch + pos));
                 } else {
                     const uint32_t nz4 = (p[u] >> 8) & 0xfu;
                     out16<NT, F32>(dst, widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
@@ -827,11 +858,25 @@ struct CodeTile {
 
     // see FastTile::store_dirty
     template <bool NT>
-    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
         int4* dst = reinterpret_cast<int4*>(g);
+        if (tile_bad) {  // rare (wave-uniform): per-chunk fallback test
+            for (int c = ln; c < nc; c += WAVE) {
+                const int r = c / CPR;
+                const int k = c - r * CPR;
+                if (!((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u)) continue;
+                if (flags[r] == FB_RESET) {
+                    dst[c] = reinterpret_cast<const int4*>(fallback2)[c];
+                } else {
+                    const uint32_t sl = slots(r)[k];
+                    dst[c] = widen4(codes_to_i8x4(sl & 0xffu, 8u * __builtin_popcount((sl >> 8) & 0xfu)));
+                }
+            }
+            return;
+        }
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
             bool wr[STAGE_UNROLL];
@@ -922,13 +967,14 @@ struct GenericTile {
     __device__ __forceinline__ void store_rows_i8(int8_t* g, int R, int lane) const {
         for (int i = lane; i < R * twoL; i += WAVE) g[i] = row(i / twoL)[i % twoL];
     }
-    __device__ __forceinline__ void restore_flags(int lane, bool flagged) {
-        flags[lane] = flagged;
+    __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
+        flags[lane] = (uint8_t)code;
         wave_sync();
     }
-    __device__ __forceinline__ void flag_rows(int lane, bool f) {
-        if (f) flags[lane] = 1;
+    __device__ __forceinline__ void flag_rows(int lane, uint32_t code) {
+        if (code) flags[lane] = (uint8_t)code;
     }
+    __device__ __forceinline__ int32_t letter(int r, int k) const { return row(r)[k]; }
     // the rows of the lanes in `rows` only, row by row (the generic-L instantiations serve
     // parity, not speed)
     __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
@@ -1006,7 +1052,7 @@ struct GenericTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         const int nc = (R * twoL) / VEC;
         It it(lane, twoL);
         for (int b0 = lane; b0 < nc; b0 += WAVE * STAGE_UNROLL) {
@@ -1028,8 +1074,9 @@ struct GenericTile {
             for (int u = 0; u < STAGE_UNROLL; ++u) {
                 if (b0 + u * WAVE >= nc) continue;
                 int32_t* dst = g + (int64_t)rows[u] * gpitch + poss[u];
-                const bool fb = FB && flags[rows[u]];
-                const int32_t* f = fallback + (int64_t)rows[u] * fpitch + poss[u];
+                const uint32_t fc = FB ? flags[rows[u]] : 0u;
+                const bool fb = fc != 0u;
+                const int32_t* f = fb_src(fc, fallback, fallback2) + (int64_t)rows[u] * fpitch + poss[u];
                 if constexpr (VEC == 4) {
                     out16<false, F32>(reinterpret_cast<int4*>(dst), fb ? *reinterpret_cast<const int4*>(f) : widen4(p[u]));
                 } else {
@@ -1089,10 +1136,22 @@ struct GenericTile {
     }
     __device__ __forceinline__ void set_dirty(int, uint32_t) const {}
     template <bool NT>
-    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane) const {
-        store<true>(g, twoL, R, g, twoL, lane);
+    __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
+        store<true>(g, twoL, R, g, twoL, lane, fallback2);
     }
 };
+
+// The int8 trajectory rows of a tile with flagged rows (rare, wave-uniform branch): byte by byte,
+// flagged rows as the int8 values of their fallback row (numpy's astype(int8) wrap)
+template <class Tile>
+__device__ __forceinline__ void store_rows_i8_fb(const Tile& t, int8_t* g, int R, int twoL, int lane,
+                                              const int32_t* fb_in, const int32_t* fb_reset) {
+    for (int i = lane; i < R * twoL; i += WAVE) {
+        const int r = i / twoL, k = i - r * twoL;
+        const uint32_t fc = t.flags[r];
+        g[i] = (int8_t)(fc ? fb_src(fc, fb_in, fb_reset)[(int64_t)r * twoL + k] : t.letter(r, k));
+    }
+}
 
 template <int NW, int LC, int VEC>
 using TileFor = typename std::conditional<
@@ -1113,54 +1172,6 @@ __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>&
             dst[h * L + k] = k < n ? v : 0;
         }
     }
-}
-
-// One lane packs its own row straight from HBM (per-lane loads, no LDS staging): the same
-// result as tile.load + tile.pack for that row.  Only for a step-kernel env whose starting row
-// turned out invalid (it keeps its input row, whose lengths are re-read here).  Rolled loops
-// (one load in flight): a rare path that must not add register pressure to the kernel.
-template <int NW, int LC>
-__device__ __forceinline__ bool pack_row_global(const int32_t* __restrict__ row, int Lr, PresRegs<NW>& p) {
-    const int L = LC > 0 ? LC : Lr;
-    bool bad = false;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        Word<NW> w = wzero<NW>();
-        uint64_t mlo = 0, mhi = 0;
-        const int32_t* src = row + h * L;
-        if constexpr (LC > 0 && LC % 4 == 0) {
-#pragma unroll 1
-            for (int k = 0; k < LC / 4; ++k) {
-                const int4 v = reinterpret_cast<const int4*>(src)[k];
-                const uint32_t d = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
-                                   (to_i8(v.w, bad) << 24);
-                uint32_t c8, nz4;
-                swar_pack4(d, c8, nz4);
-#pragma unroll
-                for (int j = 0; j < NW; ++j) w.w[j] |= (k >> 2) == j ? c8 << (8 * (k & 3)) : 0u;
-                if (k < 16) mlo |= (uint64_t)nz4 << (4 * k);
-                else mhi |= (uint64_t)nz4 << (4 * (k - 16));
-            }
-        } else {
-#pragma unroll 1
-            for (int k = 0; k < L; ++k) {
-                const uint32_t b = to_i8(src[k], bad);
-                const bool nz = b != 0u;
-                const uint32_t code = nz ? (((~b & 1u) << 1) | ((b >> 7) & 1u)) : 0u;
-#pragma unroll
-                for (int j = 0; j < NW; ++j) w.w[j] |= (k >> 4) == j ? code << (2 * (k & 15)) : 0u;
-                if (k < 64) mlo |= (uint64_t)nz << k;
-                else mhi |= (uint64_t)nz << (k - 64);
-            }
-        }
-        const int n = __builtin_popcountll(mlo) + __builtin_popcountll(mhi);
-        const uint64_t elo = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-        const uint64_t ehi = n <= 64 ? 0ull : (n >= 128 ? ~0ull : ((1ull << (n - 64)) - 1ull));
-        bad |= (mlo != elo) || (mhi != ehi);
-        if (h == 0) { p.w0 = w; p.n0 = n; }
-        else        { p.w1 = w; p.n1 = n; }
-    }
-    return bad;
 }
 
 // A wave reloads its whole tile of starting states (one coalesced pass) when more than this
@@ -1278,8 +1289,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     }
     const uint64_t rb = __ballot(reset);
     if (rb) {
-        // same-step autoreset to the env's starting state.  An out-of-domain starting row
-        // fails the env instead (err ACX_ERR_DOMAIN, state and step_count keep their inputs).
+        // same-step autoreset to the env's starting state.  An out-of-domain starting row is
+        // taken as it is, like the reference's reset (ac_env.py:113-129, no validation): the
+        // env's row becomes that row's exact values (copied from reset_state, FB_RESET), its
+        // step count 0 and its err ACX_ERR_DOMAIN; from then on it is an out-of-domain row.
         bool rbad = false;
         if (__popcll(rb) > RESET_TILE_MIN) {
             // many lanes (a synchronised truncation): one coalesced load of the tile's starting
@@ -1289,27 +1302,20 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
             tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
             if (reset) rbad = tile.pack(w.lane, p);
             wave_sync();
-            keep = keep || rbad;
-            if (w.active && !keep) tile.unpack(w.lane, p);
+            if (w.active && !keep && !rbad) tile.unpack(w.lane, p);
             dm = (w.active && !keep) ? 3u : 0u;  // the tile now holds starting rows: write every kept-moving row
-            tile.restore_flags(w.lane, w.active && keep);
+            tile.restore_flags(w.lane, (w.active && keep) ? FB_IN : (rbad ? FB_RESET : 0u));
         } else {
             // a few lanes: the wave loads just their rows (scattered resets cost their rows only)
             tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
             if (reset) {
                 rbad = tile.pack(w.lane, p);
                 if (!rbad) tile.unpack(w.lane, p);
-                dm = rbad ? 0u : 3u;
+                dm = 3u;
             }
-            keep = keep || rbad;
-            tile.flag_rows(w.lane, rbad);
+            tile.flag_rows(w.lane, rbad ? FB_RESET : 0u);
         }
-        if (rbad) {  // rare: the reported lengths are those of the kept input row
-            reset = false;
-            e = ACX_ERR_DOMAIN;
-            cnt = cnt0;
-            pack_row_global<NW, LC>(a.state_in + env * twoL, L, p);
-        }
+        if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
         if (reset) cnt = 0;
     }
     if (w.active) {
@@ -1333,14 +1339,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         // cyclic conjugation that is a no-op and a failed env leave their row as it is in HBM)
         tile.set_dirty(w.lane, dm);
         wave_sync();
-        if (__ballot(dm != 0u)) tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane);
+        if (__ballot(dm != 0u))
+            tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
     } else {
         wave_sync();
-        tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
+        tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane,
+                                  a.reset_state + w.r0 * twoL);
     }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
-                                               a.state_in + w.r0 * twoL, twoL, w.lane);
+                                               a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
 }
 
 struct RolloutArgs {
@@ -1373,9 +1381,14 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
 
     // starting states are read only when an episode ends (not kept in registers, which are
     // the rollout's occupancy limit): by the resetting lane alone, or by a coalesced reload of
-    // the tile when many lanes of the wave reset together; an out-of-domain starting row fails
-    // its env then (err ACX_ERR_DOMAIN, the env stops and its state keeps its input)
+    // the tile when many lanes of the wave reset together.
+    // Errors follow acx_step exactly, so T launches of acx_step give the same trajectory: a
+    // failed move (err 1, 2, 4) leaves the state and the step count as they are for that step
+    // (done = truncated = 0, reward = -(n0+n1)); an out-of-domain row (err 3: the input row, or
+    // a starting row an autoreset loaded -- then held as that row, count 0) never moves and
+    // never counts; its observations are its exact int32 values (fallback rows, FB_*).
     bool bad = false;
+    bool bad_reset = false;  // the out-of-domain row is the env's starting row (FB_RESET)
     PresRegs<NW> p;
     tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
@@ -1413,15 +1426,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             if (bad) e = ACX_ERR_DOMAIN;
             else if (clean) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
             else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
-            clean = clean || e == ACX_ERR_NONE;  // a successful general move leaves it clean
+            const bool ok = e == ACX_ERR_NONE;
+            clean = clean || ok;  // a successful general move leaves it clean
             if (first_err == ACX_ERR_NONE) first_err = e;
-            const bool triv = (e == ACX_ERR_NONE) && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
-            ++cnt;
-            const bool trunc = cnt >= a.horizon;
+            const bool triv = ok && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
+            cnt += ok ? 1 : 0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
+            const bool trunc = ok && cnt >= a.horizon;
             if (a.reward_traj) st_scalar<ACX_NT_SCALARS != 0, int32_t>(a.reward_traj + ti + w.r0 + ln, triv ? max_reward : -(p.n0 + p.n1));
             if (a.done_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.done_traj + ti + w.r0 + ln, (uint8_t)triv);
             if (a.trunc_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.trunc_traj + ti + w.r0 + ln, (uint8_t)trunc);
-            reset = (triv || trunc) && !bad;
+            reset = triv || trunc;
             if (reset) cnt = 0;
         }
         const uint64_t rb = __ballot(reset);
@@ -1440,6 +1454,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             if (reset) {
                 clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
                 bad = rbad;
+                bad_reset = rbad;
                 if (rbad && first_err == ACX_ERR_NONE) first_err = ACX_ERR_DOMAIN;
             }
         }
@@ -1450,6 +1465,18 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             if (w.active && !bad) {
                 if (reloaded || both) tile.unpack(w.lane, p);
                 else if (!reset) tile.unpack_half(w.lane, p, h1);
+            }
+            if (__ballot(w.active && bad)) {
+                // rare: out-of-domain rows as their exact values from their fallback rows
+                tile.restore_flags(w.lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
+                if constexpr (OBS == 1)
+                    tile.template store<true>(a.obs_traj + (ti + w.r0) * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
+                                              w.lane, a.reset_state + w.r0 * twoL);
+                else
+                    store_rows_i8_fb(tile, a.obs_traj8 + (ti + w.r0) * twoL, w.R, twoL, w.lane, a.state + w.r0 * twoL,
+                                     a.reset_state + w.r0 * twoL);
+                wave_sync();
+                return;
             }
             wave_sync();
             if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
@@ -1508,9 +1535,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         if (a.err) a.err[env] = (uint8_t)first_err;
         if (first_err != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
-    // rows flagged out-of-domain keep their (untouched) global contents
-    tile.restore_flags(w.lane, w.active && bad);
-    tile.template store<true>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL, w.lane);
+    // out-of-domain rows: their input row (untouched in HBM), or the starting row they reset to
+    tile.restore_flags(w.lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
+    tile.template store<true>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL, w.lane,
+                              a.reset_state + w.r0 * twoL);
 }
 
 // Move ids (T, B) int32 -> (ceil(T/8), B) uint32, 8 consecutive steps of one env per word,
@@ -2053,15 +2081,14 @@ static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; 
 template <class F>
 static int dispatch(int L, F&& f) {
     const bool v4 = (2 * L) % 4 == 0;
-#ifdef ACX_ISA_L128_ONLY  // faster builds for ISA inspection only
+#if defined(ACX_ISA_L128_ONLY)  // faster builds for ISA inspection only
     (void)v4;
     return L == 128 ? f.template go<8, 128, 4>() : ACX_E_ARG;
-#endif
-    if (L == 36) return f.template go<3, 36, 4>();
-#ifdef ACX_ISA_L36_ONLY  // faster builds for ISA inspection only
+#elif defined(ACX_ISA_L36_ONLY)  // faster builds for ISA inspection only
     (void)v4;
-    return ACX_E_ARG;
+    return L == 36 ? f.template go<3, 36, 4>() : ACX_E_ARG;
 #else
+    if (L == 36) return f.template go<3, 36, 4>();
     if (L == 128) return f.template go<8, 128, 4>();
     switch (nw_for(L)) {
         case 1: return v4 ? f.template go<1, 0, 4>() : f.template go<1, 0, 2>();
@@ -2081,17 +2108,131 @@ static inline unsigned grid_for(int64_t rows) {
     return (unsigned)((rows + (int64_t)BLOCK - 1) / BLOCK);
 }
 
+// One launcher per kernel family and instantiation.  They are plain (non-static) function
+// templates so that the slow-to-compile L = 128 instantiations can be explicitly instantiated in
+// separate objects built from this same file (-DACX_PART=n, compiled in parallel by build.py)
+// while the main object declares them `extern template` below.
+template <int NW, int LC, int VEC, bool LEARN>
+int launch_step(StepArgs a, hipStream_t s) {
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+    step_kernel<NW, LC, VEC, LEARN><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+    return finish_launch();
+}
+template <int NW, int LC, int VEC, int OBS>
+int launch_rollout(RolloutArgs a, hipStream_t s) {
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+    rollout_kernel<NW, LC, VEC, OBS><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+    return finish_launch();
+}
+template <int NW, int LC, int VEC>
+int launch_expand(ExpandArgs a, hipStream_t s) {
+    if constexpr (LC > 0 && LC % 4 == 0) {
+        const size_t rshm = ExpandRowsSmem<NW, LC, VEC>::bytes(a.L);
+        if (a.children && rshm <= 64 * 1024) {
+            expand12_rows_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), rshm, s>>>(a);
+            return finish_launch();
+        }
+    }
+    const size_t cshm = ExpandChildrenSmem<NW, LC, VEC>::bytes(a.L);
+    if (a.children && cshm <= 64 * 1024) {
+        expand12_children_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), cshm, s>>>(a);
+        return finish_launch();
+    }
+    const size_t kshm = ExpandKeysSmem<NW, LC, VEC>::bytes(a.L);
+    if (!a.children && a.child_key && kshm <= 40 * 1024) {  // the search path
+        expand12_keys_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), kshm, s>>>(a);
+        return finish_launch();
+    }
+    const size_t shm = (size_t)WPB * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L);
+    expand12_kernel<NW, LC, VEC><<<dim3(grid_for(a.N)), dim3(BLOCK), shm, s>>>(a);
+    return finish_launch();
+}
+template <int NW, int LC, int VEC>
+int launch_canon(CanonArgs a, hipStream_t s) {
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+    canon_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+    return finish_launch();
+}
+template <int NW, int LC, int VEC>
+int launch_unpack(UnpackArgs a, hipStream_t s) {
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+    unpack_keys_kernel<NW, LC, VEC><<<dim3(grid_for(a.M)), dim3(BLOCK), shm, s>>>(a);
+    return finish_launch();
+}
+
+// Each kernel instantiation set compiles in an object of its own, built from this same file with
+// -DACX_PART=n (build.py compiles them in parallel with the main object, which holds L = 36):
+// the runtime-L generic sets (fully unrolled per-letter loops up to 16*NW letters) took ~7 of the
+// ~7.5 minutes of one object.  The main object declares them `extern template`.
+#define ACX_INST_STEP(EXT, NW, LC, VEC)                                   \
+    EXT template int launch_step<NW, LC, VEC, false>(StepArgs, hipStream_t); \
+    EXT template int launch_step<NW, LC, VEC, true>(StepArgs, hipStream_t);
+#define ACX_INST_ROLL(EXT, NW, LC, VEC, OBS) EXT template int launch_rollout<NW, LC, VEC, OBS>(RolloutArgs, hipStream_t);
+#define ACX_INST_SEARCH(EXT, NW, LC, VEC)                                 \
+    EXT template int launch_expand<NW, LC, VEC>(ExpandArgs, hipStream_t);  \
+    EXT template int launch_canon<NW, LC, VEC>(CanonArgs, hipStream_t);    \
+    EXT template int launch_unpack<NW, LC, VEC>(UnpackArgs, hipStream_t);
+#define ACX_INST_ALL(EXT, NW, LC, VEC) \
+    ACX_INST_STEP(EXT, NW, LC, VEC)    \
+    ACX_INST_ROLL(EXT, NW, LC, VEC, 0) \
+    ACX_INST_ROLL(EXT, NW, LC, VEC, 1) \
+    ACX_INST_ROLL(EXT, NW, LC, VEC, 2) \
+    ACX_INST_SEARCH(EXT, NW, LC, VEC)
+// part n: 1-3 the L = 128 rollout (int32 obs / int8 obs / none), 4 the L = 128 step, 5 the L = 128
+// expand / canonicalize / unpack, 6-10 the generic (runtime-L) sets; build.py's KERNEL_PARTS = 10
+#if !defined(ACX_PART)
+#if !defined(ACX_ISA_L36_ONLY) && !defined(ACX_ISA_L128_ONLY)
+ACX_INST_ROLL(extern, 8, 128, 4, 1)
+ACX_INST_ROLL(extern, 8, 128, 4, 2)
+ACX_INST_ROLL(extern, 8, 128, 4, 0)
+ACX_INST_STEP(extern, 8, 128, 4)
+ACX_INST_SEARCH(extern, 8, 128, 4)
+ACX_INST_ALL(extern, 8, 0, 4)
+ACX_INST_ALL(extern, 8, 0, 2)
+ACX_INST_ALL(extern, 4, 0, 4)
+ACX_INST_ALL(extern, 4, 0, 2)
+ACX_INST_ALL(extern, 3, 0, 4)
+ACX_INST_ALL(extern, 3, 0, 2)
+ACX_INST_ALL(extern, 2, 0, 4)
+ACX_INST_ALL(extern, 2, 0, 2)
+ACX_INST_ALL(extern, 1, 0, 4)
+ACX_INST_ALL(extern, 1, 0, 2)
+#endif
+#elif ACX_PART == 1
+ACX_INST_ROLL(, 8, 128, 4, 1)
+#elif ACX_PART == 2
+ACX_INST_ROLL(, 8, 128, 4, 2)
+#elif ACX_PART == 3
+ACX_INST_ROLL(, 8, 128, 4, 0)
+#elif ACX_PART == 4
+ACX_INST_STEP(, 8, 128, 4)
+#elif ACX_PART == 5
+ACX_INST_SEARCH(, 8, 128, 4)
+#elif ACX_PART == 6
+ACX_INST_ALL(, 8, 0, 4)
+#elif ACX_PART == 7
+ACX_INST_ALL(, 8, 0, 2)
+#elif ACX_PART == 8
+ACX_INST_ALL(, 4, 0, 4)
+ACX_INST_ALL(, 4, 0, 2)
+#elif ACX_PART == 9
+ACX_INST_ALL(, 3, 0, 4)
+ACX_INST_ALL(, 3, 0, 2)
+#elif ACX_PART == 10
+ACX_INST_ALL(, 2, 0, 4)
+ACX_INST_ALL(, 2, 0, 2)
+ACX_INST_ALL(, 1, 0, 4)
+ACX_INST_ALL(, 1, 0, 2)
+#endif
+
 struct StepLaunch {
     StepArgs a;
     hipStream_t s;
     bool learn;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
         a.in_place = a.state_in == a.state_out;
-        if (learn) step_kernel<NW, LC, VEC, true><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        else step_kernel<NW, LC, VEC, false><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
+        return learn ? launch_step<NW, LC, VEC, true>(a, s) : launch_step<NW, LC, VEC, false>(a, s);
     }
 };
 struct RolloutLaunch {
@@ -2099,70 +2240,44 @@ struct RolloutLaunch {
     hipStream_t s;
     template <int NW, int LC, int VEC>
     int go() {
-        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        if (a.obs_traj8) rollout_kernel<NW, LC, VEC, 2><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        else if (a.obs_traj) rollout_kernel<NW, LC, VEC, 1><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        else rollout_kernel<NW, LC, VEC, 0><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
+        if (a.obs_traj8) return launch_rollout<NW, LC, VEC, 2>(a, s);
+        if (a.obs_traj) return launch_rollout<NW, LC, VEC, 1>(a, s);
+        return launch_rollout<NW, LC, VEC, 0>(a, s);
     }
 };
 struct ExpandLaunch {
     ExpandArgs a;
     hipStream_t s;
     template <int NW, int LC, int VEC>
-    int go() {
-        if constexpr (LC > 0 && LC % 4 == 0) {
-            const size_t rshm = ExpandRowsSmem<NW, LC, VEC>::bytes(a.L);
-            if (a.children && rshm <= 64 * 1024) {
-                expand12_rows_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), rshm, s>>>(a);
-                return finish_launch();
-            }
-        }
-        const size_t cshm = ExpandChildrenSmem<NW, LC, VEC>::bytes(a.L);
-        if (a.children && cshm <= 64 * 1024) {
-            expand12_children_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), cshm, s>>>(a);
-            return finish_launch();
-        }
-        const size_t kshm = ExpandKeysSmem<NW, LC, VEC>::bytes(a.L);
-        if (!a.children && a.child_key && kshm <= 40 * 1024) {  // the search path
-            expand12_keys_kernel<NW, LC, VEC><<<dim3((unsigned)((a.N + WAVE - 1) / WAVE)), dim3(BLOCK), kshm, s>>>(a);
-            return finish_launch();
-        }
-        const size_t shm = (size_t)WPB * ExpandLaunchSmem<NW, LC, VEC>::wave_bytes(a.L);
-        expand12_kernel<NW, LC, VEC><<<dim3(grid_for(a.N)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
-    }
+    int go() { return launch_expand<NW, LC, VEC>(a, s); }
 };
 struct CanonLaunch {
     CanonArgs a;
     hipStream_t s;
     template <int NW, int LC, int VEC>
-    int go() {
-        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        canon_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
-    }
+    int go() { return launch_canon<NW, LC, VEC>(a, s); }
 };
 struct UnpackLaunch {
     UnpackArgs a;
     hipStream_t s;
     template <int NW, int LC, int VEC>
-    int go() {
-        const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-        unpack_keys_kernel<NW, LC, VEC><<<dim3(grid_for(a.M)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
-    }
+    int go() { return launch_unpack<NW, LC, VEC>(a, s); }
 };
 
 }  // namespace acx
 
+#ifndef ACX_PART  // the C-ABI lives in the main object only
 using namespace acx;
 
 extern "C" {
 
 int32_t acx_key_words(int32_t L) { return (4 * L + 16 + 63) / 64; }
 
-const char* acx_version(void) { return "acx 0.1 gfx950"; }
+// build provenance: build.py passes the sha256 of the sources this library is compiled from
+#ifndef ACX_SOURCE_HASH
+#define ACX_SOURCE_HASH "unknown"
+#endif
+const char* acx_version(void) { return "acx 0.3 gfx950 acx-src-sha256:" ACX_SOURCE_HASH; }
 
 int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
              int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
@@ -2332,3 +2447,4 @@ int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out,
 }
 
 }  // extern "C"
+#endif  // ACX_PART

@@ -139,6 +139,45 @@ def cpu_baseline_c_all(L: int, horizon: int, seconds: float, max_procs: int = 16
             "sample": f"oracle/acx_oracle.c env_step, {procs_n} procs x 16384 envs x {seconds:.0f}s"}
 
 
+def dist_setup(local_rank: int, world: int, backend: str = "nccl", force: bool = False):
+    """One process per GPU (torchrun's LOCAL_RANK / WORLD_SIZE / MASTER_*): select this rank's
+    GPU and, for world > 1 (or `force`, a one-rank group: tests/test_gpu_sbfs.py runs the RCCL
+    path that way on one GPU), join the process group -- "nccl" is RCCL over xGMI, bound to the
+    rank's device; "gloo" rehearses N ranks on one GPU.  Returns the rank's device."""
+    import torch
+    import torch.distributed as dist
+
+    gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if world > 1 or force:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dev
+
+
+def synced_max(value: float, dev) -> float:
+    """max over the ranks of a host float (the timed region's wall time): an RCCL all_reduce of a
+    device scalar; the value itself in a single process without a process group."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier() -> None:
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,14 +214,7 @@ def main():
     import torch.distributed as dist
 
     backend = os.environ.get("ACX_DIST_BACKEND", "nccl")  # "gloo": rehearse N ranks on one GPU
-    gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+    dev = dist_setup(local_rank, world, backend)
 
     import acx
     from acx import ops
@@ -220,8 +252,7 @@ def main():
     if W > 0:
         roll(actions[:W], W)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -231,15 +262,11 @@ def main():
     t_launch = time.perf_counter() - t0
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_s = ev0.elapsed_time(ev1) / 1e3
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = synced_max(elapsed, dev)
     n_err = int(err_count.item())  # the headline rollout's env errors (warmup + timed)
 
     # algorithmic bytes of the rollout launch (DESIGN.md "Roofline"): per env-step action 4 B
@@ -481,17 +508,14 @@ def main():
             SB.sharded_bfs(ak3, nb, device=dev)  # warmup: workspace allocation
         best = None
         for _ in range(3):
-            if world > 1:
-                dist.barrier()
+            barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             with contextlib.redirect_stdout(io.StringIO()):
                 res = SB.sharded_bfs(ak3, nb, device=dev)
             torch.cuda.synchronize()
-            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-            if world > 1:
-                dist.all_reduce(el, op=dist.ReduceOp.MAX)
-            best = el.item() if best is None else min(best, el.item())
+            el = synced_max(time.perf_counter() - t0, dev)
+            best = el if best is None else min(best, el)
         st = SB.LAST_STATS
         return {
             "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],

@@ -30,6 +30,19 @@
  *     ACX_ERR_* codes below; an env with err != 0 keeps its input state (the reference
  *     raises instead).  `err_count` (nullable, one int32) is atomically incremented once
  *     per env with err != 0, so the host can check one word instead of B bytes.
+ *   - Env-step error contract (acx_step, acx_step_record, acx_step_learner and every rollout
+ *     entry point; T rollout steps = T acx_step calls, tests/test_gpu_rollout_errors.py):
+ *       * a failed move (ACX_ERR_INVALID, _EMPTY_CONJ, _ACTION) leaves the env's state and
+ *         step count as they are for that step -- the reference raises before
+ *         `count_steps += 1` (ac_env.py:93-103) -- with done = truncated = 0 and
+ *         reward = -(n0+n1) of the unchanged state; the env goes on with its next move id;
+ *       * a row outside the packed domain (ACX_ERR_DOMAIN) never moves and never counts; it
+ *         is stored and observed with its exact int32 values.  An autoreset to such a starting
+ *         row (same-step autoreset below) still happens, as the reference's reset takes any
+ *         row (ac_env.py:113-129): the step reports the move's reward / done / truncated /
+ *         final_obs, the env then holds that starting row with step count 0 and err
+ *         ACX_ERR_DOMAIN, and lengths_out has its non-zero counts;
+ *       * a rollout's err[b] is the first error of env b in the launch.
  *   - L (max_relator_length) must be in [1, ACX_MAX_L].
  */
 #ifndef ACX_H
@@ -156,7 +169,9 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
  * updated in place; actions is (T,B) int32.  Per step t the kernel writes (all optional):
  *   obs_traj[t]    (T,B,2L) int32  observation after step t (post autoreset)
  *   reward_traj[t] (T,B) int32, done_traj[t], trunc_traj[t] (T,B) uint8.
- * reset_state (B,2L) is required (autoreset on done/truncated, as acx_step).
+ * reset_state (B,2L) is required (autoreset on done/truncated, as acx_step).  Errors follow the
+ * env-step error contract above, so the trajectory equals T acx_step calls; err[b] is env b's
+ * first error in the launch.
  */
 int acx_rollout(int32_t* state, const int32_t* actions, const int32_t* reset_state,
                 int32_t* step_count, int32_t* obs_traj, int32_t* reward_traj, uint8_t* done_traj,
@@ -376,7 +391,9 @@ int32_t acx_search_found(void* h, int32_t* first_letters, int64_t* explored);
  * HBM hash table of the committed nodes; the host replays the reference's pop / dedup / budget
  * order exactly, checking only the children the device did not know against the nodes appended
  * since (the in-flight conflicts).  batch = parents per round (<= 0: 64).
- *   acx_greedy_run       searches from `presentation` (HOST pointer, 2L int32, letters +-1/+-2);
+ *   acx_greedy_run       searches from `presentation` (HOST pointer, 2L int32, letters +-1/+-2),
+ *                        max_nodes <= 2^38; the device key store and visited set start at
+ *                        min(max_nodes, 2^22) nodes and double as the search grows;
  *                        *out_handle receives the finished search (query it, then destroy)
  *   acx_greedy_status / _path / _min_trace / _popped / _node_keys / _found   as acx_search_*
  *   acx_greedy_stats     out[0] rounds, [1] parents expanded, [2] popped, [3] children the device

@@ -155,6 +155,26 @@ def test_key_packing_roundtrip():
             assert np.array_equal(_unpack_key_host(E._pack_key(s, L), L), s)
 
 
+def test_search_engine_name_is_validated():
+    """A misspelt engine raises instead of silently running another engine."""
+    ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+    with pytest.raises(ValueError):
+        acx.greedy_search(ak2, engine="devcie")
+    with pytest.raises(ValueError):
+        acx.bfs(ak2, engine="devcie")
+
+
+def test_library_source_hash_matches_shipped_sources():
+    """Build provenance: libacx.so embeds the sha256 of the sources it was compiled from
+    (build.py source_hash()) in acx_version(); a stale library fails here."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("acx_build", os.path.join(REPO, "ac-solver-caltech_amd", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    ver = _lib.load().acx_version().decode()
+    assert ver.endswith("acx-src-sha256:" + mod.source_hash()), ver
+
+
 def test_engine_matches_reference_searches_on_oracle_expansions():
     with open(os.path.join(GOLDEN, "kat_search.json")) as f:
         kat = json.load(f)

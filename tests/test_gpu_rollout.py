@@ -143,7 +143,9 @@ def test_desynchronised_resets_equal_oracle(L, B, T, H, kind):
 @pytest.mark.parametrize("L", [36, 128, 17])
 def test_bad_starting_row_fails_env_at_its_reset(L):
     """A starting row outside the domain is found when the env resets to it: err = 3
-    (ACX_ERR_DOMAIN), the env stops and its state keeps its input; other envs are unaffected."""
+    (ACX_ERR_DOMAIN), the env then holds that row (exact values) with step count 0 and never
+    moves again; other envs are unaffected (tests/test_gpu_rollout_errors.py has the whole
+    contract)."""
     B, T, H = 256, 12, 4
     starts = _starts(L, B, seed=3)
     resets = starts.copy()
@@ -157,7 +159,8 @@ def test_bad_starting_row_fails_env_at_its_reset(L):
         st, cnt, obs, rew, dn, tr, err, ec = _roll(starts, acts, L, H, True, pack=pack, count0=count0, resets=resets)
         assert err[5] == 3 and err[70] == 3 and int(ec[0]) == 2
         assert (np.delete(err, [5, 70]) == 0).all()
-        assert np.array_equal(st[5], starts[5]) and np.array_equal(st[70], starts[70])
+        assert np.array_equal(st[5], resets[5]) and np.array_equal(st[70], resets[70])
+        assert cnt[5] == 0 and cnt[70] == 0
         good = np.setdiff1d(np.arange(B), [5, 70])
         o_st = starts.copy()
         o_cnt = count0.copy()

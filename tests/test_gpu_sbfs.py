@@ -175,3 +175,54 @@ def test_sharded_bfs_multi_rank(world):
         assert n >= min(nd, 1) and len(ids) >= n and np.unique(ids).size == len(ids), name
         assert np.array_equal(ids[:n], np.arange(n)), name
         assert np.array_equal(keys[:n], dk), name
+
+
+_RCCL_SCRIPT = r"""
+import json, sys
+sys.path[:0] = [%(repo)r, %(pkg)r, %(tests)r]
+import numpy as np
+import torch
+import torch.distributed as dist
+import bench
+from conftest import state_digest, unpack_keys_np
+dev = bench.dist_setup(0, 1, "nccl", force=True)   # bench.py's own multi-GPU setup, one rank
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+bench.barrier()
+assert bench.synced_max(1.5, dev) == 1.5
+from acx.search import _sharded_bfs as SB
+c = json.loads(sys.argv[1])
+res = SB.sharded_bfs(np.array(c["presentation"]), c["budget"], cyclically_reduce_after_moves=c["cyclical"],
+                     device=dev, keep_node_keys=True, always_exchange=True)
+st = SB.LAST_STATS
+order = np.argsort(st["node_ids"])
+keys = st["node_keys"][order][: c["parents"]]
+dig, cps = state_digest(unpack_keys_np(keys, c["L"]), c["checkpoints"].keys())
+print(json.dumps({"exchange": st["exchange"], "parents": st["parents"], "digest": dig, "cps": cps,
+                  "result": [bool(res[0]), None if res[1] is None else [list(x) for x in res[1]]]}))
+SB.release_workspaces()
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_exchanges_one_rank_at_scale():
+    """The RCCL code paths on hardware without a multi-GPU run: bench.py's
+    multi-GPU setup (dist_setup: nccl process group bound to cuda:0 with device_id, barrier,
+    max-over-ranks all_reduce) in a one-rank group, then the owner-partitioned BFS with every
+    per-chunk exchange forced through _Comm's device-tensor branch (RCCL all_gather,
+    all_to_all_single, all_reduce) on the AK(3) 10^6-node reference run (search_scale.json):
+    the parent order digest, parent count and result equal the reference's."""
+    import subprocess
+    import sys
+    with open(os.path.join(GOLDEN, "search_scale.json")) as f:
+        c = next(x for x in json.load(f) if x["search_fn"] == "bfs" and x["L"] == 36 and not x["cyclical"]
+                 and x["presentation"] == _ak3(36).tolist() and x["budget"] == 10 ** 6)
+    code = _RCCL_SCRIPT % {"repo": REPO, "pkg": PKG_ROOT, "tests": os.path.join(REPO, "tests")}
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", code, json.dumps(c)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["exchange"] == "device"
+    assert out["parents"] == c["parents"] and out["digest"] == c["digest"] and out["cps"] == c["checkpoints"]
+    assert out["result"] == [c["ok"], c["path"]]

@@ -174,6 +174,66 @@ def test_greedy_device_engine_aged_caches():
     _check_order(unpack_keys_np(st["node_keys"][st["popped"]], c["L"]), c)
 
 
+@pytest.mark.parametrize("log2_age,batch", [(4, 1), (4, 64), (5, 7), (6, 1024)])
+def test_greedy_device_engine_tiny_cache_age(log2_age, batch):
+    """Cache age limits of 16..64 appends (test hook): nearly every replay stops at an aged cache
+    and the in-flight table switches generations every few visits, so visits whose 12 appends
+    cross a generation boundary happen constantly (a visit must not lose ids >= its
+    probe's node count to a generation switch).  The pop order equals the reference's at every
+    checkpoint the search reaches (20,000 nodes)."""
+    import ctypes
+    from acx import _lib
+    from acx.search import _engine as E
+    hook = _lib.load().acx_internal_greedy_age
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    for c in GREEDY_CASES[:2]:
+        hook(log2_age)
+        try:
+            ok, path = E.run_search(E.GREEDY, np.array(c["presentation"]), 20000, False, c["cyclical"], device=DEV,
+                                    keep_node_keys=True, batch=batch)
+        finally:
+            hook(0)
+        st = E.LAST_STATS
+        assert st["stop_aged"] + st["retired_caches"] > 100
+        states = unpack_keys_np(st["node_keys"][st["popped"]], c["L"])
+        want = {k: v for k, v in c["checkpoints"].items() if int(k) <= len(states)}
+        assert len(want) >= 3
+        _, cps = state_digest(states, want.keys())
+        assert cps == want
+        # the node set has no duplicates (a missed in-flight conflict would add one twice)
+        keys = st["node_keys"]
+        assert len(np.unique(keys, axis=0)) == len(keys)
+
+
+def test_greedy_device_engine_grows_its_store():
+    """The device store no longer allocates for the budget: a 2^36-node budget on a
+    search that ends early just works (AK(2), the reference's greedy.py known answer); and a store
+    forced to start at 2^10 nodes (test hook) regrows 10 times on the way to 10^6 nodes, re-entering
+    the committed nodes each time, with the pop order still the reference's."""
+    import ctypes
+    import acx
+    from acx import _lib
+    from acx.search import _engine as E
+    with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+        kat = json.load(f)
+    ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+    ok, path = acx.greedy_search(ak2, max_nodes_to_explore=1 << 36, device=DEV)
+    assert [ok, [list(x) for x in path]] == kat["greedy_ak2"]
+    hook = _lib.load().acx_internal_greedy_init_cap
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    c = GREEDY_CASES[0]
+    hook(10)
+    try:
+        ok, path = E.run_search(E.GREEDY, np.array(c["presentation"]), c["budget"], False, c["cyclical"], device=DEV,
+                                keep_node_keys=True)
+    finally:
+        hook(0)
+    assert [bool(ok), [list(x) for x in path]] == [c["ok"], c["path"]]
+    _check_order(unpack_keys_np(E.LAST_STATS["node_keys"][E.LAST_STATS["popped"]], c["L"]), c)
+
+
 with open(os.path.join(GOLDEN, "search_scale_1e7.json")) as _f:
     CONFIG4 = json.load(_f)[0]
 
