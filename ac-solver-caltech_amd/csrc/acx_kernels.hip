@@ -1287,6 +1287,9 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
     }
+    // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
+    // hold it) are stored from their input row too
+    tile.flag_rows(w.lane, (w.active && e == ACX_ERR_DOMAIN) ? FB_IN : 0u);
     const uint64_t rb = __ballot(reset);
     if (rb) {
         // same-step autoreset to the env's starting state.  An out-of-domain starting row is
@@ -1625,6 +1628,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
         bad = tile.pack(w.lane, p);
         clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
     }
+    tile.flag_rows(w.lane, bad ? FB_IN : 0u);  // children of out-of-domain parents copy the parent row
     int nerr = 0;
     // keys only (the search path): stage each group of KEY_GROUP actions' keys in LDS
     // (the parents' rows are no longer needed once packed) and write them out as
@@ -1825,6 +1829,7 @@ __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) 
         bad = tile.pack(lane, p);
         clean = !bad && is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
     }
+    tile.flag_rows(lane, bad ? FB_IN : 0u);  // incl. a zero inside a relator (not flagged by the load)
 
     int nerr = 0;
     const int64_t par = r0 + lane;
@@ -2013,9 +2018,10 @@ __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
     tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
+    bool bad = false;
     if (w.active) {
         PresRegs<NW> p;
-        const bool bad = tile.pack(w.lane, p);
+        bad = tile.pack(w.lane, p);
         const int e = bad ? ACX_ERR_DOMAIN : ((p.n0 == 0 || p.n1 == 0) ? ACX_ERR_INVALID : ACX_ERR_NONE);
         if (e == ACX_ERR_NONE) {
             simplify<NW>(p.w0, p.n0, a.cyclical != 0);
@@ -2029,6 +2035,7 @@ __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
         if (a.err) a.err[env] = (uint8_t)e;
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
+    tile.flag_rows(w.lane, bad ? FB_IN : 0u);  // incl. a zero inside a relator (not flagged by the load)
     wave_sync();
     tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
 }

