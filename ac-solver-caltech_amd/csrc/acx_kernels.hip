@@ -30,6 +30,7 @@
 #include "acx.h"
 
 #include "acx_moves.h"
+#include "acx_planes.h"
 
 namespace acx {
 
@@ -439,6 +440,92 @@ struct FastTile {
         }
     }
 
+    // ---- bit-plane registers (acx_planes.h; the env-step kernels) ----
+    static constexpr int PW = PlaneWords<NW>::value;
+
+    // lane's row -> bit planes; returns true if the row is outside the domain.  Streams the row
+    // 8 letters (two dwords) at a time through one gather per plane (pl::i8x8_to_bytes), so few
+    // values are live at once: this pack sets the env-step kernels' register peak
+    __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t* src = lds + ln * S;
+        bool bad = flags[ln] != 0;
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {  // one relator at a time (register peak)
+            Planes<PW> w;
+            uint64_t nz[PW];
+#pragma unroll
+            for (int j = 0; j < PW; ++j) w.s[j] = w.y[j] = nz[j] = 0ull;
+#pragma unroll
+            for (int k = 0; k < HALF; k += 2) {
+                const uint32_t d0 = src[h * HALF + k];
+                const uint32_t d1 = k + 1 < HALF ? src[h * HALF + k + 1] : 0u;
+                uint32_t s8, y8, z8;
+                pl::i8x8_to_bytes(d0, d1, s8, y8, z8);
+                const int sh = 4 * (k & 15);
+                w.s[k >> 4] |= (uint64_t)s8 << sh;
+                w.y[k >> 4] |= (uint64_t)y8 << sh;
+                nz[k >> 4] |= (uint64_t)z8 << sh;
+            }
+            int n = 0;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) n += __builtin_popcountll(nz[j]);
+            const pl::Bits<PW> e = pl::bmask<PW>(n);  // zeros only as right padding <=> mask == low n bits
+#pragma unroll
+            for (int j = 0; j < PW; ++j) bad |= nz[j] != e.b[j];
+            if (h == 0) { p.w0 = w; p.n0 = n; }
+            else        { p.w1 = w; p.n1 = n; }
+        }
+        return bad;
+    }
+    __device__ __forceinline__ void unpack(int lane, const PlaneRegs<PW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        uint32_t d[CPR];
+        image(p, d);
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
+    }
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        uint32_t d[CPR];
+        image(p, d);
+        uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+        for (int k = 0; k < CPR; k += 2) {
+            const uint2 o = *reinterpret_cast<const uint2*>(dst + k);
+            if (k < HALF) x0 |= o.x ^ d[k];
+            else x1 |= o.x ^ d[k];
+            if (k + 1 < HALF) x0 |= o.y ^ d[k + 1];
+            else x1 |= o.y ^ d[k + 1];
+            *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
+        }
+        return (x0 != 0u ? 1u : 0u) | (x1 != 0u ? 2u : 0u);
+    }
+    __device__ __forceinline__ void unpack_half(int lane, const PlaneRegs<PW>& p, bool h1) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const Planes<PW> w = pl::psel<PW>(h1, p.w1, p.w0);
+        const int n8 = 8 * (h1 ? p.n1 : p.n0);
+        uint32_t* dst = lds + ln * S + (h1 ? HALF : 0);
+#pragma unroll
+        for (int k = 0; k < HALF; ++k) dst[k] = pl::nibbles_to_i8x4(pl::nib<PW>(w.s, k), pl::nib<PW>(w.y, k), clamp_bits(n8 - 32 * k));
+    }
+    __device__ __forceinline__ static void image(const PlaneRegs<PW>& p, uint32_t (&d)[CPR]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const Planes<PW>& w = h ? p.w1 : p.w0;
+            const int n8 = 8 * (h ? p.n1 : p.n0);
+#pragma unroll
+            for (int k = 0; k < HALF; ++k)
+                d[h * HALF + k] = pl::nibbles_to_i8x4(pl::nib<PW>(w.s, k), pl::nib<PW>(w.y, k), clamp_bits(n8 - 32 * k));
+        }
+    }
+
     // lane's row -> packed registers; returns true if the row is outside the domain
     __device__ __forceinline__ bool pack(int lane, PresRegs<NW>& p) const {
         int ln = lane;
@@ -796,6 +883,103 @@ struct CodeTile {
         }
     }
 
+    // ---- bit-plane registers (acx_planes.h; the env-step kernels) ----
+    // 4 slots (16 letters) per 8-byte LDS access: their code fields -> 32 bits of 2-bit codes ->
+    // the even / odd bits compressed into the s / y planes (and back the same way)
+    static constexpr int PW = PlaneWords<NW>::value;
+    __device__ __forceinline__ static uint32_t compress_even(uint32_t x) {
+        x &= 0x55555555u;
+        x = (x | (x >> 1)) & 0x33333333u;
+        x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+        x = (x | (x >> 4)) & 0x00FF00FFu;
+        return (x | (x >> 8)) & 0x0000FFFFu;
+    }
+    __device__ __forceinline__ static uint32_t spread_even(uint32_t x) {
+        x = (x | (x << 8)) & 0x00FF00FFu;
+        x = (x | (x << 4)) & 0x0F0F0F0Fu;
+        x = (x | (x << 2)) & 0x33333333u;
+        return (x | (x << 1)) & 0x55555555u;
+    }
+    __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
+        static_assert(HALF % 4 == 0, "16-letter groups per relator");
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t* src = lds + ln * S;
+        bool bad = flags[ln] != 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            Planes<PW> w;
+            uint64_t nz[PW];
+#pragma unroll
+            for (int j = 0; j < PW; ++j) w.s[j] = w.y[j] = nz[j] = 0ull;
+#pragma unroll
+            for (int g = 0; g < HALF / 4; ++g) {  // 16 letters
+                const uint2 x = *reinterpret_cast<const uint2*>(src + (h * HALF + 4 * g) / 2);
+                const uint32_t codes = __builtin_amdgcn_perm(x.y, x.x, 0x06040200u);
+                uint32_t nzb = __builtin_amdgcn_perm(x.y, x.x, 0x07050301u) & 0x0F0F0F0Fu;
+                nzb = (nzb | (nzb >> 4)) & 0x00FF00FFu;
+                nzb = (nzb | (nzb >> 8)) & 0x0000FFFFu;
+                const int sh = 16 * (g & 3);
+                w.s[g >> 2] |= (uint64_t)compress_even(codes) << sh;
+                w.y[g >> 2] |= (uint64_t)compress_even(codes >> 1) << sh;
+                nz[g >> 2] |= (uint64_t)nzb << sh;
+            }
+            int n = 0;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) n += __builtin_popcountll(nz[j]);
+            const pl::Bits<PW> e = pl::bmask<PW>(n);
+#pragma unroll
+            for (int j = 0; j < PW; ++j) bad |= nz[j] != e.b[j];
+            if (h == 0) { p.w0 = w; p.n0 = n; }
+            else        { p.w1 = w; p.n1 = n; }
+        }
+        return bad;
+    }
+    // relator h of the lane's row from planes (canonical slots: codes and nz of absent letters 0)
+    __device__ __forceinline__ uint32_t put_relator(uint32_t* dst, const Planes<PW>& w, int n, bool cmp) const {
+        const pl::Bits<PW> m = pl::bmask<PW>(n);
+        uint32_t x = 0;
+#pragma unroll
+        for (int g = 0; g < HALF / 4; ++g) {
+            const int sh = 16 * (g & 3);
+            const uint32_t s16 = (uint32_t)(w.s[g >> 2] >> sh) & 0xffffu;
+            const uint32_t y16 = (uint32_t)(w.y[g >> 2] >> sh) & 0xffffu;
+            const uint32_t codes = spread_even(s16) | (spread_even(y16) << 1);
+            uint32_t nzb = (uint32_t)(m.b[g >> 2] >> sh) & 0xffffu;
+            nzb = (nzb | (nzb << 8)) & 0x00FF00FFu;
+            nzb = (nzb | (nzb << 4)) & 0x0F0F0F0Fu;
+            const uint2 v = make_uint2(__builtin_amdgcn_perm(nzb, codes, 0x05010400u),
+                                       __builtin_amdgcn_perm(nzb, codes, 0x07030602u));
+            uint2* q = reinterpret_cast<uint2*>(dst + 2 * g);
+            if (cmp) {
+                const uint2 o = *q;
+                x |= (o.x ^ v.x) | (o.y ^ v.y);
+            }
+            *q = v;
+        }
+        return x;
+    }
+    __device__ __forceinline__ void unpack(int lane, const PlaneRegs<PW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        put_relator(dst, p.w0, p.n0, false);
+        put_relator(dst + HALF / 2, p.w1, p.n1, false);
+    }
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        uint32_t* dst = lds + ln * S;
+        const uint32_t x0 = put_relator(dst, p.w0, p.n0, true);
+        const uint32_t x1 = put_relator(dst + HALF / 2, p.w1, p.n1, true);
+        return (x0 != 0u ? 1u : 0u) | (x1 != 0u ? 2u : 0u);
+    }
+    __device__ __forceinline__ void unpack_half(int lane, const PlaneRegs<PW>& p, bool h1) const {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        put_relator(lds + ln * S + (h1 ? HALF / 2 : 0), pl::psel<PW>(h1, p.w1, p.w0), h1 ? p.n1 : p.n0, false);
+    }
+
     __device__ __forceinline__ bool pack(int lane, PresRegs<NW>& p) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -1089,6 +1273,53 @@ struct GenericTile {
         }
     }
 
+    // ---- bit-plane registers (acx_planes.h; the env-step kernels), letter by letter ----
+    static constexpr int PW = PlaneWords<NW>::value;
+    __device__ __forceinline__ void pack_relator(const int8_t* src, Planes<PW>& w, int& n, bool& bad) const {
+#pragma unroll
+        for (int j = 0; j < PW; ++j) w.s[j] = w.y[j] = 0ull;
+        n = 0;
+        bool zero_seen = false;
+#pragma unroll
+        for (int k = 0; k < LMAX; ++k) {
+            int b = src[k];
+            if (LC == 0) b = (k < L) ? b : 0;
+            const bool nz = b != 0;
+            w.s[k >> 6] |= (uint64_t)(nz && b < 0) << (k & 63);
+            w.y[k >> 6] |= (uint64_t)(nz && (b & 1) == 0) << (k & 63);
+            n += nz;
+            bad |= nz && zero_seen;
+            zero_seen |= !nz;
+        }
+    }
+    __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
+        const int8_t* r = row(lane);
+        bool bad = flags[lane] != 0;
+        pack_relator(r, p.w0, p.n0, bad);
+        pack_relator(r + L, p.w1, p.n1, bad);
+        return bad;
+    }
+    __device__ __forceinline__ void unpack_relator(int8_t* dst, const Planes<PW>& w, int n) const {
+#pragma unroll
+        for (int k = 0; k < LMAX; ++k) {
+            const uint32_t code = (uint32_t)(((w.y[k >> 6] >> (k & 63)) & 1ull) << 1 | ((w.s[k >> 6] >> (k & 63)) & 1ull));
+            const uint32_t letter = (0xFE02FF01u >> (code << 3)) & 0xffu;  // code -> 1, -1, 2, -2
+            if (LC > 0 || k < L) dst[k] = (int8_t)(k < n ? letter : 0u);
+        }
+    }
+    __device__ __forceinline__ void unpack(int lane, const PlaneRegs<PW>& p) const {
+        int8_t* r = row(lane);
+        unpack_relator(r, p.w0, p.n0);
+        unpack_relator(r + L, p.w1, p.n1);
+    }
+    __device__ __forceinline__ void unpack_half(int lane, const PlaneRegs<PW>& p, bool h1) const {
+        unpack_relator(row(lane) + (h1 ? L : 0), pl::psel<PW>(h1, p.w1, p.w0), h1 ? p.n1 : p.n0);
+    }
+    __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
+        unpack(lane, p);
+        return 3u;
+    }
+
     __device__ __forceinline__ void pack_relator(const int8_t* src, Word<NW>& w, int& n, bool& bad) const {
         w = wzero<NW>();
         n = 0;
@@ -1174,6 +1405,20 @@ __device__ __forceinline__ void regs_to_global(int32_t* dst, const PresRegs<NW>&
     }
 }
 
+template <int PW>
+__device__ __forceinline__ void regs_to_global(int32_t* dst, const PlaneRegs<PW>& p, int L) {
+    for (int h = 0; h < 2; ++h) {
+        const Planes<PW> w = h ? p.w1 : p.w0;
+        const int n = h ? p.n1 : p.n0;
+#pragma unroll 1
+        for (int k = 0; k < L; ++k) {
+            const uint32_t code = pl::pletter<PW>(w, k);
+            const int32_t v = (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu);
+            dst[h * L + k] = k < n ? v : 0;
+        }
+    }
+}
+
 // A wave reloads its whole tile of starting states (one coalesced pass) when more than this
 // many of its lanes reset on the same step (a synchronised truncation); for fewer resetting
 // lanes the wave loads just their rows (tile.load_rows), so scattered resets cost their rows.
@@ -1247,7 +1492,8 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     bool fin = false;    // done | truncated (the curriculum's "finished")
     bool reset = false;  // same-step autoreset of this env
     bool keep = false;   // the env's row is left as loaded (out of domain, or its move failed)
-    PresRegs<NW> p;
+    constexpr int PW = Tile::PW;
+    PlaneRegs<PW> p;
     int cnt0 = 0, cnt = 0, e = ACX_ERR_NONE;
     uint32_t dm = 0;     // relators of the row that differ from state_in (in-place store)
     if (w.active) {
@@ -1267,12 +1513,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
         if (bad) e = ACX_ERR_DOMAIN;
-        else if (is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
-        else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+        else if (pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+        else {
+                const pl::MoveOut<PW> mo = pl::ac_move_call<PW>(p, act, L, cyc);
+                p = mo.p;
+                e = mo.e;
+            }
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
         if (!keep) dm = tile.unpack_dirty(w.lane, p);
-        const bool triv = !keep && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
+        const bool triv = !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
         const bool trunc = !keep && a.step_count && cnt >= a.horizon;
         if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
         if (a.done) a.done[env] = triv;
@@ -1285,7 +1535,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         }
         reset = fin && a.reset_state && !keep;
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
-        if (reset && a.final_obs) regs_to_global<NW>(a.final_obs + env * twoL, p, L);
+        if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
     }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
@@ -1392,7 +1642,8 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     // never counts; its observations are its exact int32 values (fallback rows, FB_*).
     bool bad = false;
     bool bad_reset = false;  // the out-of-domain row is the env's starting row (FB_RESET)
-    PresRegs<NW> p;
+    constexpr int PW = Tile::PW;
+    PlaneRegs<PW> p;
     tile.load(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
     int cnt = 0;
@@ -1402,7 +1653,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         bad = tile.pack(w.lane, p);
         cnt = a.step_count[env];
         if (bad) first_err = ACX_ERR_DOMAIN;
-        clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+        clean = pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc);
     }
     const int32_t max_reward = a.horizon * L * 2;
     // Drain the prologue's loads here: otherwise the waitcnt pass carries the pending
@@ -1427,12 +1678,16 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             both = !clean;
             h1 = ((act + 1) & 1) != 0;
             if (bad) e = ACX_ERR_DOMAIN;
-            else if (clean) e = ac_move_clean<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
-            else e = ac_move<NW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+            else if (clean) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+            else {
+                const pl::MoveOut<PW> mo = pl::ac_move_call<PW>(p, act, L, cyc);
+                p = mo.p;
+                e = mo.e;
+            }
             const bool ok = e == ACX_ERR_NONE;
             clean = clean || ok;  // a successful general move leaves it clean
             if (first_err == ACX_ERR_NONE) first_err = e;
-            const bool triv = ok && is_trivial<NW>(p.w0, p.n0, p.w1, p.n1);
+            const bool triv = ok && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
             cnt += ok ? 1 : 0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
             const bool trunc = ok && cnt >= a.horizon;
             if (a.reward_traj) st_scalar<ACX_NT_SCALARS != 0, int32_t>(a.reward_traj + ti + w.r0 + ln, triv ? max_reward : -(p.n0 + p.n1));
@@ -1455,7 +1710,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 if (reset) rbad = tile.pack(w.lane, p);
             }
             if (reset) {
-                clean = is_clean<NW>(p.w0, p.n0, p.w1, p.n1, cyc);
+                clean = pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc);
                 bad = rbad;
                 bad_reset = rbad;
                 if (rbad && first_err == ACX_ERR_NONE) first_err = ACX_ERR_DOMAIN;
