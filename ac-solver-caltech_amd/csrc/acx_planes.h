@@ -17,6 +17,10 @@
 
 #include "acx_moves.h"
 
+// the plane algebra is also compiled for the host: tests/planes_check.cpp checks it against the
+// C oracle on the CPU
+#define ACX_HD __host__ __device__
+
 namespace acx {
 
 template <int PW>
@@ -47,7 +51,7 @@ struct Bits {
 };
 
 template <int PW>
-__device__ __forceinline__ Bits<PW> bzero() {
+ACX_HD __forceinline__ Bits<PW> bzero() {
     Bits<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) r.b[k] = 0ull;
@@ -56,7 +60,7 @@ __device__ __forceinline__ Bits<PW> bzero() {
 
 // low n bits set, 0 <= n <= 64*PW
 template <int PW>
-__device__ __forceinline__ Bits<PW> bmask(int n) {
+ACX_HD __forceinline__ Bits<PW> bmask(int n) {
     Bits<PW> m;
 #pragma unroll
     for (int k = 0; k < PW; ++k) {
@@ -68,7 +72,7 @@ __device__ __forceinline__ Bits<PW> bmask(int n) {
 
 // logical shift right by s bits, 0 <= s (s >= 64*PW -> 0)
 template <int PW>
-__device__ __forceinline__ Bits<PW> bshr(const Bits<PW>& a, int s) {
+ACX_HD __forceinline__ Bits<PW> bshr(const Bits<PW>& a, int s) {
     Bits<PW> r;
     if constexpr (PW == 1) {
         r.b[0] = s >= 64 ? 0ull : (a.b[0] >> s);
@@ -85,7 +89,7 @@ __device__ __forceinline__ Bits<PW> bshr(const Bits<PW>& a, int s) {
 
 // logical shift left by s bits, 0 <= s (s >= 64*PW -> 0)
 template <int PW>
-__device__ __forceinline__ Bits<PW> bshl(const Bits<PW>& a, int s) {
+ACX_HD __forceinline__ Bits<PW> bshl(const Bits<PW>& a, int s) {
     Bits<PW> r;
     if constexpr (PW == 1) {
         r.b[0] = s >= 64 ? 0ull : (a.b[0] << s);
@@ -102,7 +106,7 @@ __device__ __forceinline__ Bits<PW> bshl(const Bits<PW>& a, int s) {
 
 // reverse the first n bits (result bit u = a bit n-1-u), 1 <= n <= 64*PW
 template <int PW>
-__device__ __forceinline__ Bits<PW> brev(const Bits<PW>& a, int n) {
+ACX_HD __forceinline__ Bits<PW> brev(const Bits<PW>& a, int n) {
     Bits<PW> f;
 #pragma unroll
     for (int k = 0; k < PW; ++k) f.b[k] = __builtin_bitreverse64(a.b[PW - 1 - k]);
@@ -111,7 +115,7 @@ __device__ __forceinline__ Bits<PW> brev(const Bits<PW>& a, int n) {
 
 // index of the lowest set bit (64*PW if none)
 template <int PW>
-__device__ __forceinline__ int bfirst(const Bits<PW>& a) {
+ACX_HD __forceinline__ int bfirst(const Bits<PW>& a) {
     int idx = 64 * PW;
 #pragma unroll
     for (int k = PW - 1; k >= 0; --k) idx = a.b[k] ? (64 * k + (int)__builtin_ctzll(a.b[k])) : idx;
@@ -119,7 +123,7 @@ __device__ __forceinline__ int bfirst(const Bits<PW>& a) {
 }
 
 template <int PW>
-__device__ __forceinline__ bool bnonzero(const Bits<PW>& a) {
+ACX_HD __forceinline__ bool bnonzero(const Bits<PW>& a) {
     uint64_t o = 0;
 #pragma unroll
     for (int k = 0; k < PW; ++k) o |= a.b[k];
@@ -130,21 +134,21 @@ __device__ __forceinline__ bool bnonzero(const Bits<PW>& a) {
 // words of letters (two planes)
 // ---------------------------------------------------------------------------------
 template <int PW>
-__device__ __forceinline__ Bits<PW> S(const Planes<PW>& w) {
+ACX_HD __forceinline__ Bits<PW> S(const Planes<PW>& w) {
     Bits<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) r.b[k] = w.s[k];
     return r;
 }
 template <int PW>
-__device__ __forceinline__ Bits<PW> Y(const Planes<PW>& w) {
+ACX_HD __forceinline__ Bits<PW> Y(const Planes<PW>& w) {
     Bits<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) r.b[k] = w.y[k];
     return r;
 }
 template <int PW>
-__device__ __forceinline__ Planes<PW> make(const Bits<PW>& s, const Bits<PW>& y) {
+ACX_HD __forceinline__ Planes<PW> make(const Bits<PW>& s, const Bits<PW>& y) {
     Planes<PW> w;
 #pragma unroll
     for (int k = 0; k < PW; ++k) {
@@ -155,7 +159,7 @@ __device__ __forceinline__ Planes<PW> make(const Bits<PW>& s, const Bits<PW>& y)
 }
 
 template <int PW>
-__device__ __forceinline__ Planes<PW> psel(bool c, const Planes<PW>& a, const Planes<PW>& b) {
+ACX_HD __forceinline__ Planes<PW> psel(bool c, const Planes<PW>& a, const Planes<PW>& b) {
     Planes<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) {
@@ -167,16 +171,16 @@ __device__ __forceinline__ Planes<PW> psel(bool c, const Planes<PW>& a, const Pl
 
 // letters shifted down by n (letter k of the result = letter k + n)
 template <int PW>
-__device__ __forceinline__ Planes<PW> pshr(const Planes<PW>& a, int n) {
+ACX_HD __forceinline__ Planes<PW> pshr(const Planes<PW>& a, int n) {
     return make<PW>(bshr<PW>(S(a), n), bshr<PW>(Y(a), n));
 }
 template <int PW>
-__device__ __forceinline__ Planes<PW> pshl(const Planes<PW>& a, int n) {
+ACX_HD __forceinline__ Planes<PW> pshl(const Planes<PW>& a, int n) {
     return make<PW>(bshl<PW>(S(a), n), bshl<PW>(Y(a), n));
 }
 // the first n letters only
 template <int PW>
-__device__ __forceinline__ Planes<PW> pkeep(const Planes<PW>& a, int n) {
+ACX_HD __forceinline__ Planes<PW> pkeep(const Planes<PW>& a, int n) {
     const Bits<PW> m = bmask<PW>(n);
     Planes<PW> r;
 #pragma unroll
@@ -187,7 +191,7 @@ __device__ __forceinline__ Planes<PW> pkeep(const Planes<PW>& a, int n) {
     return r;
 }
 template <int PW>
-__device__ __forceinline__ Planes<PW> por(const Planes<PW>& a, const Planes<PW>& b) {
+ACX_HD __forceinline__ Planes<PW> por(const Planes<PW>& a, const Planes<PW>& b) {
     Planes<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) {
@@ -198,12 +202,12 @@ __device__ __forceinline__ Planes<PW> por(const Planes<PW>& a, const Planes<PW>&
 }
 // the first n letters reversed
 template <int PW>
-__device__ __forceinline__ Planes<PW> prev(const Planes<PW>& a, int n) {
+ACX_HD __forceinline__ Planes<PW> prev(const Planes<PW>& a, int n) {
     return make<PW>(brev<PW>(S(a), n), brev<PW>(Y(a), n));
 }
 // the inverse word of the first n letters: reversed, every letter inverted
 template <int PW>
-__device__ __forceinline__ Planes<PW> pinv(const Planes<PW>& a, int n) {
+ACX_HD __forceinline__ Planes<PW> pinv(const Planes<PW>& a, int n) {
     Planes<PW> r = prev<PW>(a, n);
     const Bits<PW> m = bmask<PW>(n);
 #pragma unroll
@@ -213,7 +217,7 @@ __device__ __forceinline__ Planes<PW> pinv(const Planes<PW>& a, int n) {
 
 // mask of the letters k where a[k] is NOT the inverse of b[k] (bits beyond the words: set)
 template <int PW>
-__device__ __forceinline__ Bits<PW> noncancel(const Planes<PW>& a, const Planes<PW>& b) {
+ACX_HD __forceinline__ Bits<PW> noncancel(const Planes<PW>& a, const Planes<PW>& b) {
     Bits<PW> r;
 #pragma unroll
     for (int k = 0; k < PW; ++k) r.b[k] = (a.y[k] ^ b.y[k]) | ~(a.s[k] ^ b.s[k]);
@@ -222,13 +226,13 @@ __device__ __forceinline__ Bits<PW> noncancel(const Planes<PW>& a, const Planes<
 
 // code of letter k (y<<1 | s)
 template <int PW>
-__device__ __forceinline__ uint32_t pletter(const Planes<PW>& a, int k) {
+ACX_HD __forceinline__ uint32_t pletter(const Planes<PW>& a, int k) {
     const Bits<PW> s = bshr<PW>(S(a), k), y = bshr<PW>(Y(a), k);
     return (uint32_t)(((y.b[0] & 1ull) << 1) | (s.b[0] & 1ull));
 }
 // a word holding the letter `code` at position p
 template <int PW>
-__device__ __forceinline__ Planes<PW> psingle(uint32_t code, int p) {
+ACX_HD __forceinline__ Planes<PW> psingle(uint32_t code, int p) {
     Bits<PW> s = bzero<PW>(), y = bzero<PW>();
     s.b[0] = code & 1u;
     y.b[0] = code >> 1;
@@ -241,7 +245,7 @@ __device__ __forceinline__ Planes<PW> psingle(uint32_t code, int p) {
 
 // letters k < n - 1 followed by their inverse
 template <int PW>
-__device__ __forceinline__ Bits<PW> adjacent_pairs(const Planes<PW>& w, int n) {
+ACX_HD __forceinline__ Bits<PW> adjacent_pairs(const Planes<PW>& w, int n) {
     const Planes<PW> nx = pshr<PW>(w, 1);
     Bits<PW> z = noncancel<PW>(w, nx);
     const Bits<PW> m = bmask<PW>(n - 1 > 0 ? n - 1 : 0);
@@ -252,7 +256,7 @@ __device__ __forceinline__ Bits<PW> adjacent_pairs(const Planes<PW>& w, int n) {
 
 // free reduction (utils.py:211-220); the loop only runs for unreduced input
 template <int PW>
-__device__ __forceinline__ void free_reduce(Planes<PW>& w, int& n) {
+ACX_HD __forceinline__ void free_reduce(Planes<PW>& w, int& n) {
     Bits<PW> z = adjacent_pairs<PW>(w, n);
     while (bnonzero<PW>(z)) {
         const int k = bfirst<PW>(z);
@@ -264,7 +268,7 @@ __device__ __forceinline__ void free_reduce(Planes<PW>& w, int& n) {
 
 // cyclic reduction of a freely reduced word (utils.py:223-232)
 template <int PW>
-__device__ __forceinline__ void cyclic_reduce(Planes<PW>& w, int& n) {
+ACX_HD __forceinline__ void cyclic_reduce(Planes<PW>& w, int& n) {
     if (n <= 0) return;
     int p = bfirst<PW>(noncancel<PW>(w, prev<PW>(w, n)));
     p = p < (n >> 1) ? p : (n >> 1);  // a reduced word never peels past its middle
@@ -275,14 +279,14 @@ __device__ __forceinline__ void cyclic_reduce(Planes<PW>& w, int& n) {
 }
 
 template <int PW>
-__device__ __forceinline__ void simplify(Planes<PW>& w, int& n, bool cyc) {
+ACX_HD __forceinline__ void simplify(Planes<PW>& w, int& n, bool cyc) {
     free_reduce<PW>(w, n);
     if (cyc) cyclic_reduce<PW>(w, n);
 }
 
 // ACMove (ac_moves.py:159-231); returns an ACX_ERR_* code and leaves the state unchanged on error
 template <int PW>
-__device__ __forceinline__ int ac_move(Planes<PW>& w0, int& n0, Planes<PW>& w1, int& n1, int action, int L, bool cyc) {
+ACX_HD __forceinline__ int ac_move(Planes<PW>& w0, int& n0, Planes<PW>& w1, int& n1, int action, int L, bool cyc) {
     if ((unsigned)action >= 12u) return ACX_ERR_ACTION;
     const bool i1 = ((action + 1) & 1) != 0;
     const Planes<PW> A = psel<PW>(i1, w1, w0);
@@ -344,20 +348,20 @@ __device__ __noinline__ MoveOut<PW> ac_move_call(PlaneRegs<PW> p, int action, in
 
 // both relators non-empty and reduced (freely; cyclically too when cyc) -- see is_clean
 template <int PW>
-__device__ __forceinline__ bool relator_clean(const Planes<PW>& w, int n, bool cyc) {
+ACX_HD __forceinline__ bool relator_clean(const Planes<PW>& w, int n, bool cyc) {
     if (n <= 0) return false;
     if (bnonzero<PW>(adjacent_pairs<PW>(w, n))) return false;
     if (cyc && n > 1 && pletter<PW>(w, 0) == (pletter<PW>(w, n - 1) ^ 1u)) return false;
     return true;
 }
 template <int PW>
-__device__ __forceinline__ bool is_clean(const Planes<PW>& w0, int n0, const Planes<PW>& w1, int n1, bool cyc) {
+ACX_HD __forceinline__ bool is_clean(const Planes<PW>& w0, int n0, const Planes<PW>& w1, int n1, bool cyc) {
     return relator_clean<PW>(w0, n0, cyc) && relator_clean<PW>(w1, n1, cyc);
 }
 
 // ac_move for a clean input (acx_moves.h ac_move_clean: same results as ac_move)
 template <int PW>
-__device__ __forceinline__ int ac_move_clean(Planes<PW>& w0, int& n0, Planes<PW>& w1, int& n1, int action, int L,
+ACX_HD __forceinline__ int ac_move_clean(Planes<PW>& w0, int& n0, Planes<PW>& w1, int& n1, int action, int L,
                                              bool cyc) {
     if ((unsigned)action >= 12u) return ACX_ERR_ACTION;
     const bool i1 = ((action + 1) & 1) != 0;
@@ -408,7 +412,7 @@ __device__ __forceinline__ int ac_move_clean(Planes<PW>& w0, int& n0, Planes<PW>
 
 // strict triviality (ac_env.py:99, utils.py:57-87): both relators one letter, one x and one y
 template <int PW>
-__device__ __forceinline__ bool is_trivial(const Planes<PW>& w0, int n0, const Planes<PW>& w1, int n1) {
+ACX_HD __forceinline__ bool is_trivial(const Planes<PW>& w0, int n0, const Planes<PW>& w1, int n1) {
     return n0 == 1 && n1 == 1 && (((w0.y[0] ^ w1.y[0]) & 1ull) != 0ull);
 }
 
@@ -416,7 +420,7 @@ __device__ __forceinline__ bool is_trivial(const Planes<PW>& w0, int n0, const P
 // conversions for the LDS tiles (4 letters at a time, letter j of the group at bit j)
 // ---------------------------------------------------------------------------------
 // 4 int8 letters (one dword of the int8 image) -> sign / y / non-zero nibbles
-__device__ __forceinline__ void i8x4_to_nibbles(uint32_t d, uint32_t& s4, uint32_t& y4, uint32_t& nz4) {
+ACX_HD __forceinline__ void i8x4_to_nibbles(uint32_t d, uint32_t& s4, uint32_t& y4, uint32_t& nz4) {
     const uint32_t nz = (d | (d >> 1)) & 0x01010101u;  // letter != 0
     const uint32_t yb = ~d & nz;                       // |letter| == 2
     const uint32_t sb = (d >> 7) & 0x01010101u;        // letter < 0
@@ -428,7 +432,7 @@ __device__ __forceinline__ void i8x4_to_nibbles(uint32_t d, uint32_t& s4, uint32
 
 // 8 int8 letters (two dwords, letters 0-3 in d0) -> sign / y / non-zero bytes (letter j at bit j):
 // bit 0 of every byte of d0 and bit 4 of every byte of d1 gathered by one shift-or chain
-__device__ __forceinline__ void i8x8_to_bytes(uint32_t d0, uint32_t d1, uint32_t& s8, uint32_t& y8, uint32_t& z8) {
+ACX_HD __forceinline__ void i8x8_to_bytes(uint32_t d0, uint32_t d1, uint32_t& s8, uint32_t& y8, uint32_t& z8) {
     const uint32_t nz0 = (d0 | (d0 >> 1)) & 0x01010101u, nz1 = (d1 | (d1 >> 1)) & 0x01010101u;
     const uint32_t z = nz0 | (nz1 << 4);
     const uint32_t y = (~d0 & nz0) | ((~d1 & nz1) << 4);
@@ -439,6 +443,7 @@ __device__ __forceinline__ void i8x8_to_bytes(uint32_t d0, uint32_t d1, uint32_t
     z8 = gather(z);
 }
 
+#ifndef ACX_PLANES_HOST_CHECK  // device-only conversions (tests/planes_check.cpp builds the rest for the host)
 // bit j of a nibble -> bit 8j (byte j): one 24-bit multiply (no carries between the terms)
 __device__ __forceinline__ uint32_t spread4(uint32_t n4) { return __umul24(n4, 0x00204081u) & 0x01010101u; }
 
@@ -449,6 +454,8 @@ __device__ __forceinline__ uint32_t nibbles_to_i8x4(uint32_t s4, uint32_t y4, ui
     const uint32_t sel = spread4(s4) | (spread4(y4) << 1) | (uint32_t)(0x04040404ull << s);
     return __builtin_amdgcn_perm(0u, 0xFE02FF01u, sel);
 }
+
+#endif  // ACX_PLANES_HOST_CHECK
 
 // nibble j of a plane word (4 letters from letter 4j)
 template <int PW>

@@ -51,3 +51,39 @@ def state_digest(states, checkpoints=()):
         if i + 1 in want:
             cps[str(i + 1)] = h.hexdigest()
     return h.hexdigest(), cps
+
+
+def in_packed_domain(st, L):
+    """rows the packed kernels hold: letters in {-2..2}, zeros only as right padding"""
+    ok = ((st >= -2) & (st <= 2)).all(1)
+    for h in range(2):
+        nz = st[:, h * L:(h + 1) * L] != 0
+        n = nz.sum(1)
+        ok &= (nz == (np.arange(L)[None, :] < n[:, None])).all(1)
+    return ok
+
+
+def env_step_contract(st, a, cnt, resets, L, H, cyclical=True):
+    """One batched env step under acx's error contract (include/acx.h): the oracle's ACMove
+    (oracle/acx_oracle.c) for the rows that move; a failed move keeps the state and the step
+    count (done = truncated = 0, reward = -(n0+n1)); an out-of-domain row never moves (err 3);
+    same-step autoreset to `resets`, an out-of-domain starting row giving err 3.  Mutates st /
+    cnt; returns (reward, done, truncated, err)."""
+    from oracle import oracle as O
+    B = st.shape[0]
+    dom = in_packed_domain(st, L)
+    out, _, err = O.move_batch(st, a, L, cyclical)
+    err = err.copy()
+    err[~dom] = 3
+    ok = err == 0
+    st[ok] = out[ok]
+    n = (st[:, :L] != 0).sum(1) + (st[:, L:] != 0).sum(1)
+    triv = np.array([ok[b] and O.is_trivial(st[b]) for b in range(B)], dtype=bool)
+    cnt[ok] += 1
+    trunc = ok & (cnt >= H)
+    reward = np.where(triv, H * L * 2, -n).astype(np.int32)
+    reset = triv | trunc
+    st[reset] = resets[reset]
+    cnt[reset] = 0
+    err[reset & ~in_packed_domain(st, L)] = 3
+    return reward, triv.astype(np.uint8), trunc.astype(np.uint8), err

@@ -20,42 +20,15 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import oracle as O
+from conftest import env_step_contract
 
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda:0")
 
 
-def _in_domain(st, L):
-    """rows the packed kernels hold: letters in {-2..2}, zeros only as right padding"""
-    ok = ((st >= -2) & (st <= 2)).all(1)
-    for h in range(2):
-        nz = st[:, h * L:(h + 1) * L] != 0
-        n = nz.sum(1)
-        ok &= (nz == (np.arange(L)[None, :] < n[:, None])).all(1)
-    return ok
-
-
 def _model_step(st, a, cnt, resets, L, H):
-    """one step of the batched-API contract; mutates st / cnt, returns (reward, done, trunc, err)"""
-    B = st.shape[0]
-    dom = _in_domain(st, L)
-    out, lens, err = O.move_batch(st, a, L, True)
-    err = err.copy()
-    err[~dom] = 3
-    ok = err == 0
-    st[ok] = out[ok]
-    n = (st[:, :L] != 0).sum(1) + (st[:, L:] != 0).sum(1)
-    triv = np.array([ok[b] and O.is_trivial(st[b]) for b in range(B)])
-    cnt[ok] += 1
-    trunc = ok & (cnt >= H)
-    reward = np.where(triv, H * L * 2, -n).astype(np.int32)
-    reset = triv | trunc
-    st[reset] = resets[reset]
-    cnt[reset] = 0
-    err[reset & ~_in_domain(st, L)] = 3
-    return reward, triv.astype(np.uint8), trunc.astype(np.uint8), err
+    return env_step_contract(st, a, cnt, resets, L, H, True)
 
 
 def _starts(L, B, seed):
