@@ -1685,7 +1685,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 e = mo.e;
             }
             const bool ok = e == ACX_ERR_NONE;
-            clean = clean || ok;  // a successful general move leaves it clean
+            // a successful general move leaves both relators reduced -- clean unless the
+            // reduction emptied one (an unreduced input like [y^-1 y]: the reference keeps going
+            // with the empty relator, utils.py:264-266 checks only before the reduction)
+            clean = clean || (ok && p.n0 > 0 && p.n1 > 0);
             if (first_err == ACX_ERR_NONE) first_err = e;
             const bool triv = ok && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
             cnt += ok ? 1 : 0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)

@@ -51,15 +51,20 @@ def _error_stream(L, B, T, H, seed):
     # r0 == r1: moves 1 (r0 <- r0 r1^-1) and 2 (r1 <- r1 r0^-1) empty a relator (err 1)
     eq = rng.choice(B, size=B // 6, replace=False)
     st[eq, L:] = st[eq, :L]
+    # an unreduced r0 = y^-1 y: the first move's reduction empties it (no error: the reference
+    # checks validity before reducing, utils.py:264-266); conjugating it then raises (err 2)
+    emp = rng.choice(np.setdiff1d(np.arange(B), eq), size=B // 12, replace=False)
+    st[emp, :L] = 0
+    st[emp, 0], st[emp, 1] = -2, 2
     resets = st.copy()
     # out-of-domain input rows (err 3 from step 0): a letter 3, a zero inside r1, a letter 300
-    bad_in = rng.choice(np.setdiff1d(np.arange(B), eq), size=9, replace=False)
+    bad_in = rng.choice(np.setdiff1d(np.arange(B), np.concatenate([eq, emp])), size=9, replace=False)
     st[bad_in[:3], 0] = 3
     st[bad_in[3:6], L + 1] = 0
     st[bad_in[3:6], L + 2] = 1
     st[bad_in[6:], 1] = 300
     # out-of-domain starting rows (err 3 at the env's first autoreset)
-    bad_rs = rng.choice(np.setdiff1d(np.arange(B), np.concatenate([eq, bad_in])), size=7, replace=False)
+    bad_rs = rng.choice(np.setdiff1d(np.arange(B), np.concatenate([eq, emp, bad_in])), size=7, replace=False)
     resets[bad_rs[:3], L] = -5
     resets[bad_rs[3:], 2] = 0
     resets[bad_rs[3:], 3] = -2
@@ -132,10 +137,10 @@ def test_step_api_error_contract_vs_model(L, in_place):
         assert np.array_equal(g_err, e), t
         n = np.stack([(m_st[:, :L] != 0).sum(1), (m_st[:, L:] != 0).sum(1)], 1)
         assert np.array_equal(g_len, n), t
-        for k in (1, 3, 4):
+        for k in (1, 2, 3, 4):
             seen[k] |= (e == k).any()
         seen[0] |= bool((d | trn).any())
-    assert seen[[0, 1, 3, 4]].all(), seen  # every error kind and resets occurred
+    assert seen.all(), seen  # every error kind and resets occurred
     assert (steps[-1][0][bad_rs] == resets[bad_rs]).all()  # held as the out-of-domain starting row
 
 
