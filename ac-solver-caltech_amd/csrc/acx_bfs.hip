@@ -101,6 +101,7 @@ struct Args {
     int64_t need;      // max_nodes - n_before
     int64_t qcap;
     int P, L, kw, cyc, ntiles;
+    int kt;            // key-in-table layout (bfs_insert_kt_kernel)
 };
 
 // (1) expand: one block per tile of 64 parents; wave w makes the children of actions 3w..3w+2
@@ -186,6 +187,106 @@ __global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void bfs_expand_kernel(Args a
 __device__ __forceinline__ int64_t local_pos(const Args& a, uint64_t c) {
     const uint64_t s = c - 2, g = s / 12, act = s - 12 * g;
     return (int64_t)(((int64_t)(g >> 6) - a.tile0) * TILE_CH + act * TILE + (g & 63));
+}
+
+// Key-in-table layout (L <= KT_MAX_L: the 4L + 16 key bits fit 3 x 63): an entry is 4 words,
+// [code << 24 | fp, g0, g1, g2], two entries per 64-B bucket; g_j = (bits [63j, 63j + 63) of the
+// key) << 1 | 1.  The claimer CASes the first word, then stores g0..g2, so a reader sees each g_j
+// either as written (guard bit 1: the entry's state's key bits, exactly) or still 0: an entry
+// whose three guards are set decides equality from the bucket line alone; otherwise the state's
+// key is read from the store, as in the 8-entry layout.
+constexpr int KT_MAX_L = 43;
+constexpr int KT_ENT = 4;  // words per entry
+__host__ __device__ __forceinline__ void kt_guarded(const uint64_t* k, int kw, uint64_t (&g)[3]) {
+    const uint64_t k0 = k[0], k1 = kw > 1 ? k[1] : 0ull, k2 = kw > 2 ? k[2] : 0ull;
+    const uint64_t M = (1ull << 63) - 1;
+    g[0] = ((k0 & M) << 1) | 1ull;
+    g[1] = ((((k0 >> 63) | (k1 << 1)) & M) << 1) | 1ull;
+    g[2] = (((k1 >> 62) | (k2 << 2)) << 1) | 1ull;
+}
+
+// (2') key-in-table insert: a duplicate of a committed node costs one random line (its bucket)
+template <int KWM>
+__global__ __launch_bounds__(TPB, 8) void bfs_insert_kt_kernel(Args a) {
+    const int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (c >= (int64_t)a.ntiles * TILE_CH) return;
+    const int t = (int)(c / TILE_CH);
+    const int r = (int)(c - (int64_t)t * TILE_CH);
+    const int act = r / TILE, lane = r - act * TILE;
+    const int64_t g = (a.tile0 + t) * TILE + lane;
+    uint8_t res = 0;
+    if (g >= a.head && g < a.head + a.P) {
+        const uint32_t s = (uint32_t)(g - a.head) * 12u + (uint32_t)act;
+        const uint32_t end = min(a.ctl->succ, a.ctl->err);
+        if (s < end) {
+            const int kw = a.kw;
+            const uint64_t code = (uint64_t)g * 12 + act + 2;
+            const Key<KWM> key = kload<KWM>(a.store + (1 + (a.tile0 + t) * TILE_CH + r) * kw, kw);
+            const uint64_t h = khash<KWM>(key, kw);
+            const uint32_t fp = (uint32_t)(h >> 40);
+            const uint64_t my = (code << 24) | fp;
+            uint64_t gd[3];
+            kt_guarded(key.w, kw, gd);
+            uint64_t b = h & a.bmask;
+            for (uint64_t it = 0;; ++it) {
+                if (it > a.bmask) {
+                    atomicOr(&a.ctl->overflow, 1u);
+                    break;
+                }
+                uint64_t* bk = a.table + b * BUCKET;
+                uint64_t e[BUCKET];
+#pragma unroll
+                for (int j = 0; j < BUCKET; j += 2) {
+                    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(bk + j);
+                    e[j] = v.x;
+                    e[j + 1] = v.y;
+                }
+                int done = 0;  // 1 seen / lost, 2 holds the entry
+#pragma unroll
+                for (int j = 0; j < BUCKET / KT_ENT && !done; ++j) {
+                    uint64_t* ent = bk + KT_ENT * j;
+                    uint64_t v = e[KT_ENT * j];
+                    bool fresh = true;  // e[] holds this entry's words as read with v
+                    if (v == 0) {
+                        const uint64_t old = atomicCAS((unsigned long long*)ent, 0ull, (unsigned long long)my);
+                        if (old == 0) {
+                            ent[1] = gd[0];
+                            ent[2] = gd[1];
+                            ent[3] = gd[2];
+                            done = 2;
+                            break;
+                        }
+                        v = old;
+                        fresh = false;
+                    }
+                    if (((uint32_t)v & FP_MASK) != fp) continue;
+                    const uint64_t e1 = e[KT_ENT * j + 1], e2 = e[KT_ENT * j + 2], e3 = e[KT_ENT * j + 3];
+                    bool eq;
+                    if (fresh && (e1 & e2 & e3 & 1ull)) eq = e1 == gd[0] && e2 == gd[1] && e3 == gd[2];
+                    else eq = keq<KWM>(a.store + store_index(v >> 24) * kw, key, kw);
+                    if (!eq) continue;
+                    const uint64_t vc = v >> 24;
+                    if (vc < code) {
+                        done = 1;
+                        break;
+                    }
+                    const uint64_t old = atomicMin((unsigned long long*)ent, (unsigned long long)my);
+                    if (old < my) {
+                        done = 1;
+                    } else {
+                        a.lost[local_pos(a, old >> 24)] = 1;
+                        done = 2;
+                    }
+                }
+                if (done) {
+                    res = done == 2;
+                    break;
+                }
+                b = (b + 1) & a.bmask;
+            }
+        }
+    }
+    a.cand[c] = res;
 }
 
 // (2) lane per child: probe the visited set; claim an empty slot or join the state's entry
@@ -385,7 +486,15 @@ __global__ void bfs_root_kernel(Args a) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const Key<KWM> key = kload<KWM>(a.store, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
-    a.table[(h & a.bmask) * BUCKET] = (1ull << 24) | (uint32_t)(h >> 40);
+    uint64_t* ent = a.table + (h & a.bmask) * BUCKET;
+    ent[0] = (1ull << 24) | (uint32_t)(h >> 40);
+    if (a.kt) {
+        uint64_t gd[3];
+        kt_guarded(key.w, a.kw, gd);
+        ent[1] = gd[0];
+        ent[2] = gd[1];
+        ent[3] = gd[2];
+    }
     a.queue[0] = 1;
 }
 
@@ -494,6 +603,7 @@ struct Search {
 };
 
 static constexpr int64_t PATH_CAP = 1 << 16;
+static int g_bfs_layout = 0;  // 0 default (8-entry table), 2 key-in-table where L allows (tests, A/B)
 
 template <class T>
 static bool dalloc(T*& p, size_t n) {
@@ -510,7 +620,14 @@ struct ChunkLaunch {
         const unsigned wb = (unsigned)((a.ntiles + TPB / WAVE - 1) / (TPB / WAVE));
         const int64_t nc = (int64_t)a.ntiles * TILE_CH;
         bfs_expand_kernel<NW><<<dim3((unsigned)a.ntiles), dim3(TPB), 0, st>>>(a);
-        bfs_insert_kernel<NW + 1><<<dim3((unsigned)((nc + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(a);
+        bool kt_done = false;
+        if constexpr (NW <= 3) {  // L <= KT_MAX_L
+            if (a.kt) {
+                bfs_insert_kt_kernel<NW + 1><<<dim3((unsigned)((nc + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(a);
+                kt_done = true;
+            }
+        }
+        if (!kt_done) bfs_insert_kernel<NW + 1><<<dim3((unsigned)((nc + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(a);
         bfs_count_kernel<<<dim3(wb), dim3(TPB), 0, st>>>(a);
         bfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a);
         bfs_commit_kernel<<<dim3(wb), dim3(TPB), 0, st>>>(a);
@@ -562,8 +679,14 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     // every node and every claimed chunk entry at load <= 1/2, buckets of 8 (one 64-B line per
     // probe).  (Half that -- load <= 1, 134 MB at 10^7 nodes, inside the 256 MB MALL -- measured
     // 1.83 vs 1.93 ms at 10^7 but 18.4 vs 17.0 ms at 10^8 nodes: not taken.)
+    // Key-in-table (L <= KT_MAX_L, opt-in): 4 words per entry, entries >= 1.25x the same bound
+    // (2 per bucket; the bound counts a whole last chunk's children as new: the real load stays
+    // lower).  Measured slower than the 8-entry table (r03i: 2.11 vs 1.68 ms at 10^7 nodes, 20.0
+    // vs 14.2 ms at 10^8): the saved node-key reads cost less than the table's doubled footprint.
+    const bool kt = L <= KT_MAX_L && g_bfs_layout == 2;
     uint64_t ts = 1024;
-    while (ts < 2 * (uint64_t)(S->qcap + 12 * S->pmax)) ts <<= 1;
+    const uint64_t bound = (uint64_t)(S->qcap + 12 * S->pmax);
+    while (kt ? ts < 5 * bound : ts < 2 * bound) ts <<= 1;
     S->tsize = ts;
     Args& a = S->a;
     bool ok = dalloc(a.store, (size_t)(S->scap * S->kw)) && dalloc(a.queue, (size_t)S->qcap) &&
@@ -581,12 +704,17 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
         return nullptr;
     }
     a.bmask = ts / BUCKET - 1;
+    a.kt = kt ? 1 : 0;
     a.qcap = S->qcap;
     a.L = L;
     a.kw = S->kw;
     a.cyc = S->cyc;
     return S;
 }
+
+// test / A-B hook: 2 selects the key-in-table layout (L <= 43) for searches created afterwards,
+// 0 the default 8-entry table
+void acx_internal_bfs_layout(int32_t layout) { g_bfs_layout = layout; }
 
 void acx_bfs_destroy(void* h) { delete static_cast<Search*>(h); }
 

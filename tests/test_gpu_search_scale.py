@@ -56,6 +56,34 @@ def test_device_bfs_matches_reference_at_scale(c, chunk, capsys):
     _check_order(unpack_keys_np(st["node_keys"][: c["parents"]], c["L"]), c)
 
 
+@pytest.mark.parametrize("c", [c for c in BFS_CASES if c["L"] <= 43], ids=_id)
+def test_device_bfs_key_in_table_layout_matches_reference(c, capsys):
+    """The device BFS's second visited-set layout (opt-in through the test / A-B hook, L <= 43):
+    each state's key kept in its table entry behind guard bits, so a duplicate is decided from
+    the bucket line alone, against the same reference runs as the default 8-entry table
+    (fingerprint + a key read from the node store)."""
+    import ctypes
+    from acx import _lib
+    from acx.search import _device_bfs as D
+    hook = _lib.load().acx_internal_bfs_layout
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    D.release_workspaces()
+    hook(2)
+    try:
+        res = D.device_bfs(np.array(c["presentation"]), c["budget"], verbose=True,
+                           cyclically_reduce_after_moves=c["cyclical"], device=DEV, keep_node_keys=True)
+    finally:
+        hook(0)
+        D.release_workspaces()
+    out = capsys.readouterr().out.splitlines()
+    assert out == c["stdout"]
+    assert _result(*res) == [c["ok"], c["path"]]
+    st = D.LAST_STATS
+    assert st["parents"] == c["parents"]
+    _check_order(unpack_keys_np(st["node_keys"][: c["parents"]], c["L"]), c)
+
+
 @pytest.mark.parametrize("c", BFS_CASES, ids=_id)
 def test_host_engine_bfs_matches_reference_at_scale(c, capsys):
     from acx.search import _engine as E

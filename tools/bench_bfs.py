@@ -4,9 +4,11 @@ AK(3), L = 36, cyclical = False.
     python tools/bench_bfs.py [NODES,...]        (default 10^7)
 
 Per budget: the device BFS (csrc/acx_bfs.hip) to that many nodes, best of 3 wall-clock runs after
-a warm-up (workspace allocated once), with its statistics.  Then acx_expand12 with packed-key
+a warm-up (workspace allocated once), with its statistics; the same with the key-in-table layout
+(acx_internal_bfs_layout(2)) first.  Then acx_expand12 with packed-key
 output over the first 10^7 BFS nodes (the 12-way expansion kernel alone, 576 B per parent at
 L = 36), best of 3 HIP-event timings.  One JSON line on stdout."""
+import ctypes
 import json
 import os
 import sys
@@ -28,7 +30,24 @@ ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, 
 kw = _lib.key_words(L)
 res = {}
 keys = None
+layout_hook = _lib.load().acx_internal_bfs_layout
+layout_hook.argtypes = [ctypes.c_int32]
+layout_hook.restype = None
 for nb in budgets:
+    # the key-in-table layout (opt-in, acx_internal_bfs_layout(2)), A/B against the default below
+    layout_hook(2)
+    D.release_workspaces()
+    D.device_bfs(ak3, nb, device=dev)
+    walls8 = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        D.device_bfs(ak3, nb, device=dev)
+        walls8.append(time.perf_counter() - t0)
+    layout_hook(0)
+    D.release_workspaces()
+    res[f"device_bfs_keyintable_{nb:.0e}".replace("+", "")] = {"wall_ms": min(walls8) * 1e3,
+                                                          "walls_ms": [w * 1e3 for w in walls8]}
     D.device_bfs(ak3, nb, device=dev, keep_node_keys=keys is None)
     if keys is None:
         keys = D.LAST_STATS["node_keys"][: min(10 ** 7, D.LAST_STATS["nodes"])]

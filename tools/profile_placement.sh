@@ -11,7 +11,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 run() {  # name counters...
   local n=$1; shift
-  timeout -s KILL 120 rocprofv3 -E $R/tools/pmc_instances.yaml --pmc "$@" -d $OUT/$n -o r --output-format csv -- python3 $R/tools/placement_pmc.py > $OUT/$n.log 2>&1
+  timeout -s KILL 90 rocprofv3 -E $R/tools/pmc_instances.yaml --pmc "$@" -d $OUT/$n -o r --output-format csv -- python3 $R/tools/placement_pmc.py > $OUT/$n.log 2>&1
 }
 run inst ACX_WRREQ_I0 ACX_WRREQ_I1 ACX_WRREQ_I2 ACX_WRREQ_I3 ACX_WRREQ_I4 ACX_WRREQ_I5 ACX_WRREQ_I6 ACX_WRREQ_I7 ACX_WRREQ_I8 ACX_WRREQ_I9 ACX_WRREQ_I10 ACX_WRREQ_I11 ACX_WRREQ_I12 ACX_WRREQ_I13 ACX_WRREQ_I14 ACX_WRREQ_I15 || exit 1
 run xcc ACX_WRREQ_X0 ACX_WRREQ_X1 ACX_WRREQ_X2 ACX_WRREQ_X3 ACX_WRREQ_X4 ACX_WRREQ_X5 ACX_WRREQ_X6 ACX_WRREQ_X7 || exit 2
