@@ -1667,7 +1667,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         const int64_t ti = (int64_t)t * a.B;
         // opaque per step: keeps uniform-base + lane addressing in the loop (hoisted 64-bit
         // per-lane pointers are what the register allocator spills)
-        int ln = w.lane;
+        // the lane index recomputed per step (v_mbcnt), not held across the loop: a live copy
+        // was what the register allocator spilled, and its reload put a vmcnt(0) -- a drain of
+        // the previous step's stores -- at the top of every step
+        const int lane = (int)__lane_id();
+        int ln = lane;
         asm volatile("" : "+v"(ln));
         bool reset = false;
         bool both = false;  // the LDS image needs both relators (general move: both reduced)
@@ -1704,13 +1708,13 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         if (rb) {  // same-step autoreset to the starting states
             bool rbad = false;
             if (__popcll(rb) > RESET_TILE_MIN) {  // many lanes: one coalesced tile reload
-                tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
-                if (reset) rbad = tile.pack(w.lane, p);
+                tile.load(a.reset_state + w.r0 * twoL, w.R, lane);
+                if (reset) rbad = tile.pack(lane, p);
                 wave_sync();
                 reloaded = true;
             } else {  // a few lanes: the wave loads just their rows
-                tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
-                if (reset) rbad = tile.pack(w.lane, p);
+                tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, lane);
+                if (reset) rbad = tile.pack(lane, p);
             }
             if (reset) {
                 clean = pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc);
@@ -1724,24 +1728,24 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             // its target relator, a general move both; a row reset by load_rows already holds its
             // starting row; after a whole-tile reload every row is re-imaged
             if (w.active && !bad) {
-                if (reloaded || both) tile.unpack(w.lane, p);
-                else if (!reset) tile.unpack_half(w.lane, p, h1);
+                if (reloaded || both) tile.unpack(lane, p);
+                else if (!reset) tile.unpack_half(lane, p, h1);
             }
             if (__ballot(w.active && bad)) {
                 // rare: out-of-domain rows as their exact values from their fallback rows
-                tile.restore_flags(w.lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
+                tile.restore_flags(lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
                 if constexpr (OBS == 1)
                     tile.template store<true>(a.obs_traj + (ti + w.r0) * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
-                                              w.lane, a.reset_state + w.r0 * twoL);
+                                              lane, a.reset_state + w.r0 * twoL);
                 else
-                    store_rows_i8_fb(tile, a.obs_traj8 + (ti + w.r0) * twoL, w.R, twoL, w.lane, a.state + w.r0 * twoL,
+                    store_rows_i8_fb(tile, a.obs_traj8 + (ti + w.r0) * twoL, w.R, twoL, lane, a.state + w.r0 * twoL,
                                      a.reset_state + w.r0 * twoL);
                 wave_sync();
                 return;
             }
             wave_sync();
-            if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, w.lane);
-            else tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, w.lane);
+            if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
+            else tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, lane);
             wave_sync();
         }
     };
@@ -1784,6 +1788,11 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 q[g] = qg;
             }
             }
+            // consume the loaded words here: otherwise the waitcnt pass sees them pending where
+            // this block rejoins the step and puts a vmcnt(0) on the first use of the move id in
+            // EVERY step (a drain of the wave's previous trajectory stores per step)
+#pragma unroll
+            for (int k = 0; k < QW; ++k) asm volatile("" ::"v"(q[k]));
         }
         const uint32_t id = q[0] & 15u;
 #pragma unroll
@@ -2385,7 +2394,12 @@ int launch_step(StepArgs a, hipStream_t s) {
 }
 template <int NW, int LC, int VEC, int OBS>
 int launch_rollout(RolloutArgs a, hipStream_t s) {
+#ifdef ACX_AB_ROLLOUT_SHM  // A/B builds only (tools/ab_build.sh): pad LDS per block to cap resident blocks
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L) > (size_t)ACX_AB_ROLLOUT_SHM ? smem_bytes<NW, LC, VEC>(a.L)
+                                                                                  : (size_t)ACX_AB_ROLLOUT_SHM;
+#else
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+#endif
     rollout_kernel<NW, LC, VEC, OBS><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build L = 36-only variants of the env-step kernels (acx_kernels.hip alone, C-ABI included) for
+# in-process A/B timing (tools/ab_rollout.py), in parallel:
+#   bash tools/ab_build.sh NAME "-DFLAG=.. -DFLAG2=.." [NAME2 "FLAGS2" ...]   -> abv/libacx_NAME.so
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p $R/abv
+pids=()
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I$R/include -Wno-pass-failed \
+    -DACX_ISA_L36_ONLY $flags $R/ac-solver-caltech_amd/csrc/acx_kernels.hip $R/ac-solver-caltech_amd/csrc/acx_curriculum.hip -o $R/abv/libacx_$name.so &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p; done
+ls -la $R/abv
