@@ -370,6 +370,23 @@ struct FastTile {
         // rows are 2L = 8m bytes: a tile starts 16-byte aligned unless m and the row index are
         // both odd (L = 36 with an odd batch), then dword stores (wave-uniform branch)
         const bool al = (reinterpret_cast<uintptr_t>(g) & 15u) == 0;
+        if constexpr (S == CPR) {
+            if (R == WAVE && al) {
+                // full aligned tile (wave-uniform; every step of a full batch): one 16-byte LDS
+                // read and one 16-byte store per lane and chunk, no per-dword guards (the general
+                // loop below costs ~150 VALU per wave-step at L = 36)
+                constexpr int ND = WAVE * CPR;
+#pragma unroll
+                for (int u = 0; u < (ND + 4 * WAVE - 1) / (4 * WAVE); ++u) {
+                    const int d0 = 4 * (ln + u * WAVE);
+                    if ((u + 1) * 4 * WAVE > ND && d0 >= ND) continue;  // the last, partial chunk row
+                    const v4i_t x = *reinterpret_cast<const v4i_t*>(lds + d0);
+                    if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(dst + d0));
+                    else *reinterpret_cast<v4i_t*>(dst + d0) = x;
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (int u = 0; u < (WAVE * CPR + 4 * WAVE - 1) / (4 * WAVE); ++u) {
             const int d0 = 4 * (ln + u * WAVE);
@@ -1435,7 +1452,17 @@ __device__ __forceinline__ bool wave_ctx(int64_t rows, WaveCtx& w) {
     w.lane = threadIdx.x & (WAVE - 1);
     // wave-uniform (SGPR): the tile base, its row count and the addresses derived from them
     w.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+#if defined(ACX_AB_TILE_ORDER)  // A/B builds only (tools/ab_build.sh): which tiles are resident together
+    const int64_t G = gridDim.x, b = blockIdx.x;
+#if ACX_AB_TILE_ORDER == 1  // consecutive blocks 1/2 of the grid apart
+    const int64_t tb = (G % 2 == 0) ? (b % 2) * (G / 2) + b / 2 : b;
+#else  // each XCD (block b runs on XCD b % 8) owns a contiguous eighth of the tiles
+    const int64_t tb = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+#endif
+    w.r0 = (tb * WPB + w.wid) * WAVE;
+#else
     w.r0 = ((int64_t)blockIdx.x * WPB + w.wid) * WAVE;
+#endif
     if (w.r0 >= rows) return false;
     w.R = (int)((rows - w.r0) < WAVE ? (rows - w.r0) : WAVE);
     w.active = w.lane < w.R;
@@ -1661,6 +1688,17 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     // the previous step) at each use of `cnt`.
     __builtin_amdgcn_s_waitcnt(0);
     const int32_t* act_tile = a.actions + w.r0;  // wave-uniform
+#ifdef ACX_AB_STAGGER_US
+    // A/B builds only (tools/ab_build.sh): phase-stagger the first round's waves over one step
+    // period so that at any instant the waves storing are neighbours in the trajectory (a compact
+    // write front instead of 8,192 fronts 18 KB apart)
+    if (blockIdx.x < ACX_AB_STAGGER_BLOCKS) {
+        const uint64_t wr = (uint64_t)blockIdx.x * WPB + w.wid;
+        const uint64_t wait = (uint64_t)(ACX_AB_STAGGER_US * 100.0) * wr / ((uint64_t)ACX_AB_STAGGER_BLOCKS * WPB);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
+    }
+#endif
 
     // One env step of the wave: move, reward/done/truncated, autoreset, obs rows.
     auto step = [&](int t, uint32_t id) {

@@ -34,10 +34,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--reps", type=int, default=7)
-    ap.add_argument("--K", type=int, default=20)
+    ap.add_argument("--K", default="20", help="steps per launch; a comma list runs each K on the same buffers")
     ap.add_argument("--obs", default="both")
     a = ap.parse_args()
-    K, B, L, H = a.K, 1 << 20, 36, 200
+    # each entry "T" or "T@S": a T-step launch writing trajectory rows [S, S + T) of the buffer
+    Ks = [(int(x.split("@")[0]), int(x.split("@")[1]) if "@" in x else 0) for x in a.K.split(",")]
+    K, B, L, H = max(t + o for t, o in Ks), 1 << 20, 36, 200
     dev = torch.device("cuda:0")
     libs = [(os.path.basename(p), load(p)) for p in a.libs]
     starts = torch.as_tensor(ms_starts(L, B)).to(dev)
@@ -55,45 +57,59 @@ def main():
     state = torch.empty_like(starts)
     cnt = torch.zeros(B, dtype=torch.int32, device=dev)
     kinds = ["i32", "i8"] if a.obs == "both" else (["i32"] if a.obs == "32" else ["i8"])
-    ms = {(n, k): [] for n, _ in libs for k in kinds}
+    ms = {(n, k, T, off): [] for n, _ in libs for k in kinds for T, off in Ks}
     ref = {}
     for rep in range(a.reps + 1):
         for n, lib in libs:
             for k in kinds:
-                state.copy_(starts)
-                cnt.zero_()
-                ec.zero_()
-                torch.cuda.synchronize()
-                s = torch.cuda.current_stream().cuda_stream
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                assert lib.acx_pack_actions(acts.data_ptr(), pk.data_ptr(), K, B, s) == 0
-                if k == "i32":
-                    rc = lib.acx_rollout_packed(state.data_ptr(), pk.data_ptr(), starts.data_ptr(), cnt.data_ptr(),
-                                                o32.data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(),
-                                                err.data_ptr(), ec.data_ptr(), K, B, L, H, 1, s)
-                else:
-                    rc = lib.acx_rollout_obs8(state.data_ptr(), None, pk.data_ptr(), starts.data_ptr(), cnt.data_ptr(),
-                                              o8.data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(),
-                                              err.data_ptr(), ec.data_ptr(), K, B, L, H, 1, s)
-                e1.record()
-                torch.cuda.synchronize()
-                assert rc == 0 and int(ec.item()) == 0, (n, k, rc, int(ec.item()))
-                if rep > 0:
-                    ms[(n, k)].append(e0.elapsed_time(e1))
-                # every build must produce the same trajectory (checksums of the outputs)
-                o = o32 if k == "i32" else o8
-                sig = (int(o.sum(dtype=torch.int64)), int(rew.sum(dtype=torch.int64)), int(state.sum(dtype=torch.int64)))
-                ref.setdefault(k, sig)
-                assert ref[k] == sig, (n, k, sig, ref[k])
-    state_b = B * (16 * L + 8 + 1)
+              for T, off in Ks:
+                  state.copy_(starts)
+                  cnt.zero_()
+                  ec.zero_()
+                  torch.cuda.synchronize()
+                  s = torch.cuda.current_stream().cuda_stream
+                  e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                  e0.record()
+                  assert lib.acx_pack_actions(acts.data_ptr(), pk.data_ptr(), T, B, s) == 0
+                  if k == "i32":
+                      rc = lib.acx_rollout_packed(state.data_ptr(), pk.data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                                  o32[off].data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(),
+                                                  err.data_ptr(), ec.data_ptr(), T, B, L, H, 1, s)
+                  else:
+                      rc = lib.acx_rollout_obs8(state.data_ptr(), None, pk.data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                                o8[off].data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(),
+                                                err.data_ptr(), ec.data_ptr(), T, B, L, H, 1, s)
+                  e1.record()
+                  torch.cuda.synchronize()
+                  assert rc == 0 and int(ec.item()) == 0, (n, k, rc, int(ec.item()))
+                  if rep > 0:
+                      ms[(n, k, T, off)].append(e0.elapsed_time(e1))
+                  # every build must produce the same trajectory (checksums of the outputs)
+                  o = o32 if k == "i32" else o8
+                  sig = (int(o[off:off + T].sum(dtype=torch.int64)), int(rew[:T].sum(dtype=torch.int64)), int(state.sum(dtype=torch.int64)))
+                  ref.setdefault((k, T), sig)
+                  assert ref[(k, T)] == sig, (n, k, T, sig, ref[(k, T)])
+    # the same trajectory rows written by torch's fill_ (a one-pass linear write): their store rate
     out = {}
-    for (n, k), v in ms.items():
+    for T, off in Ks:
+        fills = []
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            o32[off:off + T].fill_(1)
+            e1.record()
+            torch.cuda.synchronize()
+            fills.append(e0.elapsed_time(e1))
+        f = statistics.median(fills)
+        out[f"fill_i32_K{T}@{off}"] = {"median_ms": round(f, 4), "TB_s": round(T * B * 8 * L / (f * 1e-3) / 1e12, 3)}
+    state_b = B * (16 * L + 8 + 1)
+    for (n, k, T, off), v in ms.items():
         per = 6.5 + (8 * L if k == "i32" else 2 * L)
-        nbytes = K * B * per + state_b
+        nbytes = T * B * per + state_b
         med = statistics.median(v)
-        out[f"{n}:{k}"] = {"median_ms": round(med, 4), "min_ms": round(min(v), 4), "all": [round(x, 4) for x in v],
-                           "frac_median": round(nbytes / med / 1e9 / 8000, 4)}
+        out[f"{n}:{k}:K{T}@{off}"] = {"median_ms": round(med, 4), "min_ms": round(min(v), 4), "all": [round(x, 4) for x in v],
+                           "frac_median": round(nbytes / (med * 1e-3) / 1e9 / 8000, 4)}
     print(json.dumps(out, indent=1))
 
 
