@@ -1452,17 +1452,7 @@ __device__ __forceinline__ bool wave_ctx(int64_t rows, WaveCtx& w) {
     w.lane = threadIdx.x & (WAVE - 1);
     // wave-uniform (SGPR): the tile base, its row count and the addresses derived from them
     w.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-#if defined(ACX_AB_TILE_ORDER)  // A/B builds only (tools/ab_build.sh): which tiles are resident together
-    const int64_t G = gridDim.x, b = blockIdx.x;
-#if ACX_AB_TILE_ORDER == 1  // consecutive blocks 1/2 of the grid apart
-    const int64_t tb = (G % 2 == 0) ? (b % 2) * (G / 2) + b / 2 : b;
-#else  // each XCD (block b runs on XCD b % 8) owns a contiguous eighth of the tiles
-    const int64_t tb = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
-#endif
-    w.r0 = (tb * WPB + w.wid) * WAVE;
-#else
     w.r0 = ((int64_t)blockIdx.x * WPB + w.wid) * WAVE;
-#endif
     if (w.r0 >= rows) return false;
     w.R = (int)((rows - w.r0) < WAVE ? (rows - w.r0) : WAVE);
     w.active = w.lane < w.R;
@@ -1688,17 +1678,6 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     // the previous step) at each use of `cnt`.
     __builtin_amdgcn_s_waitcnt(0);
     const int32_t* act_tile = a.actions + w.r0;  // wave-uniform
-#ifdef ACX_AB_STAGGER_US
-    // A/B builds only (tools/ab_build.sh): phase-stagger the first round's waves over one step
-    // period so that at any instant the waves storing are neighbours in the trajectory (a compact
-    // write front instead of 8,192 fronts 18 KB apart)
-    if (blockIdx.x < ACX_AB_STAGGER_BLOCKS) {
-        const uint64_t wr = (uint64_t)blockIdx.x * WPB + w.wid;
-        const uint64_t wait = (uint64_t)(ACX_AB_STAGGER_US * 100.0) * wr / ((uint64_t)ACX_AB_STAGGER_BLOCKS * WPB);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
-    }
-#endif
 
     // One env step of the wave: move, reward/done/truncated, autoreset, obs rows.
     auto step = [&](int t, uint32_t id) {
@@ -2432,12 +2411,7 @@ int launch_step(StepArgs a, hipStream_t s) {
 }
 template <int NW, int LC, int VEC, int OBS>
 int launch_rollout(RolloutArgs a, hipStream_t s) {
-#ifdef ACX_AB_ROLLOUT_SHM  // A/B builds only (tools/ab_build.sh): pad LDS per block to cap resident blocks
-    const size_t shm = smem_bytes<NW, LC, VEC>(a.L) > (size_t)ACX_AB_ROLLOUT_SHM ? smem_bytes<NW, LC, VEC>(a.L)
-                                                                                  : (size_t)ACX_AB_ROLLOUT_SHM;
-#else
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-#endif
     rollout_kernel<NW, LC, VEC, OBS><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }
