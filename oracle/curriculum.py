@@ -32,7 +32,9 @@ class RolloutEnvs:
         self.round1_complete = False
         self.episode = [[] for _ in range(num_envs)]
 
-    def step(self, actions, host_pick):
+    def step(self, actions, host_pick, on_done=None):
+        """on_done(i, action_list): called for a solved env before its restart choice, in env
+        order (training.py:267-292 precede :319-352 for the same env)."""
         B = self.state.shape[0]
         for i in range(B):
             self.episode[i].append(int(actions[i]))
@@ -45,6 +47,8 @@ class RolloutEnvs:
                 ep_len[i] = len(self.episode[i])
                 if d[i]:
                     info_actions[i] = list(self.episode[i])
+                    if on_done is not None:
+                        on_done(i, info_actions[i])
                 self.episode[i] = []
                 self.round1_complete = self.round1_complete or max(self.states_processed) == len(self.init) - 1
                 if not self.round1_complete:

@@ -140,3 +140,48 @@ def test_step_learner_matches_acx_step():
     assert lib.acx_step_learner(st_b.data_ptr(), None, bad.data_ptr(), rs.data_ptr(), cb.data_ptr(), None, None, None,
                                 None, None, None, 0, None, None, err.data_ptr(), None, B, L, 11, 1, stream) == 0
     assert (err == _lib.ERR_ACTION).all() and torch.equal(before, st_b)
+
+
+def _curriculum_cases():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_curriculum_golden import golden_cases
+    return golden_cases()
+
+
+@pytest.mark.parametrize("case", _curriculum_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize("fused", [True, False])
+def test_learner_env_matches_reference_training_loop(case, fused):
+    """LearnerEnv + CurriculumRecord against the reference's own ppo_training_loop run
+    (tests/golden/curriculum.npz): every step's rewards / done / truncated, the float32 next_obs
+    row buffer (post autoreset and curriculum restart), curr_states, and the final
+    success_record / ACMoves_hist / states_processed -- round-2 draws from `random` seeded as
+    the trainer seeds it (training.py:204)."""
+    import random
+
+    from acx.agents import CurriculumRecord, LearnerEnv
+    from test_curriculum_golden import check_final
+    name, m, g = case
+    init = g["initial_states"].astype(np.int32)
+    B, T, U, L = m["num_envs"], m["num_steps"], m["updates"], init.shape[1] // 2
+    env = LearnerEnv(init, B, horizon_length=m["horizon"], device=DEV)
+    rng = random.Random()
+    rec = CurriculumRecord(len(init), B, m["repeat_solved_prob"], rng=rng)
+    obs = torch.empty((B, 2 * L), dtype=torch.float32, device=DEV)
+    rew = torch.empty(B, dtype=torch.float32, device=DEV)
+    nd = torch.empty(B, dtype=torch.float32, device=DEV)
+    for u in range(1, U + 1):
+        rng.seed(m["seed"] + u)
+        for s in range(T):
+            t = (u - 1) * T + s
+            a = torch.as_tensor(g["actions"][t].astype(np.int64)).to(DEV)
+            done, trunc, _, needs_host = env.step(a, obs_out=obs, reward_out=rew, done_out=nd, fused=fused)
+            rec.process(env, done, trunc, needs_host, obs_out=obs)
+            assert np.array_equal(rew.cpu().numpy(), g["reward"][t].astype(np.float32)), (name, t)
+            assert np.array_equal(done.cpu().numpy(), g["done"][t]) and np.array_equal(trunc.cpu().numpy(),
+                                                                                     g["truncated"][t]), (name, t)
+            assert rec.curr_states == list(g["curr_states"][t]), (name, t)
+            assert env.curr_index.cpu().tolist() == rec.curr_states, (name, t)
+            assert np.array_equal(obs.cpu().numpy(), g["post_state"][t].astype(np.float32)), (name, t)
+            assert np.array_equal(env.state.cpu().numpy(), g["post_state"][t].astype(np.int32)), (name, t)
+    check_final(rec, m)
