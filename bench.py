@@ -542,7 +542,7 @@ def main():
     # and per-launch terms at any K, so the ratio is K-independent) and labelled as scaled.
     traffic, traffic_src = None, None
     cands = []
-    for tag in ("r02o_k20", "r02o", "r02h_k20", "r02h", "r02_k20", "r02", "r01"):
+    for tag in ("r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h", "r02_k20", "r02", "r01"):
         prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
