@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--no-bfs", action="store_true")
     ap.add_argument("--no-desync", action="store_true")
     ap.add_argument("--no-obs8", action="store_true")
+    ap.add_argument("--bfs-timeout", type=float, default=180.0,
+                    help="world > 1: seconds the sharded-BFS variant may take before the line is printed without it")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -524,14 +526,6 @@ def main():
                         f"visited set partitioned by key owner over {world} rank(s), RCCL exchanges per chunk",
         }
 
-    if not args.no_bfs:
-        from acx.search import _sharded_bfs as SB
-        try:  # a variant: its failure (the same on every rank) must not cost the headline line
-            variants["sharded_bfs"] = sharded_bfs_variant()
-        except Exception as e:  # noqa: BLE001
-            variants["sharded_bfs"] = {"error": repr(e)[:300]}
-        SB.release_workspaces()
-
     # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
     # used only when that profile's workload matches this run's
@@ -610,6 +604,33 @@ def main():
         "variants": variants,
         "env_errors": n_err,
     }
+    if not args.no_bfs:
+        # last, behind a watchdog: the one variant with collectives on its data path.  If its RCCL
+        # exchanges at world > 1 ever stalled, every rank's watchdog prints the line (rank 0) with
+        # the variant marked and exits, so a hang there cannot cost the headline line
+        import threading
+
+        from acx.search import _sharded_bfs as SB
+        variants["sharded_bfs"] = {"error": f"timeout after {args.bfs_timeout:.0f} s"}
+        timed_out_line = json.dumps(line)
+
+        def on_timeout():
+            if rank == 0:
+                print(timed_out_line, flush=True)
+            os._exit(0)
+
+        dog = threading.Timer(args.bfs_timeout, on_timeout) if world > 1 else None
+        if dog is not None:
+            dog.daemon = True
+            dog.start()
+        try:  # a variant: its failure (the same on every rank) must not cost the headline line
+            variants["sharded_bfs"] = sharded_bfs_variant()
+        except Exception as e:  # noqa: BLE001
+            variants["sharded_bfs"] = {"error": repr(e)[:300]}
+        if dog is not None:
+            dog.cancel()
+        SB.release_workspaces()
+
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
