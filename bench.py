@@ -523,7 +523,8 @@ def main():
             "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],
             "parents_expanded": st["parents"], "chunks": st["chunks"], "result": list(res) if res[0] else [False, None],
             "workload": "BASELINE configs[3]: bfs from AK(3), L=36, cyclical=False, to 10^7 nodes; node store and "
-                        f"visited set partitioned by key owner over {world} rank(s), RCCL exchanges per chunk",
+                        f"visited set partitioned by key owner over {world} rank(s), "
+                        f"{'RCCL' if backend == 'nccl' else backend} exchanges per chunk",
         }
 
     # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
@@ -615,8 +616,9 @@ def main():
         timed_out_line = json.dumps(line)
 
         def on_timeout():
-            if rank == 0:
-                print(timed_out_line, flush=True)
+            if rank == 0:  # the variant may be inside redirect_stdout: write to the real stdout
+                sys.__stdout__.write(timed_out_line + "\n")
+                sys.__stdout__.flush()
             os._exit(0)
 
         dog = threading.Timer(args.bfs_timeout, on_timeout) if world > 1 else None
