@@ -1,6 +1,6 @@
 """Driver for the device BFS (csrc/acx_bfs.hip, C-ABI acx_bfs_* in include/acx.h): the whole
 search -- queue, visited set, 12-way expansion, dedup, budget -- runs on the GPU; the host
-launches one round of kernels per chunk of parents.  Results equal
+enqueues the chunks of parents one ahead without waiting between them.  Results equal
 ac_solver/search/breadth_first.py:15-97 (same path, same budget cut)."""
 
 from __future__ import annotations
@@ -18,7 +18,8 @@ _HANDLES = {}  # (device, L, cyclical, chunk) -> (handle, capacity)
 def _handle(lib, dev: torch.device, L: int, cyclical: bool, chunk: int, max_nodes: int):
     key = (dev.index, L, bool(cyclical), int(chunk))
     h = _HANDLES.get(key)
-    # reuse a workspace that is big enough but not wastefully big (its table is cleared per run)
+    # reuse a workspace that is big enough but not wastefully big (a search never sees an earlier
+    # one's visited set: table entries carry the search's epoch, csrc/acx_bfs.hip)
     if h is not None and h[1] >= max_nodes and (h[1] <= 16 * max_nodes or h[1] <= (1 << 20)):
         return h[0]
     if h is not None:

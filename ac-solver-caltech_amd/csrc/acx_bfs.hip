@@ -13,7 +13,7 @@
 //   * an ACMove that empties a relator raises in the reference (utils.py:264-266): status
 //     ACX_BFS_MOVE_ERROR when it happens before the search would have ended;
 //   * min_length and the verbose "New minimal length found" sequence (:79-82) are the prefix
-//     minima of the child totals in sequential order (bfs_trace_kernel).
+//     minima of the child totals in sequential order (bfs_close_kernel).
 //
 // Layout.  Child (g, a) -- move a of the g-th node in FIFO order -- has the global sequence
 // number s = 12 g + a, its position in the reference's sequential order.  Every child key the
@@ -36,7 +36,14 @@
 //   3. bfs_count_kernel   wave per tile: survivors per tile;
 //   4. bfs_scan_kernel    exclusive scan of the tile counts;
 //   5. bfs_commit_kernel  wave per tile: survivors' codes appended to the queue in (parent,
-//                         action) order (LDS-staged, coalesced), the node-budget cut.
+//                         action) order (LDS-staged, coalesced), the node-budget cut;
+//   6. bfs_close_kernel   one block: the reference's decision for the chunk, the min_length
+//                         trace, the next chunk's parameters (Live, on the device) and a copy
+//                         of the state in pinned host memory.
+// The host never sits between chunks: it keeps one chunk enqueued beyond the one whose outcome
+// it is reading (grids sized for an upper bound, parameters read from Live), so a chunk's
+// kernels follow the previous chunk's back to back (round 3: 10^7 nodes had 8 host round trips
+// of ~20 us plus a D2H copy and a reset kernel per chunk, a quarter of the search's time).
 // Cross-XCD visibility: every value a kernel compares against (child keys, queue codes) was
 // written by an earlier kernel; within bfs_insert_kernel an entry only goes 0 -> one state's
 // code -> a smaller code of the same state, so stale plain reads are harmless (a stale 0 is
@@ -62,6 +69,12 @@ constexpr int TILE_CH = 12 * TILE;      // children per tile
 constexpr int BUCKET = 8;               // table entries per bucket (64 B)
 constexpr int TRACE_CAP = 1024;         // new-minimum records per trace walk (<= 2L + 1 ever)
 constexpr uint32_t FP_MASK = 0xffffffu;
+// 8-entry table: entry = epoch << 58 | code << 24 | fp; codes < 12 (2^30 + 12) + 14 < 2^34.  An
+// entry of another epoch (an earlier search on this workspace) is an empty slot, so a search
+// does not clear the table (it did: a 512 MB memset per 10^7-node search); the table is
+// cleared only when the 6-bit epoch wraps.
+constexpr int EP_SHIFT = 58;
+constexpr uint64_t CODE_MASK = (1ull << 34) - 1;
 
 // store index (in keys) of the node with code c
 __host__ __device__ __forceinline__ int64_t store_index(uint64_t c) {
@@ -83,7 +96,26 @@ struct Ctl {
     uint32_t pad;
 };
 
+// The search's state across chunks, kept on the device (bfs_close_kernel advances it), so the
+// host can enqueue several chunks ahead without reading anything back; every chunk kernel takes
+// its chunk's parameters from here and does nothing once `stop` is set.
+struct Live {
+    int64_t head;       // FIFO index of the next chunk's first parent
+    int64_t n_nodes;    // len(tree_nodes)
+    int64_t parents;    // parents the reference has expanded
+    int64_t chunks;     // chunks run
+    int64_t max_nodes, pmax;
+    int64_t tile0;      // next chunk: head / 64
+    int64_t succ_node, succ_act;
+    int32_t P, ntiles;  // next chunk: parents, tiles
+    uint32_t stop;      // the search has ended: later chunks do nothing
+    int32_t status;     // ACX_BFS_* once stopped; -1 table overflow
+    uint32_t running;   // min_length so far (breadth_first.py:79-82)
+    uint32_t ntrace;    // "New minimal length" records so far
+};
+
 struct Args {
+    Live* live;        // per-chunk parameters below are loaded from here (chunk_args)
     uint64_t* store;   // (scap, kw) node / child keys, store_index layout
     uint64_t* queue;   // (qcap) node codes in FIFO order
     uint8_t* cand;     // (ntiles * 768) child holds its state's entry after its own probe
@@ -102,7 +134,22 @@ struct Args {
     int64_t qcap;
     int P, L, kw, cyc, ntiles;
     int kt;            // key-in-table layout (bfs_insert_kt_kernel)
+    uint64_t ep;       // this search's epoch << EP_SHIFT (8-entry table)
 };
+
+// this chunk's parameters from the device-side state; false once the search has ended (the
+// chunk was enqueued speculatively and has nothing to do)
+__device__ __forceinline__ bool chunk_args(Args& a) {
+    const Live* lv = a.live;
+    if (lv->stop) return false;
+    a.head = lv->head;
+    a.P = lv->P;
+    a.tile0 = lv->tile0;
+    a.ntiles = lv->ntiles;
+    a.n_before = lv->n_nodes;
+    a.need = lv->max_nodes - lv->n_nodes;
+    return true;
+}
 
 // (1) expand: one block per tile of 64 parents; wave w makes the children of actions 3w..3w+2
 // (4x the lanes of a lane-per-parent loop: the move chain is latency-bound, and a 2^19-parent
@@ -112,8 +159,10 @@ template <int NW>
 __global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void bfs_expand_kernel(Args a) {
     __shared__ uint64_t kst[TPB / WAVE][TILE * (NW + 1)];
     __shared__ uint32_t smin[TILE];
+    if (!chunk_args(a)) return;
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-    const int t = blockIdx.x;  // one tile per block
+    const int t = blockIdx.x;  // one tile per block (the grid is an upper bound on the tiles)
+    if (t >= a.ntiles) return;
     const int64_t gt = (a.tile0 + t) * TILE;  // FIFO index of the tile's parent 0
     const int64_t g = gt + lane;
     const bool active = g >= a.head && g < a.head + a.P;
@@ -208,6 +257,7 @@ __host__ __device__ __forceinline__ void kt_guarded(const uint64_t* k, int kw, u
 // (2') key-in-table insert: a duplicate of a committed node costs one random line (its bucket)
 template <int KWM>
 __global__ __launch_bounds__(TPB, 8) void bfs_insert_kt_kernel(Args a) {
+    if (!chunk_args(a)) return;
     const int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (c >= (int64_t)a.ntiles * TILE_CH) return;
     const int t = (int)(c / TILE_CH);
@@ -292,6 +342,7 @@ __global__ __launch_bounds__(TPB, 8) void bfs_insert_kt_kernel(Args a) {
 // (2) lane per child: probe the visited set; claim an empty slot or join the state's entry
 template <int KWM>
 __global__ __launch_bounds__(TPB, 8) void bfs_insert_kernel(Args a) {  // 8 waves/SIMD: latency-bound, SGPRs capped at 96
+    if (!chunk_args(a)) return;
     const int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (c >= (int64_t)a.ntiles * TILE_CH) return;
     const int t = (int)(c / TILE_CH);
@@ -308,7 +359,7 @@ __global__ __launch_bounds__(TPB, 8) void bfs_insert_kernel(Args a) {  // 8 wave
             const Key<KWM> key = kload<KWM>(a.store + (1 + (a.tile0 + t) * TILE_CH + r) * kw, kw);
             const uint64_t h = khash<KWM>(key, kw);
             const uint32_t fp = (uint32_t)(h >> 40);
-            const uint64_t my = (code << 24) | fp;
+            const uint64_t my = a.ep | (code << 24) | fp;
             uint64_t b = h & a.bmask;
             for (uint64_t it = 0;; ++it) {
                 if (it > a.bmask) {
@@ -327,16 +378,17 @@ __global__ __launch_bounds__(TPB, 8) void bfs_insert_kernel(Args a) {  // 8 wave
 #pragma unroll
                 for (int j = 0; j < BUCKET && !done; ++j) {
                     uint64_t v = e[j];
-                    if (v == 0) {
-                        const uint64_t old = atomicCAS((unsigned long long*)(bk + j), 0ull, (unsigned long long)my);
-                        if (old == 0) {
+                    if ((v >> EP_SHIFT) != (a.ep >> EP_SHIFT)) {  // empty in this search
+                        const uint64_t old = atomicCAS((unsigned long long*)(bk + j), (unsigned long long)v,
+                                                       (unsigned long long)my);
+                        if (old == v) {
                             done = 2;
                             break;
                         }
-                        v = old;
+                        v = old;  // claimed meanwhile: a value of this search
                     }
                     if (((uint32_t)v & FP_MASK) != fp) continue;
-                    const uint64_t vc = v >> 24;
+                    const uint64_t vc = (v >> 24) & CODE_MASK;
                     if (!keq<KWM>(a.store + store_index(vc) * kw, key, kw)) continue;
                     if (vc < code) {  // an earlier occurrence (a node, or an earlier child of the chunk)
                         done = 1;
@@ -346,7 +398,7 @@ __global__ __launch_bounds__(TPB, 8) void bfs_insert_kernel(Args a) {  // 8 wave
                     if (old < my) {
                         done = 1;
                     } else {  // replaced a later child of the chunk: it learns it lost
-                        a.lost[local_pos(a, old >> 24)] = 1;
+                        a.lost[local_pos(a, (old >> 24) & CODE_MASK)] = 1;
                         done = 2;
                     }
                 }
@@ -377,6 +429,7 @@ __device__ __forceinline__ uint32_t survivors(const Args& a, int t, int lane, bo
 
 // (3) survivors per tile
 __global__ __launch_bounds__(TPB) void bfs_count_kernel(Args a) {
+    if (!chunk_args(a)) return;
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     const int t = blockIdx.x * (TPB / WAVE) + wid;
     if (t >= a.ntiles) return;
@@ -387,6 +440,7 @@ __global__ __launch_bounds__(TPB) void bfs_count_kernel(Args a) {
 // (4) exclusive scan of the tile counts (one block of 1024 threads)
 __global__ __launch_bounds__(1024) void bfs_scan_kernel(Args a) {
     __shared__ uint32_t sh[1024 / WAVE];
+    if (!chunk_args(a)) return;
     const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
     const int nb = a.ntiles;
     const int per = (nb + 1023) / 1024;
@@ -423,6 +477,7 @@ __global__ __launch_bounds__(1024) void bfs_scan_kernel(Args a) {
 // (5) append the survivors' codes in (parent, action) order; the node-budget cut
 __global__ __launch_bounds__(TPB) void bfs_commit_kernel(Args a) {
     __shared__ uint64_t stage[TPB / WAVE][TILE_CH];
+    if (!chunk_args(a)) return;
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     const int t = blockIdx.x * (TPB / WAVE) + wid;
     if (t >= a.ntiles) return;
@@ -461,25 +516,6 @@ __global__ __launch_bounds__(TPB) void bfs_commit_kernel(Args a) {
         if (n0 + i < a.qcap) a.queue[n0 + i] = st[i];
 }
 
-// the chunk's control block to its initial values (a kernel, so the reset is asynchronous on
-// the stream: a host-to-device copy from pageable memory blocks the host for its duration)
-__global__ void bfs_ctl_reset_kernel(Ctl* c) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Ctl z;
-    memset(&z, 0, sizeof(z));
-    z.succ = z.err = z.cut_p = z.min_len = NONE;
-    *c = z;
-}
-
-// wait for the stream by polling (hipStreamSynchronize may sleep and wake late: one wait per
-// chunk is on the search's critical path)
-static int stream_wait(hipStream_t st) {
-    hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
-    }
-    return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
-}
-
 // root: node 0 (code 1) and its table entry
 template <int KWM>
 __global__ void bfs_root_kernel(Args a) {
@@ -487,7 +523,7 @@ __global__ void bfs_root_kernel(Args a) {
     const Key<KWM> key = kload<KWM>(a.store, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
     uint64_t* ent = a.table + (h & a.bmask) * BUCKET;
-    ent[0] = (1ull << 24) | (uint32_t)(h >> 40);
+    ent[0] = a.ep | (1ull << 24) | (uint32_t)(h >> 40);  // (a.ep is 0 in the key-in-table layout)
     if (a.kt) {
         uint64_t gd[3];
         kt_guarded(key.w, a.kw, gd);
@@ -498,60 +534,162 @@ __global__ void bfs_root_kernel(Args a) {
     a.queue[0] = 1;
 }
 
-// min_length trace over the chunk's children in sequential order up to (exclusive) seq `end`
-// (one block): parents whose min child total beats the running minimum are found with a
-// prefix-min scan; those few are re-expanded and walked move by move (breadth_first.py:79-82)
+// the control block to its initial values (before each chunk)
+__device__ __forceinline__ void ctl_reset(Ctl* c) {
+    Ctl z;
+    memset(&z, 0, sizeof(z));
+    z.succ = z.err = z.cut_p = z.min_len = NONE;
+    *c = z;
+}
+
+// the search's state before its first chunk (one thread)
+__global__ void bfs_init_kernel(Args a, int64_t max_nodes, int64_t pmax, uint32_t total0) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Live* lv = a.live;
+    Live z;
+    memset(&z, 0, sizeof(z));
+    z.n_nodes = 1;
+    z.max_nodes = max_nodes;
+    z.pmax = pmax;
+    z.P = 1;
+    z.ntiles = 1;
+    z.status = ACX_BFS_EXHAUSTED;
+    z.running = total0;
+    *lv = z;
+    ctl_reset(a.ctl);
+}
+
+// what the host reads after each chunk (pinned host memory, one slot per chunk in flight)
+struct LiveMirror {
+    Live s;
+    uint64_t seq;  // chunk number + 1 once the slot holds that chunk's state
+};
+constexpr int RING = 4;
+
+// (6) close the chunk (one block, after commit), in the reference's order: a raising child
+// before the first success and not after the budget cut -> AssertionError; else a success not
+// after the cut -> the path; else the cut -> the budget message; else the next chunk; an empty
+// queue -> (False, None).  Then min_length: when the chunk's minimum child total beats the
+// running minimum, the parents whose minimum does are found with a prefix-min scan and walked
+// move by move, appending the reference's "New minimal length found" values
+// (breadth_first.py:79-82).  Then the state for the next chunk, the control block reset, and
+// the state published to the host's slot for chunk `k` (also when the search had already ended
+// before this speculatively enqueued chunk).
 template <int NW>
-__global__ __launch_bounds__(256) void bfs_trace_kernel(Args a, uint32_t end, uint32_t running) {
+__global__ __launch_bounds__(256) void bfs_close_kernel(Args a, int64_t k, LiveMirror* mirror, uint16_t* trace_host) {
     __shared__ uint32_t lmin[256];
     __shared__ uint32_t list[TRACE_CAP];
-    __shared__ uint32_t nlist;
+    __shared__ uint32_t nlist, s_end, s_trace;
     const int t = threadIdx.x;
-    const int64_t np = ((int64_t)end + 11) / 12;  // parents with children before `end`
-    const int64_t per = (np + 255) / 256;
-    const int64_t p0 = t * per, p1 = min<int64_t>(np, p0 + per);
-    uint32_t m = 0xffffffffu;
-    for (int64_t p = p0; p < p1; ++p) m = min(m, (uint32_t)a.pmin[p]);
-    lmin[t] = m;
-    if (t == 0) nlist = 0;
-    __syncthreads();
-    uint32_t r = running;
-    for (int i = 0; i < t; ++i) r = min(r, lmin[i]);
-    for (int64_t p = p0; p < p1; ++p) {
-        const uint32_t v = a.pmin[p];
-        if (v < r) {
-            const uint32_t k = atomicAdd(&nlist, 1u);
-            if (k < TRACE_CAP) list[k] = (uint32_t)p;
-            r = v;
-        }
+    Live* lv = a.live;
+    const bool run = chunk_args(a);
+    bool ends = false, err_first = false, succ_first = false;
+    int64_t cut = INT64_MAX, err_p = INT64_MAX, suc_p = INT64_MAX;
+    Ctl c;
+    if (run && t == 0) {
+        c = *a.ctl;
+        cut = c.cut_p == NONE ? INT64_MAX : (int64_t)c.cut_p;
+        err_p = c.err == NONE ? INT64_MAX : (int64_t)(c.err / 12);
+        suc_p = c.succ == NONE ? INT64_MAX : (int64_t)(c.succ / 12);
+        err_first = c.err != NONE && c.err < c.succ && err_p <= cut;
+        succ_first = !err_first && c.succ != NONE && suc_p <= cut;
+        ends = err_first || succ_first || cut != INT64_MAX;
+        // children the reference looks at in this chunk, in order: up to and including the
+        // success child, up to (not including) the raising child, through the cut parent
+        s_end = err_first ? c.err : succ_first ? c.succ + 1 : cut != INT64_MAX ? (uint32_t)((cut + 1) * 12)
+                                                                                : (uint32_t)a.P * 12u;
+        s_trace = !c.overflow && c.min_len < lv->running;
+        nlist = 0;
     }
     __syncthreads();
-    if (t != 0) return;
-    const uint32_t n = min(nlist, (uint32_t)TRACE_CAP);
-    for (uint32_t i = 1; i < n; ++i) {  // insertion sort: the parents in order (few)
-        const uint32_t v = list[i];
-        uint32_t j = i;
-        for (; j > 0 && list[j - 1] > v; --j) list[j] = list[j - 1];
-        list[j] = v;
-    }
-    uint32_t cur = running, nt = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t p = list[i];
-        PresRegs<NW> pr;
-        load_key<NW>(a.store + store_index(a.queue[a.head + p]) * a.kw, a.kw, a.L, pr);
-        for (int act = 0; act < 12 && p * 12u + act < end; ++act) {
-            PresRegs<NW> q = pr;
-            if (ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, a.cyc != 0) != ACX_ERR_NONE) continue;
-            const uint32_t tot = (uint32_t)(q.n0 + q.n1);
-            if (tot < cur) {
-                cur = tot;
-                if (nt < TRACE_CAP) a.trace[nt] = (uint16_t)tot;
-                ++nt;
+    if (run && s_trace) {
+        const uint32_t end = s_end, running = lv->running;
+        const int64_t np = ((int64_t)end + 11) / 12;  // parents with children before `end`
+        const int64_t per = (np + 255) / 256;
+        const int64_t p0 = t * per, p1 = min<int64_t>(np, p0 + per);
+        uint32_t m = 0xffffffffu;
+        for (int64_t p = p0; p < p1; ++p) m = min(m, (uint32_t)a.pmin[p]);
+        lmin[t] = m;
+        __syncthreads();
+        uint32_t r = running;
+        for (int i = 0; i < t; ++i) r = min(r, lmin[i]);
+        for (int64_t p = p0; p < p1; ++p) {
+            const uint32_t v = a.pmin[p];
+            if (v < r) {
+                const uint32_t q = atomicAdd(&nlist, 1u);
+                if (q < TRACE_CAP) list[q] = (uint32_t)p;
+                r = v;
             }
         }
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t n = min(nlist, (uint32_t)TRACE_CAP);
+            for (uint32_t i = 1; i < n; ++i) {  // insertion sort: the parents in order (few)
+                const uint32_t v = list[i];
+                uint32_t j = i;
+                for (; j > 0 && list[j - 1] > v; --j) list[j] = list[j - 1];
+                list[j] = v;
+            }
+            uint32_t cur = running, nt = lv->ntrace;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t p = list[i];
+                PresRegs<NW> pr;
+                load_key<NW>(a.store + store_index(a.queue[a.head + p]) * a.kw, a.kw, a.L, pr);
+                for (int act = 0; act < 12 && p * 12u + act < end; ++act) {
+                    PresRegs<NW> q = pr;
+                    if (ac_move<NW>(q.w0, q.n0, q.w1, q.n1, act, a.L, a.cyc != 0) != ACX_ERR_NONE) continue;
+                    const uint32_t tot = (uint32_t)(q.n0 + q.n1);
+                    if (tot < cur) {
+                        cur = tot;
+                        if (nt < TRACE_CAP) trace_host[nt] = (uint16_t)tot;  // pinned host memory
+                        ++nt;
+                    }
+                }
+            }
+            lv->ntrace = nt;
+            lv->running = cur;
+        }
     }
-    a.ctl->ntrace = nt;
-    a.ctl->trace_min = cur;
+    if (t != 0) return;
+    if (run) {
+        if (c.overflow) {
+            lv->status = -1;
+            lv->stop = 1;
+        } else if (ends) {
+            const int64_t last = err_first ? err_p : succ_first ? suc_p : cut;
+            lv->parents += last + 1;
+            if (err_first) {
+                lv->status = ACX_BFS_MOVE_ERROR;
+            } else if (succ_first) {
+                lv->status = ACX_BFS_FOUND;
+                lv->succ_node = a.head + suc_p;
+                lv->succ_act = c.succ % 12;
+            } else {
+                lv->status = ACX_BFS_BUDGET;
+                lv->n_nodes = (int64_t)c.nodes_at_cut;
+            }
+            lv->stop = 1;
+        } else {
+            lv->parents += a.P;
+            lv->n_nodes += (int64_t)c.total_new;
+            lv->head += a.P;
+            if (lv->head >= lv->n_nodes) {  // the queue ran dry: (False, None)
+                lv->status = ACX_BFS_EXHAUSTED;
+                lv->stop = 1;
+            } else {
+                const int64_t avail = lv->n_nodes - lv->head;
+                lv->P = (int32_t)(avail < lv->pmax ? avail : lv->pmax);
+                lv->tile0 = lv->head / TILE;
+                lv->ntiles = (int32_t)((lv->head + lv->P - 1) / TILE - lv->tile0 + 1);
+            }
+        }
+        lv->chunks += 1;
+        ctl_reset(a.ctl);
+    }
+    LiveMirror* m = mirror + (k % RING);
+    m->s = *lv;
+    __threadfence_system();
+    __hip_atomic_store(&m->seq, (uint64_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // path root -> node (FIFO index v): (action, total length) per edge into out[0..2*depth)
@@ -586,19 +724,29 @@ struct Search {
     int64_t last_nodes = 0;  // len(tree_nodes) at the end of the last run (<= qcap)
     uint64_t tsize = 0;
     Args a{};
-    Ctl* ctl_host = nullptr;
+    LiveMirror* mirror = nullptr;  // pinned host memory, RING slots (bfs_close_kernel publishes)
+    hipEvent_t ev[RING] = {};      // recorded after each chunk's close kernel
+    hipEvent_t fin = nullptr;      // after a search's last (speculative) chunk: the next search
+                                   // and the destructor wait for it (any stream)
+    bool fin_pending = false;
+    int64_t kbase = 0;             // chunks enqueued by earlier searches
+    int epoch = 0;                 // 8-entry table: the last search's epoch (0: table all zero)
     uint16_t* trace_host = nullptr;
     int32_t* path_dev = nullptr;
     int64_t* path_n_dev = nullptr;
     std::vector<int32_t> trace;  // new minima of the last run, in order
 
     ~Search() {
+        if (fin_pending) (void)hipEventSynchronize(fin);
         void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.tmin, a.table, a.ctl, a.trace, path_dev,
-                        path_n_dev};
+                        path_n_dev, a.live};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
-        if (ctl_host) (void)hipHostFree(ctl_host);
+        if (mirror) (void)hipHostFree(mirror);
         if (trace_host) (void)hipHostFree(trace_host);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (fin) (void)hipEventDestroy(fin);
     }
 };
 
@@ -610,16 +758,19 @@ static bool dalloc(T*& p, size_t n) {
     return hipMalloc((void**)&p, n * sizeof(T) + 64) == hipSuccess;
 }
 
-// launches of one chunk, templated on the key-word bound
+// launches of one chunk (number k), templated on the key-word bound; the grids cover `ntiles`
+// tiles, an upper bound on the chunk's real tile count (the kernels read the real one, Live)
 struct ChunkLaunch {
     Search* S;
     hipStream_t st;
+    int64_t k;
+    int ntiles;
     template <int NW>
     void go() {
         Args& a = S->a;
-        const unsigned wb = (unsigned)((a.ntiles + TPB / WAVE - 1) / (TPB / WAVE));
-        const int64_t nc = (int64_t)a.ntiles * TILE_CH;
-        bfs_expand_kernel<NW><<<dim3((unsigned)a.ntiles), dim3(TPB), 0, st>>>(a);
+        const unsigned wb = (unsigned)((ntiles + TPB / WAVE - 1) / (TPB / WAVE));
+        const int64_t nc = (int64_t)ntiles * TILE_CH;
+        bfs_expand_kernel<NW><<<dim3((unsigned)ntiles), dim3(TPB), 0, st>>>(a);
         bool kt_done = false;
         if constexpr (NW <= 3) {  // L <= KT_MAX_L
             if (a.kt) {
@@ -631,6 +782,7 @@ struct ChunkLaunch {
         bfs_count_kernel<<<dim3(wb), dim3(TPB), 0, st>>>(a);
         bfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a);
         bfs_commit_kernel<<<dim3(wb), dim3(TPB), 0, st>>>(a);
+        bfs_close_kernel<NW><<<dim3(1), dim3(256), 0, st>>>(a, k, S->mirror, S->trace_host);
     }
 };
 struct RootLaunch {
@@ -646,14 +798,6 @@ struct PathLaunch {
     template <int NW>
     void go() { bfs_path_kernel<NW><<<dim3(1), dim3(64), 0, st>>>(S->a, node, S->path_dev, PATH_CAP, S->path_n_dev); }
 };
-struct TraceLaunch {
-    Search* S;
-    hipStream_t st;
-    uint32_t end, running;
-    template <int NW>
-    void go() { bfs_trace_kernel<NW><<<dim3(1), dim3(256), 0, st>>>(S->a, end, running); }
-};
-
 }  // namespace bfs
 }  // namespace acx
 
@@ -694,10 +838,13 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
               dalloc(a.pmin, (size_t)S->pmax) && dalloc(a.tsum, (size_t)S->tiles_max) &&
               dalloc(a.tmin, (size_t)S->tiles_max) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.trace, (size_t)TRACE_CAP) && dalloc(S->path_dev, (size_t)(2 * PATH_CAP)) &&
-              dalloc(S->path_n_dev, 1) &&
-              hipHostMalloc((void**)&S->ctl_host, sizeof(Ctl), hipHostMallocDefault) == hipSuccess &&
+              dalloc(S->path_n_dev, 1) && dalloc(a.live, 1) &&
+              hipHostMalloc((void**)&S->mirror, sizeof(LiveMirror) * RING, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void**)&S->trace_host, sizeof(uint16_t) * TRACE_CAP, hipHostMallocDefault) == hipSuccess &&
-              hipMemset(a.lost, 0, (size_t)(S->tiles_max * TILE_CH)) == hipSuccess;
+              hipMemset(a.lost, 0, (size_t)(S->tiles_max * TILE_CH)) == hipSuccess &&
+              hipMemset(a.table, 0, (size_t)ts * 8) == hipSuccess;
+    for (auto& e : S->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&S->fin, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         delete S;
@@ -731,77 +878,75 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     int total0 = 0;
     for (int i = 0; i < 2 * L; ++i) total0 += presentation[i] != 0;
 
+    // the previous search's speculative chunk may still be in flight (on another stream, too)
+    if (S->fin_pending && hipStreamWaitEvent(st, S->fin, 0) != hipSuccess) return ACX_E_LAUNCH;
     if (hipMemcpyAsync(a.store, root, (size_t)kw * 8, hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
-    if (hipMemsetAsync(a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (a.kt) {  // key-in-table entries have no epoch: cleared per search
+        if (hipMemsetAsync(a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
+        a.ep = 0;
+    } else {
+        if (++S->epoch == 64) {  // the epoch wraps: clear once every 63 searches
+            if (hipMemsetAsync(a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
+            S->epoch = 1;
+        }
+        a.ep = (uint64_t)S->epoch << EP_SHIFT;
+    }
     RootLaunch rl{S, st};
     by_nw(L, rl);
+    bfs_init_kernel<<<dim3(1), dim3(64), 0, st>>>(a, max_nodes, S->pmax, (uint32_t)total0);
 
+    // Chunks are enqueued one ahead of the one the host waits for: chunk k + 1 is in the stream
+    // before the host reads chunk k's outcome, so no chunk waits for a host round trip.  Its
+    // grids are sized for an upper bound on its parents -- after chunk k the queue holds at most
+    // avail_k - P_k + 12 P_k unexpanded nodes -- and its kernels take the real parameters from
+    // the device state; once the search has ended they do nothing.
     S->trace.clear();
-    int64_t n_nodes = 1, head = 0, parents = 0, chunks = 0;
-    int64_t min_len = total0, path_len = 0;
-    int status = ACX_BFS_EXHAUSTED;
-    int64_t succ_node = -1, succ_act = -1;
-    while (head < n_nodes) {
-        const int64_t avail = n_nodes - head;
-        const int P = (int)(avail < S->pmax ? avail : S->pmax);
-        a.P = P;
-        a.head = head;
-        a.tile0 = head / TILE;
-        a.ntiles = (int)((head + P - 1) / TILE - a.tile0 + 1);
-        a.n_before = n_nodes;
-        a.need = max_nodes - n_nodes;
-        bfs_ctl_reset_kernel<<<dim3(1), dim3(64), 0, st>>>(a.ctl);
-        ChunkLaunch cl{S, st};
+    // chunk numbers run on across searches (S->kbase), so a slot never holds a stale match
+    auto enqueue = [&](int64_t k, int64_t avail_ub) -> int {
+        const int64_t pub = avail_ub < S->pmax ? avail_ub : S->pmax;
+        ChunkLaunch cl{S, st, S->kbase + k, (int)((pub - 1) / TILE + 2)};
         by_nw(L, cl);
         if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
-        if (hipMemcpyAsync(S->ctl_host, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess)
-            return ACX_E_LAUNCH;
-        if (stream_wait(st) != ACX_OK) return ACX_E_LAUNCH;
-        const Ctl c = *S->ctl_host;
-        ++chunks;
-        if (c.overflow) return ACX_E_LAUNCH;
-        const int64_t cut = c.cut_p == NONE ? INT64_MAX : (int64_t)c.cut_p;
-        const int64_t err_p = c.err == NONE ? INT64_MAX : (int64_t)(c.err / 12);
-        const int64_t suc_p = c.succ == NONE ? INT64_MAX : (int64_t)(c.succ / 12);
-        const bool err_first = c.err != NONE && c.err < c.succ && err_p <= cut;
-        const bool succ_first = !err_first && c.succ != NONE && suc_p <= cut;
-        const bool ends = err_first || succ_first || cut != INT64_MAX;
-        // children the reference looks at in this chunk, in order: up to and including the
-        // success child, up to (not including) the raising child, through the cut parent
-        const uint32_t end = err_first ? c.err : succ_first ? c.succ + 1
-                           : cut != INT64_MAX ? (uint32_t)((cut + 1) * 12) : (uint32_t)P * 12u;
-        if (c.min_len < (uint32_t)min_len) {  // a new minimum somewhere in the chunk: walk it
-            TraceLaunch tl{S, st, end, (uint32_t)min_len};
-            by_nw(L, tl);
-            if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
-            if (hipMemcpyAsync(S->ctl_host, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(S->trace_host, a.trace, sizeof(uint16_t) * TRACE_CAP, hipMemcpyDeviceToHost, st) !=
-                    hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess)
-                return ACX_E_LAUNCH;
-            const uint32_t nt = S->ctl_host->ntrace < (uint32_t)TRACE_CAP ? S->ctl_host->ntrace : TRACE_CAP;
-            for (uint32_t i = 0; i < nt; ++i) S->trace.push_back(S->trace_host[i]);
-            min_len = S->ctl_host->trace_min;
+        return hipEventRecord(S->ev[(S->kbase + k) % RING], st) == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+    };
+    auto wait_chunk = [&](int64_t k) -> int {  // poll (a sleeping wait can wake late)
+        hipError_t e;
+        const int64_t K = S->kbase + k;
+        while ((e = hipEventQuery(S->ev[K % RING])) == hipErrorNotReady) {
         }
-        if (ends) {
-            const int64_t last = err_first ? err_p : succ_first ? suc_p : cut;
-            parents += last + 1;
-            if (err_first) {
-                status = ACX_BFS_MOVE_ERROR;
-            } else if (succ_first) {
-                status = ACX_BFS_FOUND;
-                succ_node = head + suc_p;
-                succ_act = c.succ % 12;
-            } else {
-                status = ACX_BFS_BUDGET;
-                n_nodes = (int64_t)c.nodes_at_cut;
-            }
-            break;
-        }
-        parents += P;
-        n_nodes += (int64_t)c.total_new;
-        head += P;
+        if (e != hipSuccess) return ACX_E_LAUNCH;
+        return S->mirror[K % RING].seq == (uint64_t)(K + 1) ? ACX_OK : ACX_E_LAUNCH;
+    };
+    const int64_t qcap = S->qcap;
+    auto grow = [&](int64_t avail) -> int64_t {  // bound on the next chunk's available parents
+        const int64_t p = avail < S->pmax ? avail : S->pmax;
+        const int64_t ub = avail + 11 * p;
+        return ub < qcap ? ub : qcap;
+    };
+    int64_t next_ub = grow(1);  // chunk 1's bound (chunk 0 expands the root alone)
+    if (enqueue(0, 1) != ACX_OK || enqueue(1, next_ub) != ACX_OK) return ACX_E_LAUNCH;
+    Live lv{};
+    int64_t k = 0;
+    for (;; ++k) {
+        if (wait_chunk(k) != ACX_OK) return ACX_E_LAUNCH;
+        lv = S->mirror[(S->kbase + k) % RING].s;
+        if (lv.stop) break;
+        // exact state after chunk k = chunk k + 1's parameters: bound chunk k + 2
+        const int64_t avail = lv.n_nodes - lv.head;
+        if (enqueue(k + 2, grow(avail)) != ACX_OK) return ACX_E_LAUNCH;
     }
+    S->kbase += k + 2;  // chunk k + 1 is in the stream (it does nothing)
+    if (hipEventRecord(S->fin, st) != hipSuccess) return ACX_E_LAUNCH;
+    S->fin_pending = true;
+    if (lv.status < 0) return ACX_E_LAUNCH;  // table overflow (cannot happen at load <= 1/2)
+    const int status = lv.status;
+    const int64_t n_nodes = lv.n_nodes, parents = lv.parents, chunks = lv.chunks;
+    const int64_t min_len = lv.running;
+    const int64_t succ_node = lv.succ_node, succ_act = lv.succ_act;
+    int64_t path_len = 0;
+    // the close kernels wrote the trace straight into pinned host memory before publishing
+    const uint32_t nt = lv.ntrace < (uint32_t)TRACE_CAP ? lv.ntrace : TRACE_CAP;
+    for (uint32_t i = 0; i < nt; ++i) S->trace.push_back(S->trace_host[i]);
     if (status == ACX_BFS_FOUND) {
         PathLaunch pl{S, st, succ_node};
         by_nw(L, pl);

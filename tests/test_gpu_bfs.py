@@ -41,6 +41,26 @@ def test_device_bfs_random_reference_searches(chunk):
             assert LAST_STATS["status"] == 2 and LAST_STATS["nodes"] == c["budget_nodes"], c
 
 
+def test_device_bfs_workspace_reuse_across_epoch_wraps():
+    """One workspace, 150 searches in a row (the visited set is never cleared between searches:
+    entries carry a 6-bit search epoch and the table is cleared when it wraps, every 63
+    searches): alternating AK(2) and AK(3) searches of several budgets keep giving the same
+    results, node counts and discovered node sets as their first run, across two wraps."""
+    from acx.search import _device_bfs as D
+    D.release_workspaces()
+    ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+    ak3 = _ak3(7)
+    first = {}
+    for i in range(150):
+        pres, budget = [(ak2, 20_000), (ak3, 5_000), (ak2, 300), (ak3, 60_000)][i % 4]
+        res = D.device_bfs(pres, budget, device=DEV, keep_node_keys=True)
+        got = (res[0], None if res[1] is None else [list(x) for x in res[1]], D.LAST_STATS["nodes"],
+               D.LAST_STATS["parents"], np.asarray(D.LAST_STATS["node_keys"]).tobytes())
+        first.setdefault(i % 4, got)
+        assert got == first[i % 4], i
+    D.release_workspaces()
+
+
 @pytest.mark.parametrize("chunk", [0, 5])
 def test_device_bfs_kat_ak2_and_budgets(chunk):
     from acx.search._device_bfs import device_bfs
