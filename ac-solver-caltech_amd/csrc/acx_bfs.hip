@@ -725,7 +725,6 @@ struct Search {
     uint64_t tsize = 0;
     Args a{};
     LiveMirror* mirror = nullptr;  // pinned host memory, RING slots (bfs_close_kernel publishes)
-    hipEvent_t ev[RING] = {};      // recorded after each chunk's close kernel
     hipEvent_t fin = nullptr;      // after a search's last (speculative) chunk: the next search
                                    // and the destructor wait for it (any stream)
     bool fin_pending = false;
@@ -744,8 +743,6 @@ struct Search {
             if (p) (void)hipFree(p);
         if (mirror) (void)hipHostFree(mirror);
         if (trace_host) (void)hipHostFree(trace_host);
-        for (auto& e : ev)
-            if (e) (void)hipEventDestroy(e);
         if (fin) (void)hipEventDestroy(fin);
     }
 };
@@ -839,11 +836,10 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
               dalloc(a.tmin, (size_t)S->tiles_max) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.trace, (size_t)TRACE_CAP) && dalloc(S->path_dev, (size_t)(2 * PATH_CAP)) &&
               dalloc(S->path_n_dev, 1) && dalloc(a.live, 1) &&
-              hipHostMalloc((void**)&S->mirror, sizeof(LiveMirror) * RING, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void**)&S->trace_host, sizeof(uint16_t) * TRACE_CAP, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&S->mirror, sizeof(LiveMirror) * RING, hipHostMallocCoherent) == hipSuccess &&
+              hipHostMalloc((void**)&S->trace_host, sizeof(uint16_t) * TRACE_CAP, hipHostMallocCoherent) == hipSuccess &&
               hipMemset(a.lost, 0, (size_t)(S->tiles_max * TILE_CH)) == hipSuccess &&
               hipMemset(a.table, 0, (size_t)ts * 8) == hipSuccess;
-    for (auto& e : S->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&S->fin, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
@@ -906,16 +902,23 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
         const int64_t pub = avail_ub < S->pmax ? avail_ub : S->pmax;
         ChunkLaunch cl{S, st, S->kbase + k, (int)((pub - 1) / TILE + 2)};
         by_nw(L, cl);
-        if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
-        return hipEventRecord(S->ev[(S->kbase + k) % RING], st) == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+        return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
     };
-    auto wait_chunk = [&](int64_t k) -> int {  // poll (a sleeping wait can wake late)
-        hipError_t e;
+    // poll the slot's sequence number (written last, system scope, by the chunk's close kernel);
+    // no per-chunk event (an event marker held the next chunk back ~5 us).  Every 4096 polls
+    // the stream is queried so that a failed launch cannot leave the host spinning.
+    auto wait_chunk = [&](int64_t k) -> int {
         const int64_t K = S->kbase + k;
-        while ((e = hipEventQuery(S->ev[K % RING])) == hipErrorNotReady) {
+        const uint64_t* seq = &S->mirror[K % RING].seq;
+        for (uint64_t it = 1;; ++it) {
+            if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) == (uint64_t)(K + 1)) return ACX_OK;
+            if ((it & 4095) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipSuccess)  // idle: the slot is final now
+                    return __atomic_load_n(seq, __ATOMIC_ACQUIRE) == (uint64_t)(K + 1) ? ACX_OK : ACX_E_LAUNCH;
+                if (e != hipErrorNotReady) return ACX_E_LAUNCH;
+            }
         }
-        if (e != hipSuccess) return ACX_E_LAUNCH;
-        return S->mirror[K % RING].seq == (uint64_t)(K + 1) ? ACX_OK : ACX_E_LAUNCH;
     };
     const int64_t qcap = S->qcap;
     auto grow = [&](int64_t avail) -> int64_t {  // bound on the next chunk's available parents
