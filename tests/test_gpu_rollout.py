@@ -223,3 +223,39 @@ def test_int8_obs_trajectory_equals_int32(L, B, T, pack):
     assert np.array_equal(a[2], b[2].astype(np.int32))
     for i in (0, 1, 3, 4, 5, 6, 7):
         assert np.array_equal(a[i], b[i]), i
+
+
+@pytest.mark.parametrize("L,obs_dtype", [(36, torch.int32), (36, torch.int8), (128, torch.int32)])
+def test_rollout_plan_equals_rollout_over_consecutive_launches(L, obs_dtype):
+    """ops.RolloutPlan (checks/pointers resolved once, reused buffers) launched three times in a
+    row gives the same states, counts, trajectories and errors as ops.rollout per chunk."""
+    from acx import ops
+    B, T, H = 777, 11, 6
+    rng = np.random.default_rng(L)
+    starts = torch.as_tensor(_starts(L, B, seed=3)).to(DEV)
+    acts = torch.as_tensor(rng.integers(0, 12, size=(3 * T, B)).astype(np.int32)).to(DEV)
+
+    def bufs():
+        return dict(obs_traj=torch.full((T, B, 2 * L), -7, dtype=obs_dtype, device=DEV),
+                    reward_traj=torch.zeros((T, B), dtype=torch.int32, device=DEV),
+                    done_traj=torch.zeros((T, B), dtype=torch.uint8, device=DEV),
+                    trunc_traj=torch.zeros((T, B), dtype=torch.uint8, device=DEV),
+                    err=torch.zeros(B, dtype=torch.uint8, device=DEV), err_count=torch.zeros(1, dtype=torch.int32,
+                                                                                             device=DEV))
+    st_a, cnt_a, ba = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV), bufs()
+    st_b, cnt_b, bb = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV), bufs()
+    plan = ops.RolloutPlan(st_b, starts, cnt_b, T=T, horizon=H, cyclical=True, **bb)
+    for k in range(3):
+        a = acts[k * T:(k + 1) * T]
+        ops.rollout(st_a, a, starts, cnt_a, horizon=H, cyclical=True, **ba)
+        plan(a)
+        torch.cuda.synchronize()
+        assert torch.equal(st_a, st_b) and torch.equal(cnt_a, cnt_b), k
+        for n in ba:
+            assert torch.equal(ba[n], bb[n]), (k, n)
+    with pytest.raises(ValueError):
+        plan(acts[: T + 1])
+    with pytest.raises(ValueError):
+        plan(acts[:T].to(torch.int64))
+    with pytest.raises(ValueError):
+        plan(acts[:T].t().contiguous().t())
