@@ -115,6 +115,19 @@ def _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, don
     return L, B, dev, obs8
 
 
+def packs_actions(T: int, obs_traj: Optional[torch.Tensor]) -> bool:
+    """The move-id path ops.rollout / RolloutPlan take by default.  The rollout loads the ids of
+    32 steps at a time when it writes an obs trajectory, so for T <= 32 every id load is issued
+    before the first trajectory store and the int32 ids cost no store drain; the separate pack
+    pass (a ~20-37 us launch at 2^20 envs) then costs more than the extra id bytes.  Measured
+    in one process on the same buffers (tools/ab_pack.py, profiles/r03/r03v_ab_pack.json, 2^20
+    envs, L = 36): int32 obs K = 20 1.350 vs 1.368 ms, K = 200 9.79 vs 9.63 ms (packed wins);
+    int8 obs K = 20 0.475 vs 0.480, K = 200 3.750 vs 3.803 (int32 ids win)."""
+    if obs_traj is None:
+        return True
+    return obs_traj.dtype != torch.int8 and T > 32
+
+
 def rollout(
     state: torch.Tensor,
     actions: torch.Tensor,
@@ -129,15 +142,16 @@ def rollout(
     trunc_traj: Optional[torch.Tensor] = None,
     err: Optional[torch.Tensor] = None,
     err_count: Optional[torch.Tensor] = None,
-    pack_actions: bool = True,
+    pack_actions: Optional[bool] = None,
     packed_workspace: Optional[torch.Tensor] = None,
 ) -> None:
     """acx_rollout: T = actions.shape[0] fused env steps; state/step_count updated in place.
 
-    pack_actions (default): acx_pack_actions + acx_rollout_packed -- one streaming pass packs
-    the (T, B) int32 move ids 8 per word (0.5 B per env-step) into `packed_workspace`
-    ((ceil(T/8), B) int32, allocated if not given), then the rollout reads those; identical
-    results to acx_rollout (pack_actions=False).
+    pack_actions=True: acx_pack_actions + acx_rollout_packed -- one streaming pass packs the
+    (T, B) int32 move ids 8 per word (0.5 B per env-step) into `packed_workspace`
+    ((ceil(T/8), B) int32, allocated if not given), then the rollout reads those.
+    pack_actions=False: the rollout reads the int32 ids itself (acx_rollout / acx_rollout_obs8).
+    Identical results either way; None (default) picks by `packs_actions` (T, obs dtype).
 
     obs_traj may be int32 or int8 (T, B, 2L): int8 is the reference's observation dtype
     (ac_env.py:64-70) and goes to acx_rollout_obs8 (a quarter of the trajectory bytes)."""
@@ -146,6 +160,8 @@ def rollout(
     L, B, dev, obs8 = _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, done_traj, trunc_traj,
                                      err, err_count)
     _check(actions, "actions", _INT32, (T, B), dev)
+    if pack_actions is None:
+        pack_actions = packs_actions(T, obs_traj)
     if pack_actions and T > 0 and B > 0:
         words = (T + 7) // 8
         if packed_workspace is None:
@@ -187,12 +203,14 @@ def rollout(
 
 
 class RolloutPlan:
-    """ops.rollout (pack_actions=True) over buffers fixed once: the argument checks, the pointer
-    lookups and the packed-move workspace are done here, so each call only checks the (T, B)
-    actions tensor and issues the two launches (acx_pack_actions + acx_rollout_packed /
-    acx_rollout_obs8) on the current stream.  This is what a PPO loop that reuses its rollout
-    storage every update calls; results are identical to ops.rollout with the same arguments.
-    The plan keeps references to its tensors; their storage must not be resized or replaced."""
+    """ops.rollout over buffers fixed once: the argument checks, the pointer lookups, the
+    move-id path (`packs_actions`, or `pack_actions`) and the packed-move workspace are settled
+    here, so each call only checks the (T, B) actions tensor and issues the launches
+    (acx_pack_actions + acx_rollout_packed / acx_rollout_obs8, or acx_rollout /
+    acx_rollout_obs8 on the int32 ids) on the current stream.  This is what a PPO loop that
+    reuses its rollout storage every update calls; results are identical to ops.rollout with the
+    same arguments.  The plan keeps references to its tensors; their storage must not be
+    resized or replaced."""
 
     def __init__(
         self,
@@ -209,6 +227,7 @@ class RolloutPlan:
         trunc_traj: Optional[torch.Tensor] = None,
         err: Optional[torch.Tensor] = None,
         err_count: Optional[torch.Tensor] = None,
+        pack_actions: Optional[bool] = None,
     ):
         lib = _lib.load()
         T = int(T)
@@ -217,19 +236,26 @@ class RolloutPlan:
         L, B, dev, obs8 = _check_rollout(state, reset_state, step_count, T, obs_traj, reward_traj, done_traj,
                                          trunc_traj, err, err_count)
         self.T, self.B, self.L, self.device = T, B, L, dev
+        self.packs = packs_actions(T, obs_traj) if pack_actions is None else bool(pack_actions)
         self._ashape = torch.Size((T, B))
         self._keep = (state, reset_state, step_count, obs_traj, reward_traj, done_traj, trunc_traj, err, err_count)
-        self._ws = torch.empty(((T + 7) // 8, B), dtype=_INT32, device=dev)
-        self._wsp = self._ws.data_ptr()
-        self._pack = lib.acx_pack_actions
         tail = (_ptr(reset_state), _ptr(step_count), _ptr(obs_traj), _ptr(reward_traj), _ptr(done_traj),
                 _ptr(trunc_traj), _ptr(err), _ptr(err_count), T, B, L, int(horizon), int(bool(cyclical)))
-        if obs8:
-            self._fn, self._name = lib.acx_rollout_obs8, "acx_rollout_obs8"
-            self._args = (_ptr(state), None, self._wsp) + tail
+        self._head = (_ptr(state),)
+        if self.packs:
+            self._ws = torch.empty(((T + 7) // 8, B), dtype=_INT32, device=dev)
+            self._wsp = self._ws.data_ptr()
+            self._pack = lib.acx_pack_actions
+            if obs8:
+                self._fn, self._name = lib.acx_rollout_obs8, "acx_rollout_obs8"
+                self._args = (_ptr(state), None, self._wsp) + tail
+            else:
+                self._fn, self._name = lib.acx_rollout_packed, "acx_rollout_packed"
+                self._args = (_ptr(state), self._wsp) + tail
+        elif obs8:  # the action pointer goes in per call: (state, actions, packed=None, ...)
+            self._fn, self._name, self._tail = lib.acx_rollout_obs8, "acx_rollout_obs8", (None,) + tail
         else:
-            self._fn, self._name = lib.acx_rollout_packed, "acx_rollout_packed"
-            self._args = (_ptr(state), self._wsp) + tail
+            self._fn, self._name, self._tail = lib.acx_rollout, "acx_rollout", tail
 
     def __call__(self, actions: torch.Tensor) -> None:
         """T fused env steps with `actions` ((T, B) int32, contiguous, on the plan's device)."""
@@ -240,8 +266,11 @@ class RolloutPlan:
         if self.T == 0 or self.B == 0:
             return
         s = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(self._pack(actions.data_ptr(), self._wsp, self.T, self.B, s), "acx_pack_actions")
-        _lib.check(self._fn(*self._args, s), self._name)
+        if self.packs:
+            _lib.check(self._pack(actions.data_ptr(), self._wsp, self.T, self.B, s), "acx_pack_actions")
+            _lib.check(self._fn(*self._args, s), self._name)
+        else:
+            _lib.check(self._fn(*self._head, actions.data_ptr(), *self._tail, s), self._name)
 
 
 def expand12(

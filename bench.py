@@ -548,7 +548,7 @@ def main():
     # and per-launch terms at any K, so the ratio is K-independent) and labelled as scaled.
     traffic, traffic_src = None, None
     cands = []
-    for tag in ("r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h", "r02_k20", "r02", "r01"):
+    for tag in ("r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h", "r02_k20", "r02", "r01"):
         prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
@@ -602,7 +602,8 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": f"acx::pack_actions_kernel + acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,1>",
+            "kernel": ("acx::pack_actions_kernel + " if plan(min(K, T_buf)).packs else "")
+            + f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,1>",
             "bytes_per_env_step": step_bytes,
             "launch_bytes": launch_bytes,
             "resets_in_launch": resets,

@@ -43,6 +43,19 @@ def test_no_cpu_fallback():
         acx.ops.expand12(s)
 
 
+def test_rollout_move_id_path_choice():
+    """ops.packs_actions: the packed ids for int32 trajectories longer than one 32-step id batch
+    (and rollouts with no trajectory), the int32 ids otherwise (DESIGN.md "Rollout")."""
+    from acx import ops
+    o32, o8 = torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int8)
+    assert ops.packs_actions(20, None) and ops.packs_actions(200, None)
+    assert not ops.packs_actions(20, o32) and not ops.packs_actions(32, o32) and ops.packs_actions(33, o32)
+    assert not ops.packs_actions(20, o8) and not ops.packs_actions(200, o8)
+    with pytest.raises(_lib.ACXError):  # still no CPU path
+        ops.RolloutPlan(torch.zeros((4, 72), dtype=torch.int32), torch.zeros((4, 72), dtype=torch.int32),
+                        torch.zeros(4, dtype=torch.int32), T=3, horizon=5)
+
+
 def test_host_utils_match_reference_cases():
     with open(os.path.join(GOLDEN, "unit_cases.json")) as f:
         unit = json.load(f)

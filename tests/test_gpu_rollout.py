@@ -225,8 +225,9 @@ def test_int8_obs_trajectory_equals_int32(L, B, T, pack):
         assert np.array_equal(a[i], b[i]), i
 
 
+@pytest.mark.parametrize("pack", [None, True, False])
 @pytest.mark.parametrize("L,obs_dtype", [(36, torch.int32), (36, torch.int8), (128, torch.int32)])
-def test_rollout_plan_equals_rollout_over_consecutive_launches(L, obs_dtype):
+def test_rollout_plan_equals_rollout_over_consecutive_launches(L, obs_dtype, pack):
     """ops.RolloutPlan (checks/pointers resolved once, reused buffers) launched three times in a
     row gives the same states, counts, trajectories and errors as ops.rollout per chunk."""
     from acx import ops
@@ -244,10 +245,11 @@ def test_rollout_plan_equals_rollout_over_consecutive_launches(L, obs_dtype):
                                                                                              device=DEV))
     st_a, cnt_a, ba = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV), bufs()
     st_b, cnt_b, bb = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV), bufs()
-    plan = ops.RolloutPlan(st_b, starts, cnt_b, T=T, horizon=H, cyclical=True, **bb)
+    plan = ops.RolloutPlan(st_b, starts, cnt_b, T=T, horizon=H, cyclical=True, pack_actions=pack, **bb)
+    assert plan.packs == (ops.packs_actions(T, bb["obs_traj"]) if pack is None else pack)
     for k in range(3):
         a = acts[k * T:(k + 1) * T]
-        ops.rollout(st_a, a, starts, cnt_a, horizon=H, cyclical=True, **ba)
+        ops.rollout(st_a, a, starts, cnt_a, horizon=H, cyclical=True, pack_actions=not plan.packs, **ba)
         plan(a)
         torch.cuda.synchronize()
         assert torch.equal(st_a, st_b) and torch.equal(cnt_a, cnt_b), k

@@ -25,12 +25,14 @@ def rows(path):
 
 trace = sorted(rows(os.path.join(d, "trace", "bench_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
 disp = {}
+starts = {}
 for r in trace:
     name = r["Kernel_Name"]
     if "acx::" not in name:
         continue
     dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     disp.setdefault(name, []).append(dur)
+    starts.setdefault(name, []).append(int(r["Start_Timestamp"]))
 pmc = {}
 for kind in ("fetch", "write"):
     p = os.path.join(d, f"pmc_{kind}", "bench_counter_collection.csv")
@@ -60,13 +62,15 @@ if bench:
     rl = bench["roofline"]
     # the timed launch = the last (in time) of the longest rollout_kernel dispatches (the warmup
     # launch comes first) plus, when ops.rollout packed the move ids first, the matching
-    # pack_actions_kernel dispatch
+    # pack_actions_kernel dispatch (the last pack dispatch that started after the previous
+    # rollout dispatch and before this one: short launches read the int32 ids directly,
+    # ops.packs_actions, so the pack and rollout dispatch counts differ)
     # the int32-trajectory instantiation: rollout_kernel<NW, LC, VEC, 1, PK> (round 2's int8 mode is
     # OBS = 2; before it the parameter was `true`, and before the PK parameter it ended there)
     import re
-    timed = [v for n, v in summary["kernels"].items()
+    timed = [(n, v) for n, v in summary["kernels"].items()
              if re.search(r"rollout_kernel<\d+, \d+, \d+, (1|true)(, (true|false))?>", n)]
-    packs = [v for n, v in summary["kernels"].items() if "pack_actions_kernel" in n]
+    packs = [n for n in summary["kernels"] if "pack_actions_kernel" in n]
 
     def hbm(k, i):
         if "write_bytes" not in k:
@@ -80,7 +84,7 @@ if bench:
     n_warm = -(-bl["warmup"] // T_buf) if bl["warmup"] > 0 else 0
     n_timed = rl.get("launches", 1)
     if timed:
-        k = max(timed, key=lambda v: v["dispatches"])
+        kname, k = max(timed, key=lambda nv: nv[1]["dispatches"])
         idx = list(range(n_warm, n_warm + n_timed))
         ms = sum(k["durations_ms"][i] for i in idx)
         parts = [hbm(k, i) for i in idx]
@@ -88,13 +92,24 @@ if bench:
         rec = {"timed_dispatch_index": idx, "rollout_kernel_ms": ms, "rollout_kernel_hbm_bytes": traffic,
                "rollout_kernel_fetch_bytes": sum(k.get("fetch_bytes_corrected", [0] * (idx[-1] + 1))[i] for i in idx),
                "rollout_kernel_write_bytes": sum(k.get("write_bytes", [0] * (idx[-1] + 1))[i] for i in idx)}
+        pidx = []
         if packs:
-            pk = packs[0]
-            ms += sum(pk["durations_ms"][i] for i in idx)
-            pparts = [hbm(pk, i) for i in idx]
+            pname = packs[0]
+            ps_ = starts[pname]
+            rs_ = starts[kname]
+            for i in idx:
+                lo = rs_[i - 1] if i > 0 else -1
+                cand = [j for j, t in enumerate(ps_) if lo < t < rs_[i]]
+                if cand:
+                    pidx.append(cand[-1])
+        if pidx:
+            pk = summary["kernels"][pname]
+            pms = sum(pk["durations_ms"][j] for j in pidx)
+            ms += pms
+            pparts = [hbm(pk, j) for j in pidx]
             pt = None if None in pparts else sum(pparts)
             traffic = None if traffic is None or pt is None else traffic + pt
-            rec.update({"pack_actions_kernel_ms": sum(pk["durations_ms"][i] for i in idx), "pack_actions_hbm_bytes": pt})
+            rec.update({"pack_dispatch_index": pidx, "pack_actions_kernel_ms": pms, "pack_actions_hbm_bytes": pt})
         rec.update({
             "rocprof_ms": ms, "bench_event_ms": rl["kernel_ms"],
             "agree_pct": 100 * abs(ms - rl["kernel_ms"]) / rl["kernel_ms"],
