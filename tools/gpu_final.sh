@@ -7,6 +7,8 @@ TAG=${1:-final}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
+# the box: HBM vendor, VBIOS, partition modes, clock levels (read only; the fast/slow rollout split is per box)
+rocm-smi --showmemvendor --showvbios --showmemorypartition --showcomputepartition --showclkfrq --showperflevel > $OUT/${TAG}_box.txt 2>&1 || true
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/${TAG}_gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/${TAG}_gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke-ok')" > $OUT/${TAG}_smoke.log 2>&1 || exit 2

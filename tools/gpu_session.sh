@@ -8,6 +8,8 @@ TAG=${1:-r02}  # usage: bash tools/gpu_session.sh TAG  (PROFILE=0: skip the rocp
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
+# the box: HBM vendor, VBIOS, partition modes, clock levels (read only; the fast/slow rollout split is per box)
+rocm-smi --showmemvendor --showvbios --showmemorypartition --showcomputepartition --showclkfrq --showperflevel > $OUT/${TAG}_box.txt 2>&1 || true
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/${TAG}_gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -3 $OUT/${TAG}_gpu_tests.log
