@@ -61,6 +61,12 @@
 
 #include "acx_bfs_common.h"
 
+// visited-set sizing: the table has >= 100/ACX_BFS_TABLE_LOAD_PCT entries per bound entry (every
+// node plus every claimed chunk entry), power of two; see acx_bfs_create
+#ifndef ACX_BFS_TABLE_LOAD_PCT
+#define ACX_BFS_TABLE_LOAD_PCT 50
+#endif
+
 namespace acx {
 namespace bfs {
 
@@ -818,8 +824,9 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     // every parent that can be expanded (< qcap) has its 12 child slots; one spare tile
     S->scap = 1 + ((S->qcap + TILE - 1) / TILE + 1) * TILE_CH;
     // every node and every claimed chunk entry at load <= 1/2, buckets of 8 (one 64-B line per
-    // probe).  (Half that -- load <= 1, 134 MB at 10^7 nodes, inside the 256 MB MALL -- measured
-    // 1.83 vs 1.93 ms at 10^7 but 18.4 vs 17.0 ms at 10^8 nodes: not taken.)
+    // probe).  Other sizes, A/B on the final pipeline (profiles/r03/r03x_bfs_table_load.json):
+    // half the entries 1.52 vs 1.47 ms at 10^7 and (load <= 1) 16.0 vs 13.7 ms at 10^8; twice
+    // the entries within 1 % at 10^7 and 14.5 vs 13.4 ms at 10^8.
     // Key-in-table (L <= KT_MAX_L, opt-in): 4 words per entry, entries >= 1.25x the same bound
     // (2 per bucket; the bound counts a whole last chunk's children as new: the real load stays
     // lower).  Measured slower than the 8-entry table (r03i: 2.11 vs 1.68 ms at 10^7 nodes, 20.0
@@ -827,7 +834,7 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
     const bool kt = L <= KT_MAX_L && g_bfs_layout == 2;
     uint64_t ts = 1024;
     const uint64_t bound = (uint64_t)(S->qcap + 12 * S->pmax);
-    while (kt ? ts < 5 * bound : ts < 2 * bound) ts <<= 1;
+    while (kt ? ts < 5 * bound : ts * ACX_BFS_TABLE_LOAD_PCT < 100 * bound) ts <<= 1;
     S->tsize = ts;
     Args& a = S->a;
     bool ok = dalloc(a.store, (size_t)(S->scap * S->kw)) && dalloc(a.queue, (size_t)S->qcap) &&
