@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--K", default="20", help="steps per launch; a comma list runs each K on the same buffers")
     ap.add_argument("--obs", default="both")
+    ap.add_argument("--no-check", action="store_true",
+                    help="timing-only variants that skip work on purpose (outputs not compared)")
     a = ap.parse_args()
     # each entry "T" or "T@S": a T-step launch writing trajectory rows [S, S + T) of the buffer
     Ks = [(int(x.split("@")[0]), int(x.split("@")[1]) if "@" in x else 0) for x in a.K.split(",")]
@@ -88,7 +90,7 @@ def main():
                   o = o32 if k == "i32" else o8
                   sig = (int(o[off:off + T].sum(dtype=torch.int64)), int(rew[:T].sum(dtype=torch.int64)), int(state.sum(dtype=torch.int64)))
                   ref.setdefault((k, T), sig)
-                  assert ref[(k, T)] == sig, (n, k, T, sig, ref[(k, T)])
+                  assert a.no_check or ref[(k, T)] == sig, (n, k, T, sig, ref[(k, T)])
     # the same trajectory rows written by torch's fill_ (a one-pass linear write): their store rate
     out = {}
     for T, off in Ks:
