@@ -9,8 +9,9 @@ TAG=${1:-r03}
 OUT=$R/gpurun_out/prof_place_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-run() {  # name counters...
+run() {  # name counters...   (ONLY="name ...": just those passes)
   local n=$1; shift
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $n "* ]]; then return 0; fi
   timeout -s KILL 90 rocprofv3 -E $R/tools/pmc_instances.yaml --pmc "$@" -d $OUT/$n -o r --output-format csv -- python3 $R/tools/placement_pmc.py > $OUT/$n.log 2>&1
 }
 run inst ACX_WRREQ_I0 ACX_WRREQ_I1 ACX_WRREQ_I2 ACX_WRREQ_I3 ACX_WRREQ_I4 ACX_WRREQ_I5 ACX_WRREQ_I6 ACX_WRREQ_I7 ACX_WRREQ_I8 ACX_WRREQ_I9 ACX_WRREQ_I10 ACX_WRREQ_I11 ACX_WRREQ_I12 ACX_WRREQ_I13 ACX_WRREQ_I14 ACX_WRREQ_I15 || exit 1
