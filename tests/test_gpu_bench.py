@@ -1,0 +1,47 @@
+"""GPU: bench.py end to end at a small batch, in a child process (as the driver runs it): one
+JSON line with the contract's fields, the rollout split into launches of <= 200 steps through
+ops.RolloutPlan (K = 210: a packed 200-step launch and a direct-id 10-step one), no env
+errors, and the roofline / variant blocks present."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=240):
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, capture_output=True,
+                       text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_line_multi_launch_small_batch():
+    d = _bench("--batch", "8192", "--steps", "210", "--warmup", "3", "--no-cpu", "--no-bfs", "--no-learner",
+               "--no-graph")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 210 and d["warmup"] == 3
+    assert d["value"] > 0 and d["env_errors"] == 0
+    r = d["roofline"]
+    assert r["launches"] == 2 and r["kernel"].startswith("acx::pack_actions_kernel")
+    assert 0 < r["frac"] < 1.5 and r["bytes_per_env_step"] == 298
+    assert d["config"]["envs_per_gpu"] == 8192
+    for v in ("rollout_obs_int8", "rollout_desync", "step_api"):
+        assert v in d["variants"] and d["variants"][v].get("env_errors", 0) == 0, v
+
+
+def test_bench_line_short_launch_reads_int32_ids():
+    d = _bench("--batch", "4096", "--steps", "20", "--warmup", "5", "--no-cpu", "--no-bfs", "--no-learner",
+               "--no-graph", "--no-step-api", "--no-desync", "--no-obs8")
+    r = d["roofline"]
+    assert r["launches"] == 1 and r["kernel"].startswith("acx::rollout_kernel")
+    assert d["env_errors"] == 0 and d["value"] > 0
