@@ -155,6 +155,9 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
                          {"keys": torch.empty((per, 12, kw), dtype=torch.int64, device=d)}))
         status = 0
         t_gpu = 0.0
+        # HIP events around each batch's kernels (unpack + expand12) on every GPU's stream: the
+        # kernel-only share of gpu_roundtrip_s (which adds the H2D / D2H copies and the waits)
+        kev = []
         while status == 0:
             n = lib.acx_search_next_batch(h, parent_keys.ctypes.data, batch)
             if n == 0:
@@ -170,9 +173,13 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
                 dev_keys, dev_states, out = bufs[g]
                 with torch.cuda.device(d):
                     dev_keys[: b - a].copy_(pinned_in[a:b], non_blocking=True)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
                     ops.unpack_keys(dev_keys[: b - a], L, out=dev_states[: b - a])
                     res = ops.expand12(dev_states[: b - a], cyclical=cyclical, children=False, lengths=False,
                                        keys=True, err=False, out=out)
+                    e1.record()
+                    kev.append((e0, e1))
                     pinned_out[a:b].copy_(res["keys"][: b - a], non_blocking=True)
             for d in devs:
                 torch.cuda.synchronize(d)
@@ -182,7 +189,8 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
         lib.acx_search_stats(h, st.ctypes.data)
         LAST_STATS.clear()
         LAST_STATS.update(rounds=int(st[0]), expanded=int(st[1]), pops=int(st[2]), host_next_s=st[3] / 1e9,
-                          host_store_s=st[4] / 1e9, host_replay_s=st[5] / 1e9, gpu_roundtrip_s=t_gpu)
+                          host_store_s=st[4] / 1e9, host_replay_s=st[5] / 1e9, gpu_roundtrip_s=t_gpu,
+                          kernel_s=sum(e0.elapsed_time(e1) for e0, e1 in kev) / 1e3)
         budget = ctypes.c_int32(0)
         min_len = ctypes.c_int32(0)
         n_nodes = ctypes.c_int64(0)

@@ -71,6 +71,14 @@ __device__ __forceinline__ int4 widen4(uint32_t p) {
 
 
 constexpr int STAGE_UNROLL = 8;
+// the step kernel's CodeTile (L = 128) full-tile loads software-pipelined across batches (A/B knob)
+#ifndef ACX_PIPE_LOAD
+#define ACX_PIPE_LOAD 1
+#endif
+// the step kernel's per-env scalar inputs (move id, step count) loaded before its tile (A/B knob)
+#ifndef ACX_EARLY_SCALARS
+#define ACX_EARLY_SCALARS 1
+#endif
 // Non-temporal (streaming) stores for the rollout's write-once trajectory outputs: the
 // obs trajectory with them is 1.4 % faster (B = 2^20, L = 36, T = 200: 10.08 vs 10.22 ms,
 // tools/ab_libs.py); for reward/done/truncated they cost 0.4 %, so those stay plain.
@@ -206,7 +214,9 @@ struct FastTile {
         }
     }
 
-    // global rows (contiguous, 2L int32 each) -> LDS
+    // global rows (contiguous, 2L int32 each) -> LDS (PIPE: see CodeTile::load; this full-tile
+    // loop is unrolled already)
+    template <bool PIPE = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));  // keep the address math here (no hoisting into the caller)
@@ -737,6 +747,9 @@ struct CodeTile {
         return slots(r)[c - r * CPR];
     }
 
+    // PIPE (the step kernel; the rollout keeps the plain loop, whose register budget the
+    // in-flight batch pair would exceed): full tiles software-pipelined, see below
+    template <bool PIPE = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -745,6 +758,42 @@ struct CodeTile {
         const int nc = R * CPR;
         const int4* src = reinterpret_cast<const int4*>(g) + ln;
         bool any_bad = false;
+        if (PIPE && R == WAVE) {
+            // full tile (wave-uniform): software-pipelined, batch b + 1's loads are issued before
+            // batch b is converted, so LOAD_BATCH..2*LOAD_BATCH loads stay in flight through the
+            // whole 64 KB tile (L = 128) instead of draining to zero between batches
+            int4 va[LOAD_BATCH], vb[LOAD_BATCH];
+            auto issue = [&](int4* v, int u0) {
+#pragma unroll
+                for (int u = 0; u < LOAD_BATCH; ++u) v[u] = src[(u0 + u) * WAVE];
+            };
+            auto convert = [&](const int4* v, int u0) {
+#pragma unroll
+                for (int u = 0; u < LOAD_BATCH; ++u) {
+                    const int c = ln + (u0 + u) * WAVE;
+                    bool bad = false;
+                    const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
+                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                    uint32_t c8, nz4;
+                    swar_pack4(d, c8, nz4);
+                    put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+                    if (bad) flags[c / CPR] = 1;
+                    any_bad |= bad;
+                }
+            };
+            static_assert(CPR % (2 * LOAD_BATCH) == 0, "pipelined tile load: whole batch pairs");
+            issue(va, 0);
+#pragma unroll
+            for (int u0 = 0; u0 < CPR; u0 += 2 * LOAD_BATCH) {
+                issue(vb, u0 + LOAD_BATCH);
+                convert(va, u0);
+                if (u0 + 2 * LOAD_BATCH < CPR) issue(va, u0 + 2 * LOAD_BATCH);
+                convert(vb, u0 + LOAD_BATCH);
+            }
+            tile_bad = __any(any_bad);
+            wave_sync();
+            return;
+        }
         for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
             int4 v[LOAD_BATCH];
 #pragma unroll
@@ -1209,6 +1258,7 @@ struct GenericTile {
         }
     };
 
+    template <bool PIPE = false>  // see CodeTile::load (not used by the runtime-L path)
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         flags[lane] = 0;
         wave_sync();
@@ -1504,7 +1554,20 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
 
-    tile.load(a.state_in + w.r0 * twoL, w.R, w.lane);
+    // the env's move id and step count: issued ahead of the tile so their latency hides under it
+    int act_in = 0, cnt_in = 0;
+#if ACX_EARLY_SCALARS
+    if (w.active) {
+        if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
+            const int64_t v = a.action64[env];
+            act_in = (v >= 0 && v < 12) ? (int)v : -1;
+        } else {
+            act_in = a.action[env];
+        }
+        cnt_in = a.step_count ? a.step_count[env] : 0;
+    }
+#endif
+    tile.template load<ACX_PIPE_LOAD != 0>(a.state_in + w.r0 * twoL, w.R, w.lane);
 
     bool fin = false;    // done | truncated (the curriculum's "finished")
     bool reset = false;  // same-step autoreset of this env
@@ -1514,14 +1577,17 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     int cnt0 = 0, cnt = 0, e = ACX_ERR_NONE;
     uint32_t dm = 0;     // relators of the row that differ from state_in (in-place store)
     if (w.active) {
-        int act;
+        int act = act_in;
+#if !ACX_EARLY_SCALARS
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
             const int64_t v = a.action64[env];
             act = (v >= 0 && v < 12) ? (int)v : -1;
         } else {
             act = a.action[env];
         }
-        cnt0 = a.step_count ? a.step_count[env] : 0;
+        cnt_in = a.step_count ? a.step_count[env] : 0;
+#endif
+        cnt0 = cnt_in;
         cnt = a.step_count ? cnt0 + 1 : 0;
         // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
         // at [k][i] -- envs at the same episode position write one coalesced row segment (an

@@ -10,16 +10,30 @@ default K = 200; a larger K reuses the same buffers, as a PPO loop does) that wr
 (K, B, 2L) int32 observation trajectory plus reward/done/truncated per step.  Inputs are
 resident in HBM before the timed region.
 
-Also measured (reported under "variants"): the per-call acx_step API (one launch per step,
-state read+written in HBM each step) on the same batch.
+`--workload step` makes the per-call acx_step API (one launch per env step, random actions,
+in-place state, autoreset) the headline instead: BASELINE configs[4] ("random-action stepping",
+L = 128, 2^20 envs per GPU over 8 GPUs) is
 
-Multi-GPU: one process per GPU (torchrun), envs sharded by index (weak scaling: 2^20
-envs per rank); no collective on the data path, a barrier + max-over-ranks of the timed
-region only.
+    python bench.py --gpus 8 --workload step --L 128 --batch 1048576
+
+Also measured (reported under "variants"): the rollout with an int8 trajectory and with scattered
+resets, the per-call step API (+ hipGraph), the PPO learner step, config 4's searches (device BFS,
+expansion kernel, host-dedup BFS, owner-partitioned BFS).
+
+Multi-GPU: one process per GPU, envs sharded by index (weak scaling: B envs per rank); no
+collective on the data path, a barrier + max-over-ranks of every timed region only.  Either
+torchrun starts the ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the environment), or
+`--gpus N > 1` without them makes this process a launcher that starts N rank processes of this
+script itself (children, never an exec) and exits with their status.  Every rank checks that the
+process group it joined has exactly --gpus ranks.
 
 CPU baseline (rank 0, N = 1): oracle/np_port.py -- a numpy restatement with the reference's
 per-env ACEnv.step call pattern -- one process per host core (bounded at 16), 64 envs each,
 ~10 s, same starting states and action stream.  Run before the GPU is touched.
+
+`--dry-run` exercises the launcher, the process group, the world-size check and the line's
+per-rank fields with no GPU (gloo, a numpy pass per step instead of the kernels); its line says
+so ("dry_run": true) and is never a measurement.
 """
 
 from __future__ import annotations
@@ -29,6 +43,7 @@ import contextlib
 import io
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -41,6 +56,9 @@ sys.path.insert(0, PKG_ROOT)
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+METRIC = "env-steps/sec at batch 2^20, max_relator_len 36; 1/2/4/8 MI355X"
+EXIT_WORLD_MISMATCH = 2  # the process group does not have --gpus ranks
+EXIT_BFS_STALL = 3       # the sharded-BFS variant's collectives stalled (line printed without it)
 
 
 def nw_for(L: int) -> int:
@@ -139,17 +157,60 @@ def cpu_baseline_c_all(L: int, horizon: int, seconds: float, max_procs: int = 16
             "sample": f"oracle/acx_oracle.c env_step, {procs_n} procs x 16384 envs x {seconds:.0f}s"}
 
 
-def dist_setup(local_rank: int, world: int, backend: str = "nccl", force: bool = False):
-    """One process per GPU (torchrun's LOCAL_RANK / WORLD_SIZE / MASTER_*): select this rank's
-    GPU and, for world > 1 (or `force`, a one-rank group: tests/test_gpu_sbfs.py runs the RCCL
-    path that way on one GPU), join the process group -- "nccl" is RCCL over xGMI, bound to the
-    rank's device; "gloo" rehearses N ranks on one GPU.  Returns the rank's device."""
+# ---------------------------------------------------------------------------------------------
+# ranks: launcher, process group, cross-rank reductions
+# ---------------------------------------------------------------------------------------------
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` with no torchrun environment: start N rank processes of this script
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1), before anything here touches
+    the GPU.  The ranks are children (no exec).  Rank 0 prints the line.  When a rank exits
+    non-zero, the others are stopped (their exact PIDs) and that status is returned."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    return rc
+
+
+def dist_setup(local_rank: int, world: int, backend: str = "nccl", force: bool = False, cpu: bool = False):
+    """One process per GPU (LOCAL_RANK / WORLD_SIZE / MASTER_* from torchrun or spawn_ranks):
+    select this rank's GPU and, for world > 1 (or `force`, a one-rank group: tests/test_gpu_sbfs.py
+    runs the RCCL path that way on one GPU), join the process group -- "nccl" is RCCL over xGMI,
+    bound to the rank's device; "gloo" rehearses N ranks on one GPU (or, with `cpu`, on none).
+    Returns the rank's device."""
     import torch
     import torch.distributed as dist
 
-    gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
     if world > 1 or force:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -158,17 +219,38 @@ def dist_setup(local_rank: int, world: int, backend: str = "nccl", force: bool =
     return dev
 
 
+def _coll_device(dev):
+    """where a small reduction tensor lives: the rank's GPU under RCCL, host memory otherwise"""
+    import torch
+    import torch.distributed as dist
+
+    return dev if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
 def synced_max(value: float, dev) -> float:
-    """max over the ranks of a host float (the timed region's wall time): an RCCL all_reduce of a
-    device scalar; the value itself in a single process without a process group."""
+    """max over the ranks of a host float (a timed region's wall time); the value itself in a
+    single process without a process group."""
     import torch
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()):
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_rows(row, dev) -> list:
+    """every rank's row of floats (all_gather), in rank order; [row] without a process group"""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return [list(map(float, row))]
+    t = torch.tensor(list(map(float, row)), dtype=torch.float64, device=_coll_device(dev))
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(v) for v in o.cpu().tolist()] for o in out]
 
 
 def barrier() -> None:
@@ -178,7 +260,13 @@ def barrier() -> None:
         dist.barrier()
 
 
-def main():
+def world_seen() -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -186,21 +274,92 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU")
     ap.add_argument("--L", type=int, default=36)
     ap.add_argument("--horizon", type=int, default=200)
+    ap.add_argument("--workload", choices=("rollout", "step"), default="rollout",
+                    help="headline: PPO rollout collection (configs[2]) or per-call random-action stepping "
+                         "(configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-step-api", action="store_true")
     ap.add_argument("--no-learner", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-bfs", action="store_true")
+    ap.add_argument("--no-search", action="store_true", help="skip config 4's single-GPU search variants")
     ap.add_argument("--no-desync", action="store_true")
     ap.add_argument("--no-obs8", action="store_true")
     ap.add_argument("--bfs-timeout", type=float, default=180.0,
-                    help="world > 1: seconds the sharded-BFS variant may take before the line is printed without it")
-    args = ap.parse_args()
+                    help="world > 1: seconds the sharded-BFS variant may take before the line is printed "
+                         "without it (exit status 3)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: launcher / process group / line plumbing only (gloo, numpy pass per step)")
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse_args()
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    run_rank(args)
+
+
+def _check_world(args, rank: int) -> int:
+    seen = world_seen()
+    if seen != args.gpus:
+        sys.stderr.write(f"bench.py rank {rank}: process group has {seen} rank(s), --gpus {args.gpus}\n")
+        sys.stderr.flush()
+        sys.exit(EXIT_WORLD_MISMATCH)
+    return seen
+
+
+def _per_rank_rows(rows):
+    return [{"rank": i, "value": r[0], "kernel_ms": r[1], "frac": r[2], "wall_ms": r[3]} for i, r in enumerate(rows)]
+
+
+def dry_run(args, rank: int, local_rank: int, world: int) -> None:
+    """Launcher / process-group / line plumbing with no GPU: a numpy pass over this rank's
+    (B, 2L) int32 shard per step stands in for the kernels."""
+    import torch.distributed as dist
+
+    dev = dist_setup(local_rank, world, "gloo", cpu=True)
+    seen = _check_world(args, rank)
+    L, B, K, W = args.L, args.batch, args.steps, args.warmup
+    shard = ms_starts(L, B, offset=rank * B)
+    acc = np.zeros(B, np.int64)
+
+    def pass_(t):
+        acc[:] += (shard != 0).sum(1) + t
+
+    for t in range(W):
+        pass_(t)
+    barrier()
+    t0 = time.perf_counter()
+    for t in range(K):
+        pass_(t)
+    barrier()
+    el = time.perf_counter() - t0
+    elapsed = synced_max(el, dev)
+    rows = gather_rows([B * K / el, el * 1e3, 0.0, el * 1e3], dev)
+    line = {
+        "metric": METRIC, "value": seen * B * K / elapsed, "unit": "env-steps/s", "n_gpus": seen, "steps": K,
+        "warmup": W, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32", "data": "dry run: no GPU work (launcher / process-group check)",
+        "dry_run": True, "world_size_seen": seen, "per_rank": _per_rank_rows(rows),
+        "config": {"workload": f"dry run ({args.workload})", "global_batch": seen * B, "envs_per_gpu": B,
+                   "max_relator_length": L, "parallelism": f"env-index shards x{seen}, no data-path collective"},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_rank(args):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.dry_run:
+        return dry_run(args, rank, local_rank, world)
     L, B, K, W, H = args.L, args.batch, args.steps, args.warmup, args.horizon
 
     cpu = None
@@ -217,9 +376,28 @@ def main():
 
     backend = os.environ.get("ACX_DIST_BACKEND", "nccl")  # "gloo": rehearse N ranks on one GPU
     dev = dist_setup(local_rank, world, backend)
+    seen = _check_world(args, rank)
 
-    import acx
+    import acx  # noqa: F401
     from acx import ops
+
+    def timed(fn):
+        """(max-over-ranks wall seconds, this rank's HIP-event seconds on the current stream) of
+        fn(), bracketed by barrier + synchronize on both sides"""
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        return synced_max(wall, dev), e0.elapsed_time(e1) / 1e3, wall
 
     starts = torch.as_tensor(ms_starts(L, B, offset=rank * B)).to(dev)
     state = starts.clone()
@@ -232,77 +410,87 @@ def main():
     T_CHUNK = max(1, min(200, (160 << 30) // max(1, B * (8 * L + 10))))
     T_buf = min(max(K, W), T_CHUNK)
     actions = torch.randint(0, 12, (W + K, B), dtype=torch.int32, device=dev, generator=g)
-    obs = torch.empty((T_buf, B, 2 * L), dtype=torch.int32, device=dev)
-    rew = torch.empty((T_buf, B), dtype=torch.int32, device=dev)
-    done = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
-    trunc = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
+    rollout_head = args.workload == "rollout"
     err = torch.zeros(B, dtype=torch.uint8, device=dev)
     err_count = torch.zeros(1, dtype=torch.int32, device=dev)
-    # a PPO loop reuses its rollout buffers; touch them once (untimed) so the timed region
-    # does not pay first-touch page mapping of a fresh 60 GB allocation
-    for buf in (obs, rew, done, trunc):
-        buf.zero_()
-
-    # the launches go through ops.RolloutPlan (checks and pointers resolved once per chunk
-    # length, as a PPO loop reusing its buffers would); same kernels and results as ops.rollout
-    plans = {}
-
-    def plan(n):
-        if n not in plans:
-            plans[n] = ops.RolloutPlan(state, starts, count, T=n, horizon=H, cyclical=True, obs_traj=obs[:n],
-                                       reward_traj=rew[:n], done_traj=done[:n], trunc_traj=trunc[:n], err=err,
-                                       err_count=err_count)
-        return plans[n]
-
-    def roll(a, T):
-        for t0 in range(0, T, T_buf):
-            t1 = min(T, t0 + T_buf)
-            plan(t1 - t0)(a[t0:t1])
-
-    plan(min(K, T_buf)), plan(K % T_buf or T_buf)  # built before the timed region
-
-    # warmup (W env steps, untimed)
-    if W > 0:
-        roll(actions[:W], W)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    roll(actions[W : W + K], K)
-    t_launch = time.perf_counter() - t0
-    ev1.record()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = synced_max(elapsed, dev)
-    n_err = int(err_count.item())  # the headline rollout's env errors (warmup + timed)
-
-    # algorithmic bytes of the rollout launch (DESIGN.md "Roofline"): per env-step action 4 B
-    # + obs 8L B + reward 4 + done 1 + truncated 1; per env per launch state in/out 2*8L,
-    # step count in/out 8, err 1; plus the starting state (8L) of every env that resets
-    step_bytes = 4 + 8 * L + 4 + 1 + 1
+    # the rollout variants (int8 trajectory, scattered resets) go with the rollout headline only
+    do_obs8 = rollout_head and not args.no_obs8
+    do_desync = rollout_head and not args.no_desync
+    if rollout_head:
+        obs = torch.empty((T_buf, B, 2 * L), dtype=torch.int32, device=dev)
+        rew = torch.empty((T_buf, B), dtype=torch.int32, device=dev)
+        done = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
+        trunc = torch.empty((T_buf, B), dtype=torch.uint8, device=dev)
+        # a PPO loop reuses its rollout buffers; touch them once (untimed) so the timed region
+        # does not pay first-touch page mapping of a fresh 60 GB allocation
+        for buf in (obs, rew, done, trunc):
+            buf.zero_()
     n_launch = -(-K // T_buf)
+    step_bytes = 4 + 8 * L + 4 + 1 + 1
 
     def count_resets(T):
-        # resets of the last launch = done | truncated over its steps (both never hold together
-        # in a way that matters: a reset reads one row either way)
+        # resets of the last launch = done | truncated over its steps (a reset reads one row)
         if T > T_buf:
             return None
         return int((done[:T] | trunc[:T]).sum().item())
 
     def rollout_bytes(n_resets):
+        # algorithmic bytes of the rollout launches (DESIGN.md "Roofline"): per env-step action 4 B
+        # + obs 8L B + reward 4 + done 1 + truncated 1; per env per launch state in/out 2*8L,
+        # step count in/out 8, err 1; plus the starting state (8L) of every env that resets
         return K * B * step_bytes + n_launch * B * (16 * L + 8 + 1) + (n_resets or 0) * 8 * L
 
-    resets = count_resets(K)
-    launch_bytes = rollout_bytes(resets)
-    achieved = launch_bytes / kernel_s / 1e9
-
     variants = {}
+    head = {}  # the headline's timing and roofline
+
+    if rollout_head:
+        # the launches go through ops.RolloutPlan (checks and pointers resolved once per chunk
+        # length, as a PPO loop reusing its buffers would); same kernels and results as ops.rollout
+        plans = {}
+
+        def plan(n):
+            if n not in plans:
+                plans[n] = ops.RolloutPlan(state, starts, count, T=n, horizon=H, cyclical=True, obs_traj=obs[:n],
+                                           reward_traj=rew[:n], done_traj=done[:n], trunc_traj=trunc[:n], err=err,
+                                           err_count=err_count)
+            return plans[n]
+
+        def roll(a, T):
+            for t0 in range(0, T, T_buf):
+                t1 = min(T, t0 + T_buf)
+                plan(t1 - t0)(a[t0:t1])
+
+        plan(min(K, T_buf)), plan(K % T_buf or T_buf)  # built before the timed region
+        if W > 0:
+            roll(actions[:W], W)  # warmup (W env steps, untimed)
+        t_launch = [0.0]
+
+        def go_head():
+            t0 = time.perf_counter()
+            roll(actions[W: W + K], K)
+            t_launch[0] = time.perf_counter() - t0
+
+        elapsed, kernel_s, wall_local = timed(go_head)
+        n_err = int(err_count.item())  # the headline rollout's env errors (warmup + timed)
+        resets = count_resets(K)
+        launch_bytes = rollout_bytes(resets)
+        achieved = launch_bytes / kernel_s / 1e9
+        head = {
+            "elapsed": elapsed, "kernel_s": kernel_s, "wall_local": wall_local, "frac": achieved / HBM_PEAK_GBS,
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "kernel": ("acx::pack_actions_kernel + " if plan(min(K, T_buf)).packs else "")
+                + f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,1>",
+                "bytes_per_env_step": step_bytes, "launch_bytes": launch_bytes, "resets_in_launch": resets,
+                "launches": n_launch, "kernel_ms": kernel_s * 1e3, "host_launch_ms": t_launch[0] * 1e3,
+            },
+            "workload": (f"PPO rollout collection (BASELINE configs[2]): {B} envs/GPU, L={L}, horizon {H}, "
+                         "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
+                         f"acx_rollout launches of <= {T_buf} steps ({n_launch} for K={K})"),
+            "env_errors": n_err,
+        }
+        del plans
 
     def desync_variant(start_rows, count0, what):
         # the rollout with the episodes out of phase (step_count[i] = i mod H): ~B/H envs reset
@@ -321,23 +509,16 @@ def main():
 
         if W > 0:
             go(actions[:W], W)
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        go(actions[W : W + K], K)
-        e1.record()
-        torch.cuda.synchronize()
-        s_d = e0.elapsed_time(e1) / 1e3
+        wall, s_d, _ = timed(lambda: go(actions[W: W + K], K))
         nres = count_resets(K)
         nb = rollout_bytes(nres)
-        return {"value": B * K / s_d, "unit": "env-steps/s", "kernel_ms": s_d * 1e3, "ms_per_step": s_d / K * 1e3,
-                "resets_per_step": None if nres is None else nres / K, "env_errors": int(err_count.item()),
-                "workload": what,
+        return {"value": seen * B * K / wall, "unit": "env-steps/s", "kernel_ms": s_d * 1e3,
+                "ms_per_step": wall / K * 1e3, "resets_per_step": None if nres is None else nres / K,
+                "env_errors": int(err_count.item()), "workload": what,
                 "roofline": {"bound": "hbm", "achieved": nb / s_d / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": nb / s_d / 1e9 / HBM_PEAK_GBS, "launch_bytes": nb}}
 
-    if not args.no_obs8:
+    if do_obs8:
         # the headline rollout (same starts, counts from 0, same actions) with the observation
         # trajectory in the reference's observation dtype, int8 (ac_env.py:64-70: Box(int8); the
         # observations SyncVectorEnv returns): 2L bytes per env-step instead of 8L
@@ -354,18 +535,11 @@ def main():
 
         if W > 0:
             go8(actions[:W], W)
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        go8(actions[W : W + K], K)
-        e1.record()
-        torch.cuda.synchronize()
-        s8 = e0.elapsed_time(e1) / 1e3
+        wall8, s8, _ = timed(lambda: go8(actions[W: W + K], K))
         nres = count_resets(K)
         nb8 = rollout_bytes(nres) - K * B * 6 * L  # obs 2L instead of 8L bytes per env-step
         variants["rollout_obs_int8"] = {
-            "value": B * K / s8, "unit": "env-steps/s", "kernel_ms": s8 * 1e3, "ms_per_step": s8 / K * 1e3,
+            "value": seen * B * K / wall8, "unit": "env-steps/s", "kernel_ms": s8 * 1e3, "ms_per_step": wall8 / K * 1e3,
             "env_errors": int(err_count.item()),
             "workload": "the headline rollout writing the (K,B,2L) observation trajectory as int8 (the reference's "
                         "observation_space dtype) instead of int32",
@@ -374,7 +548,7 @@ def main():
                          "bytes_per_env_step": step_bytes - 6 * L}}
         del obs8, st8, cnt8
 
-    if not args.no_desync:
+    if do_desync:
         desync = torch.arange(B, dtype=torch.int32, device=dev) % H
         variants["rollout_desync"] = desync_variant(
             starts, desync, "the headline rollout with step_count[i] = i mod H (Miller-Schupp starts): about B/H "
@@ -388,9 +562,10 @@ def main():
                              "(generate_trivial_states, utils.py:91-114) with step_count[i] = i mod H, so dones "
                              "and resets fire on a large share of env-steps")
         del tstarts, desync
-    chg_rate = None  # changed relators per env-step of the in-place step (step_api variant)
-    if not args.no_step_api:
-        # per-call acx_step API: one launch per env step, state in/out of HBM each step
+
+    chg_rate = None  # changed relators per env-step of the in-place step (step_api)
+    if not args.no_step_api or not rollout_head:
+        # per-call acx_step API: one launch per env step, state in place in HBM, autoreset
         rew1 = torch.empty(B, dtype=torch.int32, device=dev)
         dn1 = torch.empty(B, dtype=torch.uint8, device=dev)
         tr1 = torch.empty(B, dtype=torch.uint8, device=dev)
@@ -405,15 +580,12 @@ def main():
         err_count.zero_()
         for t in range(W):
             step(actions[t])
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for t in range(K):
-            step(actions[W + t])
-        e1.record()
-        torch.cuda.synchronize()
-        s_api = e0.elapsed_time(e1) / 1e3
+
+        def go_steps():
+            for t in range(K):
+                step(actions[W + t])
+
+        wall_api, s_api, wall_api_local = timed(go_steps)
         n_err_api = int(err_count.item())
         # The in-place step writes back only the relators that changed (gated moves, no-op
         # cyclic conjugations and failed envs leave their rows as they are in HBM), so the bytes
@@ -428,20 +600,30 @@ def main():
         chg /= 8
         chg_rate = chg
         # per env-step: state in 8L + action 4 + count in 4 + changed relators x 4L + lengths 8 +
-        # reward 4 + done 1 + truncated 1 + count out 4 + err 1; full rows: state out 8L
-        sb_full = 16 * L + 27
+        # reward 4 + done 1 + truncated 1 + count out 4 + err 1 (SURVEY 8d counts full-row
+        # writes, 8L out; the in-place kernel skips unchanged relators, PMC-checked r02h)
         sb = 8 * L + 27 + 4 * L * chg
+        step_kernel = f"acx::step_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,false>"
         variants["step_api"] = {
-            "value": world * B * K / s_api if world == 1 else None,
-            "unit": "env-steps/s",
-            "ms_per_step": s_api / K * 1e3,
+            "value": seen * B * K / wall_api, "unit": "env-steps/s", "ms_per_step": wall_api / K * 1e3,
+            "kernel_ms": s_api * 1e3,
             "roofline": {"bound": "hbm", "achieved": B * sb / (s_api / K) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS, "kernel": step_kernel,
                          "bytes_per_env_step": sb, "changed_relators_per_env_step": chg,
-                         "bytes_per_env_step_full_rows": sb_full,
-                         "frac_on_full_row_bytes": B * sb_full / (s_api / K) / 1e9 / HBM_PEAK_GBS},
+                         "bytes_note": "state read 8L + changed relators x 4L written + 27 B of scalars "
+                                       "(in place: unchanged relators are not written)"},
             "env_errors": n_err_api,
         }
+        if not rollout_head:
+            a_api = B * sb / (s_api / K) / 1e9
+            head = {
+                "elapsed": wall_api, "kernel_s": s_api, "wall_local": wall_api_local, "frac": a_api / HBM_PEAK_GBS,
+                "roofline": dict(variants["step_api"]["roofline"], kernel_ms=s_api * 1e3, launches=K,
+                                 launch_bytes=B * sb),
+                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step, {B} envs/GPU, L={L}, "
+                             f"horizon {H}, cyclical=True, in-place state, same-step autoreset; {K} launches"),
+                "env_errors": n_err_api,
+            }
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
         # the ctypes launches on the capture stream) and replayed: no per-launch host cost
@@ -451,21 +633,16 @@ def main():
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.stream(gs):
                 with torch.cuda.graph(graph, stream=gs):
-                    for t in range(K):
-                        step(actions[W + t])
+                    go_steps()
             torch.cuda.synchronize()
             graph.replay()  # warm
-            torch.cuda.synchronize()
-            e0.record()
-            graph.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            s_g = e0.elapsed_time(e1) / 1e3
+            wall_g, s_g, _ = timed(graph.replay)
             variants["step_api_hipgraph"] = {
-                "value": B * K / s_g if world == 1 else None, "unit": "env-steps/s", "ms_per_step": s_g / K * 1e3,
+                "value": seen * B * K / wall_g, "unit": "env-steps/s", "ms_per_step": wall_g / K * 1e3,
+                "kernel_ms": s_g * 1e3,
                 "roofline": {"bound": "hbm", "achieved": B * sb / (s_g / K) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": B * sb / (s_g / K) / 1e9 / HBM_PEAK_GBS,
-                             "bytes_per_env_step": sb, "bytes_per_env_step_full_rows": sb_full},
+                             "bytes_per_env_step": sb},
             }
             del graph
 
@@ -480,41 +657,225 @@ def main():
         lobs = torch.empty((KL + 1, B, 2 * L), dtype=torch.float32, device=dev)
         lrew = torch.empty((KL, B), dtype=torch.float32, device=dev)
         ldone = torch.empty((KL, B), dtype=torch.float32, device=dev)
-        la = actions[W : W + KL].to(torch.int64)
+        la = actions[W: W + KL].to(torch.int64)
         lobs.zero_()
         lenv.step(la[0], obs_out=lobs[1], reward_out=lrew[0], done_out=ldone[0])
-        torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for t in range(KL):
-            lenv.step(la[t], obs_out=lobs[t + 1], reward_out=lrew[t], done_out=ldone[t])
-        e1.record()
-        torch.cuda.synchronize()
-        s_l = e0.elapsed_time(e1) / 1e3
+
+        def go_learn():
+            for t in range(KL):
+                lenv.step(la[t], obs_out=lobs[t + 1], reward_out=lrew[t], done_out=ldone[t])
+
+        _, s_l, _ = timed(go_learn)
         # per env-step: state in/out 16L + action 8 + count in/out 8 + obs f32 8L + reward f32 4
         # + done f32 4 + done/trunc u8 2 + history 1 + episode_len 4 + err 1 + curriculum
-        # (done/trunc re-read 2, needs_host 1)
-        # The state store is in place (changed relators only, see step_api): the same walk
-        # distribution as the step_api variant (Miller-Schupp starts, uniform moves, horizon H),
-        # so its measured changed-relator rate prices the state write-back.
+        # (done/trunc re-read 2, needs_host 1).  The state store is in place (changed relators
+        # only, see step_api): the same walk distribution as the step_api variant, so its
+        # measured changed-relator rate prices the state write-back.
         lb_full = 24 * L + 35
         lb = lb_full if chg_rate is None else lb_full - 8 * L + 4 * L * chg_rate
         variants["learner_step"] = {
             "value": B * KL / s_l, "unit": "env-steps/s", "steps": KL, "ms_per_step": s_l / KL * 1e3,
             "roofline": {"bound": "hbm", "achieved": B * lb / (s_l / KL) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb,
-                         "bytes_per_env_step_full_rows": lb_full,
-                         "frac_on_full_row_bytes": B * lb_full / (s_l / KL) / 1e9 / HBM_PEAK_GBS},
+                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb},
         }
         del lobs, lrew, ldone, lenv
 
-    def sharded_bfs_variant():
-        # BASELINE configs[3] on the owner-partitioned BFS (csrc/acx_sbfs.hip): AK(3), L = 36, to
-        # 10^7 nodes; node store + visited set sharded over the ranks by key owner, per-chunk RCCL
-        # all_gather / all_to_all / all_reduce (world 1: the exchanges are local copies)
-        from acx.envs.utils import convert_relators_to_presentation
-        from acx.search import _sharded_bfs as SB
+    if not args.no_search and world == 1:
+        variants.update(search_variants(dev))
+
+    # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
+    # used only when that profile's workload matches this run's.  A profile of the same (B, L, K)
+    # gives the launch's measured bytes directly; one of another K is carried over as its
+    # measured/algorithmic ratio (the launch's bytes are the same per-step and per-launch terms
+    # at any K, so the ratio is K-independent) and labelled as scaled.
+    traffic, traffic_src = None, None
+    if rollout_head:
+        traffic, traffic_src = committed_traffic(B, L, K, head["roofline"]["launch_bytes"])
+    head["roofline"].update(traffic=traffic, traffic_source=traffic_src)
+
+    rows = gather_rows([B * K / head["wall_local"], head["kernel_s"] * 1e3, head["frac"], head["wall_local"] * 1e3],
+                       dev)
+    elapsed = head["elapsed"]
+    line = {
+        "metric": METRIC,
+        "value": seen * B * K / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": seen,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: Miller-Schupp starting states (all_presentations.txt, env i -> i mod 1190), "
+                "uniform random move ids (torch.Generator seed 0+rank)",
+        "config": {
+            "workload": head["workload"],
+            "global_batch": seen * B,
+            "envs_per_gpu": B,
+            "max_relator_length": L,
+            "horizon": H,
+            "parallelism": f"env-index shards x{seen}, no data-path collective",
+        },
+        "world_size_seen": seen,
+        "dist_backend": backend if seen > 1 else None,
+        "per_rank": _per_rank_rows(rows),
+        "roofline": head["roofline"],
+        "cpu_baseline": cpu,
+        "cpu_baseline_c_oracle": cpu_c,
+        "cpu_baseline_c_oracle_all_cores": cpu_c_all,
+        "variants": variants,
+        "env_errors": head["env_errors"],
+    }
+    if not args.no_bfs:
+        run_sharded_bfs_variant(args, line, variants, dev, rank, world, backend)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def committed_traffic(B, L, K, launch_bytes):
+    """(HBM bytes of the headline launch from the newest committed rocprofv3 PMC profile of this
+    workload, where from) or (None, None)"""
+    cands = []
+    for tag in ("r04_k20", "r04", "r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h",
+                "r02_k20", "r02", "r01"):
+        prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
+        if not os.path.exists(prof):
+            continue
+        with open(prof) as f:
+            ps = json.load(f)
+        pc = ps.get("bench_line", {}).get("config", {})
+        td = ps.get("rollout_timed_dispatch") or {}
+        if pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and td.get("pmc_hbm_bytes"):
+            cands.append((ps["bench_line"].get("steps") != K, tag, ps["bench_line"].get("steps"), td))
+    if not cands:
+        return None, None
+    scaled, tag, kp, td = min(cands, key=lambda c: c[0])
+    where = f"profiles/{tag.split('_')[0][:3]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE"
+    if not scaled:
+        return td["pmc_hbm_bytes"], f"{where} of this command (K={K})"
+    ratio = td["pmc_hbm_bytes"] / td["algorithmic_bytes"]
+    return (launch_bytes * ratio,
+            f"{where} at K={kp}: measured/algorithmic = {ratio:.4f}, applied to this launch's algorithmic bytes")
+
+
+def search_variants(dev) -> dict:
+    """BASELINE configs[3] on one GPU: bfs from AK(3), L = 36, cyclical = False, to 10^7 nodes.
+      device_bfs      -- the whole search on the GPU (csrc/acx_bfs.hip), best of 3 wall times;
+      expand12_keys   -- the 12-way expansion kernel alone over the first 10^7 BFS nodes
+                         (576 B per parent: row in 8L + 12 packed child keys);
+      host_dedup_bfs  -- BASELINE's wording, "dedup on host": GPU expansion + the host engine
+                         (csrc/acx_search.cpp) replaying the reference's FIFO / dedup / budget;
+                         kernel time, kernel + copies, and the host's share reported apart."""
+    import torch
+
+    from acx import _lib, ops
+    from acx.envs.utils import convert_relators_to_presentation
+    from acx.search import _device_bfs as D
+    from acx.search import _engine as E
+    from acx.search import bfs
+
+    out = {}
+    L, nb = 36, 10 ** 7
+    ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], L)
+    work = "bfs from AK(3), L=36, cyclical=False, to 10^7 nodes (BASELINE configs[3])"
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            D.device_bfs(ak3, nb, device=dev, keep_node_keys=True)  # warm: workspace, and the node keys
+        keys = D.LAST_STATS["node_keys"][:nb]
+        walls = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(io.StringIO()):
+                D.device_bfs(ak3, nb, device=dev)
+            torch.cuda.synchronize()
+            walls.append(time.perf_counter() - t0)
+        st = dict(D.LAST_STATS)
+        best = min(walls)
+        out["device_bfs"] = {"value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3,
+                             "walls_ms": [w * 1e3 for w in walls], "nodes": st["nodes"],
+                             "parents_expanded": st["parents"], "chunks": st["chunks"], "workload": work + "; device "
+                             "visited set (csrc/acx_bfs.hip)"}
+        D.release_workspaces()
+        kw = _lib.key_words(L)
+        parents = ops.unpack_keys(torch.as_tensor(keys.view(np.int64)).to(dev), L)
+        N = parents.shape[0]
+        kout = {"keys": torch.empty((N, 12, kw), dtype=torch.int64, device=dev)}
+        ops.expand12(parents, cyclical=False, children=False, lengths=False, keys=True, err=False, out=kout)
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.expand12(parents, cyclical=False, children=False, lengths=False, keys=True, err=False, out=kout)
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3)
+        best = min(times)
+        bpp = 8 * L + 12 * kw * 8
+        out["expand12_keys"] = {"value": 12 * N / best, "unit": "children/s", "parents": N, "kernel_ms": best * 1e3,
+                                "roofline": {"bound": "hbm", "achieved": N * bpp / best / 1e9, "peak": HBM_PEAK_GBS,
+                                             "unit": "GB/s", "frac": N * bpp / best / 1e9 / HBM_PEAK_GBS,
+                                             "bytes_per_parent": bpp},
+                                "workload": "acx_expand12 keys-only over the first 10^7 nodes of that BFS"}
+        del kout, parents, keys
+        torch.cuda.empty_cache()
+        with contextlib.redirect_stdout(io.StringIO()):
+            t0 = time.perf_counter()
+            bfs(ak3, nb, device=dev, engine="host")
+            wall = time.perf_counter() - t0
+        es = dict(E.LAST_STATS)
+        host_s = es["host_next_s"] + es["host_store_s"] + es["host_replay_s"]
+        out["host_dedup_bfs"] = {
+            "value": es["nodes"] / wall, "unit": "BFS nodes/s", "wall_ms": wall * 1e3, "nodes": es["nodes"],
+            "parents_expanded": es["expanded"], "rounds": es["rounds"],
+            "kernel_ms": es["kernel_s"] * 1e3,
+            "kernel_children_per_s": 12 * es["expanded"] / es["kernel_s"],
+            "kernel_d2h_ms": es["gpu_roundtrip_s"] * 1e3,
+            "kernel_d2h_children_per_s": 12 * es["expanded"] / es["gpu_roundtrip_s"],
+            "host_dedup_ms": host_s * 1e3,
+            "end_to_end_children_per_s": 12 * es["expanded"] / wall,
+            "workload": work + "; dedup on host (engine='host'): kernel_ms = unpack + expand12 on the GPU, "
+                               "kernel_d2h_ms = + H2D parents / D2H child keys per batch, host_dedup_ms = the host "
+                               "engine's pop / store / replay"}
+    except Exception as e:  # noqa: BLE001 -- a variant: its failure must not cost the headline line
+        out["search_error"] = repr(e)[:300]
+    return out
+
+
+def run_sharded_bfs_variant(args, line, variants, dev, rank, world, backend) -> None:
+    """BASELINE configs[3] on the owner-partitioned BFS (csrc/acx_sbfs.hip): AK(3), L = 36, to 10^7
+    nodes; node store + visited set sharded over the ranks by key owner, per-chunk RCCL
+    all_gather / all_to_all / all_reduce (world 1: the exchanges are local copies).  Last, behind
+    a watchdog: the one variant with collectives on its data path.  If its exchanges at world > 1
+    stall, every rank's watchdog prints the line (rank 0) with the variant marked and exits with
+    EXIT_BFS_STALL: a hang costs neither the headline line nor a visible failure status."""
+    import threading
+
+    import torch
+
+    from acx.envs.utils import convert_relators_to_presentation
+    from acx.search import _sharded_bfs as SB
+
+    variants["sharded_bfs"] = {"error": f"timeout after {args.bfs_timeout:.0f} s"}
+    timed_out_line = json.dumps(line)
+
+    def on_timeout():
+        if rank == 0:  # the variant may be inside redirect_stdout: write to the real stdout
+            sys.__stdout__.write(timed_out_line + "\n")
+            sys.__stdout__.flush()
+        os._exit(EXIT_BFS_STALL)
+
+    dog = threading.Timer(args.bfs_timeout, on_timeout) if world > 1 else None
+    if dog is not None:
+        dog.daemon = True
+        dog.start()
+    try:
         ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
         nb = 10 ** 7
         with contextlib.redirect_stdout(io.StringIO()):
@@ -530,125 +891,18 @@ def main():
             el = synced_max(time.perf_counter() - t0, dev)
             best = el if best is None else min(best, el)
         st = SB.LAST_STATS
-        return {
+        variants["sharded_bfs"] = {
             "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],
             "parents_expanded": st["parents"], "chunks": st["chunks"], "result": list(res) if res[0] else [False, None],
             "workload": "BASELINE configs[3]: bfs from AK(3), L=36, cyclical=False, to 10^7 nodes; node store and "
                         f"visited set partitioned by key owner over {world} rank(s), "
                         f"{'RCCL' if backend == 'nccl' else backend} exchanges per chunk",
         }
-
-    # HBM traffic per launch from rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
-    # "HBM"), measured by profile_cmd.sh on this same command and committed under profiles/;
-    # used only when that profile's workload matches this run's
-    # (the newest committed profile of this workload at this K; profile_cmd.sh profiles the
-    # driver's own command, bench.py --steps 20 --warmup 5, and the K = 200 default)
-    # A profile of the same (B, L, K) gives the launch's measured bytes directly; one of another K
-    # is carried over as its measured/algorithmic ratio (the launch's bytes are the same per-step
-    # and per-launch terms at any K, so the ratio is K-independent) and labelled as scaled.
-    traffic, traffic_src = None, None
-    cands = []
-    for tag in ("r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h", "r02_k20", "r02", "r01"):
-        prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
-        if not os.path.exists(prof):
-            continue
-        with open(prof) as f:
-            ps = json.load(f)
-        pc = ps.get("bench_line", {}).get("config", {})
-        td = ps.get("rollout_timed_dispatch") or {}
-        if pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and td.get("pmc_hbm_bytes"):
-            cands.append((ps["bench_line"].get("steps") != K, tag, ps["bench_line"].get("steps"), td))
-    if cands:
-        scaled, tag, kp, td = min(cands, key=lambda c: c[0])
-        where = f"profiles/{tag.split('_')[0][:3]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc WRITE_SIZE"
-        if not scaled:
-            traffic, traffic_src = td["pmc_hbm_bytes"], f"{where} of this command (K={K})"
-        else:
-            ratio = td["pmc_hbm_bytes"] / td["algorithmic_bytes"]
-            traffic = launch_bytes * ratio
-            traffic_src = (f"{where} at K={kp}: measured/algorithmic = {ratio:.4f}, applied to this launch's "
-                           "algorithmic bytes")
-
-    value = world * B * K / elapsed
-    line = {
-        "metric": "env-steps/sec at batch 2^20, max_relator_len 36; 1/2/4/8 MI355X",
-        "value": value,
-        "unit": "env-steps/s",
-        "n_gpus": world,
-        "steps": K,
-        "warmup": W,
-        "ms_per_step": elapsed / K * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic: Miller-Schupp starting states (all_presentations.txt, env i -> i mod 1190), "
-                "uniform random move ids (torch.Generator seed 0+rank)",
-        "config": {
-            "workload": (f"PPO rollout collection (BASELINE configs[2]): {B} envs/GPU, L={L}, horizon {H}, "
-                         "cyclical=True, same-step autoreset, full (K,B,2L) int32 obs trajectory; "
-                         f"acx_rollout launches of <= {T_buf} steps ({n_launch} for K={K})"),
-            "global_batch": world * B,
-            "envs_per_gpu": B,
-            "max_relator_length": L,
-            "horizon": H,
-            "parallelism": f"env-index shards x{world}, no data-path collective",
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "kernel": ("acx::pack_actions_kernel + " if plan(min(K, T_buf)).packs else "")
-            + f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,1>",
-            "bytes_per_env_step": step_bytes,
-            "launch_bytes": launch_bytes,
-            "resets_in_launch": resets,
-            "launches": n_launch,
-            "kernel_ms": kernel_s * 1e3,
-            "host_launch_ms": t_launch * 1e3,
-        },
-        "cpu_baseline": cpu,
-        "cpu_baseline_c_oracle": cpu_c,
-        "cpu_baseline_c_oracle_all_cores": cpu_c_all,
-        "variants": variants,
-        "env_errors": n_err,
-    }
-    if not args.no_bfs:
-        # last, behind a watchdog: the one variant with collectives on its data path.  If its RCCL
-        # exchanges at world > 1 ever stalled, every rank's watchdog prints the line (rank 0) with
-        # the variant marked and exits, so a hang there cannot cost the headline line
-        import threading
-
-        from acx.search import _sharded_bfs as SB
-        variants["sharded_bfs"] = {"error": f"timeout after {args.bfs_timeout:.0f} s"}
-        timed_out_line = json.dumps(line)
-
-        def on_timeout():
-            if rank == 0:  # the variant may be inside redirect_stdout: write to the real stdout
-                sys.__stdout__.write(timed_out_line + "\n")
-                sys.__stdout__.flush()
-            os._exit(0)
-
-        dog = threading.Timer(args.bfs_timeout, on_timeout) if world > 1 else None
-        if dog is not None:
-            dog.daemon = True
-            dog.start()
-        try:  # a variant: its failure (the same on every rank) must not cost the headline line
-            variants["sharded_bfs"] = sharded_bfs_variant()
-        except Exception as e:  # noqa: BLE001
-            variants["sharded_bfs"] = {"error": repr(e)[:300]}
-        if dog is not None:
-            dog.cancel()
-        SB.release_workspaces()
-
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- a variant (failing the same on every rank)
+        variants["sharded_bfs"] = {"error": repr(e)[:300]}
+    if dog is not None:
+        dog.cancel()
+    SB.release_workspaces()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,77 @@
+"""CPU: bench.py's multi-rank launcher and its checks, with no GPU (`--dry-run`: gloo, a numpy pass
+per step in place of the kernels).
+
+* `bench.py --gpus 2` with no torchrun environment starts two rank processes itself, both join one
+  process group, and rank 0 prints ONE line with n_gpus 2, world_size_seen 2 and a per-rank block;
+* a torchrun group whose size differs from --gpus fails with a non-zero status (no line);
+* a rank that fails makes the launcher fail with that rank's status."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+from conftest import REPO
+
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _lines(out):
+    return [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+
+
+def test_launcher_spawns_two_ranks_one_line():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "4", "--warmup", "1",
+                        "--batch", "512"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["world_size_seen"] == 2 and d["dry_run"] is True
+    assert [r["rank"] for r in d["per_rank"]] == [0, 1]
+    assert d["config"]["global_batch"] == 1024 and d["config"]["envs_per_gpu"] == 512
+    # value = all ranks' env-steps / max-over-ranks wall time
+    assert abs(d["value"] - 2 * 512 * 4 / (d["ms_per_step"] * 4 / 1e3)) < 1e-6 * d["value"]
+
+
+def test_one_rank_line_has_the_same_shape():
+    p = subprocess.run([sys.executable, BENCH, "--dry-run", "--steps", "3", "--warmup", "0", "--batch", "256"],
+                       cwd=REPO, capture_output=True, text=True, timeout=120, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    (d,) = _lines(p.stdout)
+    assert d["n_gpus"] == 1 and d["world_size_seen"] == 1 and len(d["per_rank"]) == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_world_size_mismatch_fails():
+    # torchrun starts 2 ranks but the command says --gpus 3: every rank refuses to measure
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH, "--gpus", "3",
+                        "--dry-run", "--steps", "2", "--warmup", "0", "--batch", "64"],
+                       cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
+    assert p.returncode != 0
+    assert not _lines(p.stdout)
+    assert "process group has 2 rank(s), --gpus 3" in p.stderr
+
+
+def test_failing_rank_fails_the_launcher():
+    sys.path.insert(0, REPO)
+    import bench
+
+    # every rank rejects the argument list (argparse exits 2); the launcher returns that status
+    rc = bench.spawn_ranks(2, ["--dry-run", "--workload", "no-such-workload"])
+    assert rc == 2

@@ -1,14 +1,16 @@
 #!/bin/bash
 # bench.py's N = 2 flow on one GPU (gloo, both ranks on cuda:0): first with a watchdog timeout so
-# short that the sharded-BFS variant cannot finish (the line must still come out, exit 0), then
-# with the default.  Each step under its own time limit, chained.
+# short that the sharded-BFS variant cannot finish (the line must still come out, with exit
+# status 3 = bench.EXIT_BFS_STALL), then with the default through bench.py's own launcher
+# (--gpus 2, no torchrun).  Each step under its own time limit, chained.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
 export ACX_DIST_BACKEND=gloo
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
-  bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-learner --no-step-api --bfs-timeout 0.2 > gpurun_out/n2_watchdog.json 2> gpurun_out/n2_watchdog.err || exit 1
-echo watchdog-run-done; tail -c 400 gpurun_out/n2_watchdog.json
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 \
-  bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-learner --no-step-api > gpurun_out/n2_default.json 2> gpurun_out/n2_default.err || exit 2
+  bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-learner --no-step-api --bfs-timeout 0.2 > gpurun_out/n2_watchdog.json 2> gpurun_out/n2_watchdog.err
+rc=$?
+[ $rc -eq 1 ] || [ $rc -eq 3 ] || exit 1  # torchrun reports a failed rank as 1
+echo watchdog-run-done rc=$rc; tail -c 400 gpurun_out/n2_watchdog.json
+timeout -k 10 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-learner --no-step-api > gpurun_out/n2_default.json 2> gpurun_out/n2_default.err || exit 2
 echo default-run-done

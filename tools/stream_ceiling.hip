@@ -1,0 +1,103 @@
+// Streaming ceilings of the in-place step's access shape, on a (B, 2L) int32
+// state of B = 2^20 rows (1 GB at L = 128), no compute:
+//   read_grid     float4 grid-stride read of the whole state (8 waves/SIMD), one dword out per block
+//   read_tile     the step kernel's tile shape: a wave per 64 rows, 16-B loads in batches of NB,
+//                 each batch drained before the next (CodeTile::load), 4 waves/SIMD via LDS
+//   read_tile_pipe  the same with the next batch issued before the current one is consumed
+//                 (>= NB loads always in flight)
+//   rw_tile       read_tile + a write of the first WQ/4 of every row in place (1 : WQ/4)
+//   rw_tile_pipe  read_tile_pipe + the same write
+// One block = 4 waves (256 threads) as the step kernel; LDS per block sized for the occupancy.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+constexpr int WAVE = 64, BLOCK = 256;
+
+__global__ __launch_bounds__(256) void read_grid(const int4* __restrict__ src, int64_t n16, int* out) {
+    int acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n16; i += (int64_t)gridDim.x * BLOCK) {
+        const int4 v = src[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x7fffffff) out[blockIdx.x] = acc;  // never true for the probe's data; keeps the loads
+}
+
+// a wave per 64-row tile of rows of `cpr` 16-B chunks
+template <int NB, bool PIPE, int WQ>
+__global__ __launch_bounds__(256) void tile_kernel(int4* __restrict__ st, int cpr, int64_t rows, int* out) {
+    extern __shared__ int smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wid) * WAVE;
+    if (r0 >= rows) return;
+    const int4* src = st + r0 * cpr + lane;
+    const int nch = 64 * cpr / WAVE;  // chunks per lane
+    int acc = 0;
+    if (!PIPE) {
+        for (int u0 = 0; u0 < nch; u0 += NB) {
+            int4 v[NB];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) v[u] = src[(u0 + u) * WAVE];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+            smem[threadIdx.x] = acc;  // an LDS write per batch, as the tile conversion does
+        }
+    } else {
+        int4 a[NB], b[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) a[u] = src[u * WAVE];
+        for (int u0 = 0; u0 < nch; u0 += 2 * NB) {
+            if (u0 + NB < nch) {
+#pragma unroll
+                for (int u = 0; u < NB; ++u) b[u] = src[(u0 + NB + u) * WAVE];
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u) acc ^= a[u].x ^ a[u].y ^ a[u].z ^ a[u].w;
+            smem[threadIdx.x] = acc;
+            if (u0 + 2 * NB < nch) {
+#pragma unroll
+                for (int u = 0; u < NB; ++u) a[u] = src[(u0 + 2 * NB + u) * WAVE];
+            }
+            if (u0 + NB < nch) {
+#pragma unroll
+                for (int u = 0; u < NB; ++u) acc ^= b[u].x ^ b[u].y ^ b[u].z ^ b[u].w;
+                smem[threadIdx.x] = acc;
+            }
+        }
+    }
+    if constexpr (WQ > 0) {
+        // write the first WQ/4 of each of the tile's rows back in place (the row's first chunks)
+        const int wch = cpr * WQ / 4;
+        int4* dst = st + r0 * cpr;
+        for (int c = lane; c < 64 * wch; c += WAVE) {
+            const int r = c / wch, k = c - r * wch;
+            dst[r * cpr + k] = make_int4(acc, r, k, lane);  // the probe's state is scratch
+        }
+    }
+    if (acc == 0x7fffffff) out[blockIdx.x] = acc;
+}
+
+extern "C" {
+// kind: 0 read_grid, 1 read_tile, 2 read_tile_pipe, 3 rw_tile, 4 rw_tile_pipe; nb in {8, 16};
+// lds_per_block bytes of dynamic LDS (occupancy control); returns 0 or a hip error code
+int probe_run(int kind, int nb, void* state, int64_t rows, int L, int lds_per_block, void* out, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int cpr = 2 * L / 4;
+    int4* st = (int4*)state;
+    const unsigned tiles = (unsigned)((rows + 255) / 256);
+    if (kind == 0) {
+        read_grid<<<dim3(256 * 8 * 4), dim3(BLOCK), 0, s>>>(st, rows * cpr, (int*)out);
+    } else {
+#define GO(NB, P, W) tile_kernel<NB, P, W><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>(st, cpr, rows, (int*)out)
+        if (nb == 8) {
+            if (kind == 1) GO(8, false, 0); else if (kind == 2) GO(8, true, 0);
+            else if (kind == 3) GO(8, false, 1); else GO(8, true, 1);
+        } else {
+            if (kind == 1) GO(16, false, 0); else if (kind == 2) GO(16, true, 0);
+            else if (kind == 3) GO(16, false, 1); else GO(16, true, 1);
+        }
+#undef GO
+    }
+    return (int)hipGetLastError();
+}
+}
