@@ -63,7 +63,7 @@ class CurriculumRecord:
     def process(self, env, done, truncated, needs_host, obs_out=None) -> list:
         """One step's bookkeeping next to LearnerEnv.step: `done`, `truncated`, `needs_host` as
         returned by it (device or host arrays).  Solved episodes update the record from
-        env.episode_actions(i); envs the device placed (round 1) take env.curr_index[i]; envs it
+        env.episode_actions_many (one copy for all of them); envs the device placed (round 1) take env.curr_index[i]; envs it
         flagged are drawn here and placed with env.place (obs_out: the step's observation row
         buffer, as for LearnerEnv.place).  Returns [(env, state index)] for every restart."""
         d = np.asarray(done.cpu() if hasattr(done, "cpu") else done).astype(bool)
@@ -73,10 +73,16 @@ class CurriculumRecord:
         if fin.size == 0:
             return []
         dev_idx = env.curr_index.cpu().numpy()
+        # the solved episodes' move lists, copied to the host together (one transfer per step)
+        solved = [i for i in fin.tolist() if d[i]]
+        if hasattr(env, "episode_actions_many"):
+            acts = env.episode_actions_many(solved)
+        else:
+            acts = {i: env.episode_actions(i) for i in solved}
         out = []
         for i in fin.tolist():
             if d[i]:
-                self.on_done(i, env.episode_actions(i))
+                self.on_done(i, acts[i])
             if h[i]:
                 k = self.draw()
                 env.place(i, k, obs_out=obs_out)

@@ -121,6 +121,21 @@ class LearnerEnv:
             raise ValueError(f"episode of {n} moves exceeds hist_cap {self.hist_cap}")
         return [int(x) for x in self.action_hist[:n, i].cpu().numpy()]
 
+    def episode_actions_many(self, envs) -> dict:
+        """{i: info["actions"]} for the envs `envs` (host ints) whose episodes ended at the last
+        step: one copy of their episode lengths and one of their action-history columns (not a
+        device round trip per env)."""
+        envs = [int(i) for i in envs]
+        if not envs:
+            return {}
+        idx = torch.as_tensor(envs, dtype=torch.int64, device=self.episode_len.device)
+        lens = self.episode_len[idx].cpu().numpy()
+        n_max = int(lens.max())
+        if n_max > self.hist_cap:
+            raise ValueError(f"episode of {n_max} moves exceeds hist_cap {self.hist_cap}")
+        cols = self.action_hist[:n_max, idx].cpu().numpy()
+        return {i: [int(x) for x in cols[: int(lens[j]), j]] for j, i in enumerate(envs)}
+
     def place(self, i: int, state_index: int, obs_out: Optional[torch.Tensor] = None) -> None:
         """Host placement of env i (after round 1, training.py:337-352): start from
         initial_states[state_index]."""

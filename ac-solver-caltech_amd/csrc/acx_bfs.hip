@@ -53,6 +53,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <vector>
 
@@ -522,10 +523,16 @@ __global__ __launch_bounds__(TPB) void bfs_commit_kernel(Args a) {
         if (n0 + i < a.qcap) a.queue[n0 + i] = st[i];
 }
 
-// root: node 0 (code 1) and its table entry
+// the root's packed key, passed by value (no host-to-device copy of host memory per search)
+struct RootKey {
+    uint64_t w[ACX_MAX_L / 16 + 2];
+};
+
+// root: node 0 (code 1), its key in the store and its table entry
 template <int KWM>
-__global__ void bfs_root_kernel(Args a) {
+__global__ void bfs_root_kernel(Args a, RootKey rk) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int k = 0; k < a.kw; ++k) a.store[k] = rk.w[k];
     const Key<KWM> key = kload<KWM>(a.store, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
     uint64_t* ent = a.table + (h & a.bmask) * BUCKET;
@@ -737,23 +744,29 @@ struct Search {
     int64_t kbase = 0;             // chunks enqueued by earlier searches
     int epoch = 0;                 // 8-entry table: the last search's epoch (0: table all zero)
     uint16_t* trace_host = nullptr;
-    int32_t* path_dev = nullptr;
-    int64_t* path_n_dev = nullptr;
+    int32_t* path_dev = nullptr;    // pinned, coherent host memory: bfs_path_kernel writes the path
+    int64_t* path_n_dev = nullptr;  // there directly (no device-to-host copy)
     std::vector<int32_t> trace;  // new minima of the last run, in order
 
     ~Search() {
         if (fin_pending) (void)hipEventSynchronize(fin);
-        void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.tmin, a.table, a.ctl, a.trace, path_dev,
-                        path_n_dev, a.live};
+        void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.tmin, a.table, a.ctl, a.trace, a.live};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
-        if (mirror) (void)hipHostFree(mirror);
-        if (trace_host) (void)hipHostFree(trace_host);
+        void* hptrs[] = {mirror, trace_host, path_dev, path_n_dev};
+        for (void* p : hptrs)
+            if (p) (void)hipHostFree(p);
         if (fin) (void)hipEventDestroy(fin);
     }
 };
 
 static constexpr int64_t PATH_CAP = 1 << 16;
+// a chunk (<= 2^20 parents, ~0.15 ms) that has not published its state after this long is a
+// kernel that does not finish: acx_bfs_run returns ACX_E_LAUNCH instead of polling forever
+#ifndef ACX_BFS_CHUNK_DEADLINE_S
+#define ACX_BFS_CHUNK_DEADLINE_S 30.0
+#endif
+static constexpr int ACX_E_TIMEOUT = -100;  // internal to acx_bfs_run (returned as ACX_E_LAUNCH)
 static int g_bfs_layout = 0;  // 0 default (8-entry table), 2 key-in-table where L allows (tests, A/B)
 
 template <class T>
@@ -791,8 +804,9 @@ struct ChunkLaunch {
 struct RootLaunch {
     Search* S;
     hipStream_t st;
+    RootKey rk;
     template <int NW>
-    void go() { bfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a); }
+    void go() { bfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a, rk); }
 };
 struct PathLaunch {
     Search* S;
@@ -841,8 +855,9 @@ void* acx_bfs_create(int32_t L, int64_t max_nodes, int64_t chunk_parents, int32_
               dalloc(a.cand, (size_t)(S->tiles_max * TILE_CH)) && dalloc(a.lost, (size_t)(S->tiles_max * TILE_CH)) &&
               dalloc(a.pmin, (size_t)S->pmax) && dalloc(a.tsum, (size_t)S->tiles_max) &&
               dalloc(a.tmin, (size_t)S->tiles_max) && dalloc(a.table, (size_t)ts) &&
-              dalloc(a.ctl, 1) && dalloc(a.trace, (size_t)TRACE_CAP) && dalloc(S->path_dev, (size_t)(2 * PATH_CAP)) &&
-              dalloc(S->path_n_dev, 1) && dalloc(a.live, 1) &&
+              dalloc(a.ctl, 1) && dalloc(a.trace, (size_t)TRACE_CAP) && dalloc(a.live, 1) &&
+              hipHostMalloc((void**)&S->path_dev, sizeof(int32_t) * 2 * PATH_CAP, hipHostMallocCoherent) == hipSuccess &&
+              hipHostMalloc((void**)&S->path_n_dev, sizeof(int64_t), hipHostMallocCoherent) == hipSuccess &&
               hipHostMalloc((void**)&S->mirror, sizeof(LiveMirror) * RING, hipHostMallocCoherent) == hipSuccess &&
               hipHostMalloc((void**)&S->trace_host, sizeof(uint16_t) * TRACE_CAP, hipHostMallocCoherent) == hipSuccess &&
               hipMemset(a.lost, 0, (size_t)(S->tiles_max * TILE_CH)) == hipSuccess &&
@@ -876,14 +891,16 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;
     const int L = S->L, kw = S->kw;
-    uint64_t root[ACX_MAX_L / 16 + 2];
-    pack_key(presentation, L, kw, root);
+    RootLaunch rl{S, st, {}};
+    pack_key(presentation, L, kw, rl.rk.w);
     int total0 = 0;
     for (int i = 0; i < 2 * L; ++i) total0 += presentation[i] != 0;
 
-    // the previous search's speculative chunk may still be in flight (on another stream, too)
-    if (S->fin_pending && hipStreamWaitEvent(st, S->fin, 0) != hipSuccess) return ACX_E_LAUNCH;
-    if (hipMemcpyAsync(a.store, root, (size_t)kw * 8, hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+    // a previous search that ended on an error may have left work in flight (on another stream, too)
+    if (S->fin_pending) {
+        if (hipStreamWaitEvent(st, S->fin, 0) != hipSuccess) return ACX_E_LAUNCH;
+        S->fin_pending = false;
+    }
     if (a.kt) {  // key-in-table entries have no epoch: cleared per search
         if (hipMemsetAsync(a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
         a.ep = 0;
@@ -894,7 +911,6 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
         }
         a.ep = (uint64_t)S->epoch << EP_SHIFT;
     }
-    RootLaunch rl{S, st};
     by_nw(L, rl);
     bfs_init_kernel<<<dim3(1), dim3(64), 0, st>>>(a, max_nodes, S->pmax, (uint32_t)total0);
 
@@ -905,18 +921,22 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     // the device state; once the search has ended they do nothing.
     S->trace.clear();
     // chunk numbers run on across searches (S->kbase), so a slot never holds a stale match
+    int64_t enqueued = 0;  // chunk numbers this search has used
     auto enqueue = [&](int64_t k, int64_t avail_ub) -> int {
         const int64_t pub = avail_ub < S->pmax ? avail_ub : S->pmax;
         ChunkLaunch cl{S, st, S->kbase + k, (int)((pub - 1) / TILE + 2)};
         by_nw(L, cl);
+        enqueued = k + 1;
         return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
     };
     // poll the slot's sequence number (written last, system scope, by the chunk's close kernel);
     // no per-chunk event (an event marker held the next chunk back ~5 us).  Every 4096 polls
-    // the stream is queried so that a failed launch cannot leave the host spinning.
+    // the stream is queried so that a failed launch cannot leave the host spinning, and a chunk
+    // that has not published within ACX_BFS_CHUNK_DEADLINE_S seconds (a hung kernel) is an error.
     auto wait_chunk = [&](int64_t k) -> int {
         const int64_t K = S->kbase + k;
         const uint64_t* seq = &S->mirror[K % RING].seq;
+        const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t it = 1;; ++it) {
             if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) == (uint64_t)(K + 1)) return ACX_OK;
             if ((it & 4095) == 0) {
@@ -924,8 +944,24 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
                 if (e == hipSuccess)  // idle: the slot is final now
                     return __atomic_load_n(seq, __ATOMIC_ACQUIRE) == (uint64_t)(K + 1) ? ACX_OK : ACX_E_LAUNCH;
                 if (e != hipErrorNotReady) return ACX_E_LAUNCH;
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(ACX_BFS_CHUNK_DEADLINE_S))
+                    return ACX_E_TIMEOUT;
             }
         }
+    };
+    // every exit after the first enqueue: the chunk numbers used advance kbase, and the chunks
+    // still in the stream (the speculative one after the search's end) are retired before the
+    // search returns -- on success the stream is idle when acx_bfs_run returns.  After a
+    // timeout (a kernel that does not finish) nothing is waited for here: `fin` makes the next
+    // search and the destructor wait instead.
+    auto finish = [&](int rc) -> int {
+        S->kbase += enqueued;
+        const bool rec = hipEventRecord(S->fin, st) == hipSuccess;
+        S->fin_pending = rec;
+        if (rc == ACX_E_TIMEOUT) return ACX_E_LAUNCH;
+        if (!rec || hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+        S->fin_pending = false;
+        return rc;
     };
     const int64_t qcap = S->qcap;
     auto grow = [&](int64_t avail) -> int64_t {  // bound on the next chunk's available parents
@@ -934,21 +970,20 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
         return ub < qcap ? ub : qcap;
     };
     int64_t next_ub = grow(1);  // chunk 1's bound (chunk 0 expands the root alone)
-    if (enqueue(0, 1) != ACX_OK || enqueue(1, next_ub) != ACX_OK) return ACX_E_LAUNCH;
+    if (enqueue(0, 1) != ACX_OK || enqueue(1, next_ub) != ACX_OK) return finish(ACX_E_LAUNCH);
     Live lv{};
     int64_t k = 0;
     for (;; ++k) {
-        if (wait_chunk(k) != ACX_OK) return ACX_E_LAUNCH;
+        const int w = wait_chunk(k);
+        if (w != ACX_OK) return finish(w);
         lv = S->mirror[(S->kbase + k) % RING].s;
         if (lv.stop) break;
         // exact state after chunk k = chunk k + 1's parameters: bound chunk k + 2
         const int64_t avail = lv.n_nodes - lv.head;
-        if (enqueue(k + 2, grow(avail)) != ACX_OK) return ACX_E_LAUNCH;
+        if (enqueue(k + 2, grow(avail)) != ACX_OK) return finish(ACX_E_LAUNCH);
     }
-    S->kbase += k + 2;  // chunk k + 1 is in the stream (it does nothing)
-    if (hipEventRecord(S->fin, st) != hipSuccess) return ACX_E_LAUNCH;
-    S->fin_pending = true;
-    if (lv.status < 0) return ACX_E_LAUNCH;  // table overflow (cannot happen at load <= 1/2)
+    // chunk k + 1 is in the stream (it does nothing): retired here, with the path kernel below
+    if (lv.status < 0) return finish(ACX_E_LAUNCH);  // table overflow (cannot happen at load <= 1/2)
     const int status = lv.status;
     const int64_t n_nodes = lv.n_nodes, parents = lv.parents, chunks = lv.chunks;
     const int64_t min_len = lv.running;
@@ -960,13 +995,15 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     if (status == ACX_BFS_FOUND) {
         PathLaunch pl{S, st, succ_node};
         by_nw(L, pl);
-        int64_t d = 0;
-        if (hipMemcpyAsync(&d, S->path_n_dev, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return ACX_E_LAUNCH;
-        if (hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
+        if (hipGetLastError() != hipSuccess) return finish(ACX_E_LAUNCH);
+    }
+    const int fin_rc = finish(ACX_OK);  // the stream is idle from here on
+    if (fin_rc != ACX_OK) return fin_rc;
+    if (status == ACX_BFS_FOUND) {
+        const int64_t d = *(volatile int64_t*)S->path_n_dev;
         if (d > PATH_CAP) return ACX_E_ARG;
         std::vector<int32_t> buf((size_t)(2 * d + 2));
-        if (d && hipMemcpy(buf.data(), S->path_dev, (size_t)(2 * d) * 4, hipMemcpyDeviceToHost) != hipSuccess)
-            return ACX_E_LAUNCH;
+        for (int64_t i = 0; i < 2 * d; ++i) buf[(size_t)i] = ((volatile int32_t*)S->path_dev)[i];
         buf[2 * d] = (int32_t)succ_act;
         buf[2 * d + 1] = 2;
         // reference path: [(-1, total0)] + edges + (succ action, 2)

@@ -271,7 +271,10 @@ int acx_unpack_keys(const uint64_t* keys, int32_t* states, int32_t* lengths_out,
  *                    per node, 2.9 GB at 10^7 nodes and L = 36).
  *   acx_bfs_run      searches from `presentation` (HOST pointer, 2L int32, a valid presentation
  *                    with letters +-1, +-2) with budget max_nodes (<= the create-time value);
- *                    synchronous on `stream`.  On ACX_BFS_FOUND the reference's path
+ *                    synchronous on `stream`: when it returns, `stream` is idle (every chunk
+ *                    it enqueued, the speculative one after the search's end included, has
+ *                    retired).  A chunk that does not publish its state within 30 s (a kernel
+ *                    that does not finish) returns ACX_E_LAUNCH.  On ACX_BFS_FOUND the reference's path
  *                    [(-1, initial total), (action, total)...] is written to path_actions /
  *                    path_totals (first path_cap entries).  stats (int64[5]) = n_nodes
  *                    (len(tree_nodes) at the end), parents expanded, chunks, min total length

@@ -125,3 +125,21 @@ def test_host_engine_expansion_sharded_over_devices(mode, budget, batch, shards)
     from acx import bfs
     with pytest.raises(ValueError):
         bfs(start, 10, device=[DEV, DEV])
+
+
+@pytest.mark.parametrize("budget", [10 ** 6, 10 ** 7])
+def test_device_bfs_leaves_the_stream_idle(budget):
+    # acx_bfs_run retires every chunk it enqueued -- the speculative one after the search's end
+    # included -- before it returns (breadth_first.py:91-97: the search returns with nothing
+    # pending); a search that finds a path (AK(2)) as well as one cut by the budget (AK(3))
+    import io
+    from contextlib import redirect_stdout
+
+    from acx.envs.utils import convert_relators_to_presentation
+    from acx.search import bfs
+    ak2 = convert_relators_to_presentation([1, 1, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
+    s = torch.cuda.current_stream(DEV)
+    for pres in (_ak3(36), ak2):
+        with redirect_stdout(io.StringIO()):
+            bfs(pres, budget, device=DEV)
+        assert s.query(), "work left on the caller's stream after bfs returned"

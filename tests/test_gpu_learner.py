@@ -55,8 +55,9 @@ def test_learner_env_matches_training_loop_restatement(L, B, N, H, T, adtype):
         assert np.array_equal(rew[t].cpu().numpy(), res["reward"].astype(np.float32))
         assert np.array_equal(dones[t].cpu().numpy(), res["done"].astype(np.float32))
         assert np.array_equal(ep_len.cpu().numpy(), res["episode_len"])
+        many = env.episode_actions_many(list(res["info_actions"].keys()))
         for i, acts in res["info_actions"].items():
-            assert env.episode_actions(i) == acts
+            assert env.episode_actions(i) == acts and many[i] == acts
             n_done += 1
         assert np.array_equal(env.state.cpu().numpy(), ref.state), t
         assert np.array_equal(obs[t + 1].cpu().numpy(), ref.state.astype(np.float32)), t

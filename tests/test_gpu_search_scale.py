@@ -267,16 +267,24 @@ with open(os.path.join(GOLDEN, "search_scale_1e7.json")) as _f:
     CONFIG4 = json.load(_f)[0]
 
 
-@pytest.mark.parametrize("engine", ["device", "sharded"])
+@pytest.mark.parametrize("engine", ["device", "sharded", "host"])
 def test_config4_full_frontier_matches_reference(engine, capsys):
     """BASELINE configs[3] at its full size, pinned to the reference itself: the reference bfs
     from AK(3), L = 36, to 10^7 nodes (make_golden.py --search-scale-1e7: 1,589,594 parents
-    expanded, every parent state in the rolling sha256) against the device BFS and the
-    owner-partitioned BFS at one rank -- same printed budget message, result, parent count and
-    parent order."""
+    expanded, every parent state in the rolling sha256) against the device BFS, the
+    owner-partitioned BFS at one rank and the host-dedup engine (BASELINE's "dedup on host":
+    GPU expansion, csrc/acx_search.cpp replaying the FIFO / dedup / budget) -- same printed
+    budget message, result, parent count and parent order."""
     c = CONFIG4
     assert c["budget"] == 10 ** 7 and c["L"] == 36 and c["parents"] == 1589594
-    if engine == "device":
+    if engine == "host":
+        from acx.search import _engine as E
+        res = E.run_search(E.BFS, np.array(c["presentation"]), c["budget"], True, c["cyclical"], device=DEV,
+                           keep_node_keys=True)
+        res = (True, res[1]) if res[0] else (False, None)
+        st = dict(E.LAST_STATS, parents=len(E.LAST_STATS["popped"]))
+        keys = E.LAST_STATS["node_keys"][E.LAST_STATS["popped"]][: c["parents"]]
+    elif engine == "device":
         from acx.search import _device_bfs as D
         res = D.device_bfs(np.array(c["presentation"]), c["budget"], verbose=True,
                            cyclically_reduce_after_moves=c["cyclical"], device=DEV, keep_node_keys=True)
