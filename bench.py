@@ -689,9 +689,10 @@ def run_rank(args):
     # gives the launch's measured bytes directly; one of another K is carried over as its
     # measured/algorithmic ratio (the launch's bytes are the same per-step and per-launch terms
     # at any K, so the ratio is K-independent) and labelled as scaled.
-    traffic, traffic_src = None, None
     if rollout_head:
         traffic, traffic_src = committed_traffic(B, L, K, head["roofline"]["launch_bytes"])
+    else:
+        traffic, traffic_src = committed_step_traffic(B, L, head["roofline"]["launch_bytes"])
     head["roofline"].update(traffic=traffic, traffic_source=traffic_src)
 
     rows = gather_rows([B * K / head["wall_local"], head["kernel_s"] * 1e3, head["frac"], head["wall_local"] * 1e3],
@@ -761,6 +762,26 @@ def committed_traffic(B, L, K, launch_bytes):
     ratio = td["pmc_hbm_bytes"] / td["algorithmic_bytes"]
     return (launch_bytes * ratio,
             f"{where} at K={kp}: measured/algorithmic = {ratio:.4f}, applied to this launch's algorithmic bytes")
+
+
+def committed_step_traffic(B, L, launch_bytes):
+    """(HBM bytes per step launch, where from) for --workload step: the newest committed
+    rocprofv3 PMC profile of the step workload at this (B, L), as its measured/algorithmic ratio
+    applied to this launch's algorithmic bytes (the changed-relator rate, hence the bytes, vary
+    slightly with the walk); or (None, None)"""
+    for tag in ("r04_step128", "r04_step36"):
+        prof = os.path.join(REPO, "profiles", "r04", f"{tag}_summary.json")
+        if not os.path.exists(prof):
+            continue
+        with open(prof) as f:
+            ps = json.load(f)
+        pc = ps.get("bench_line", {}).get("config", {})
+        rec = ps.get("step_timed_dispatches") or {}
+        if pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and rec.get("pmc_over_algorithmic"):
+            r = rec["pmc_over_algorithmic"]
+            return (launch_bytes * r, f"profiles/r04/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc "
+                                      f"WRITE_SIZE per step launch, measured/algorithmic = {r:.4f}")
+    return None, None
 
 
 def search_variants(dev) -> dict:

@@ -117,6 +117,29 @@ if bench:
             "pmc_hbm_bytes": traffic,
         })
         summary["rollout_timed_dispatch"] = rec
+if bench and "random-action stepping" in bench["config"]["workload"]:
+    # bench.py --workload step: the headline is K per-call acx_step launches after W warmup
+    # calls (then 8 off-the-clock calls for the changed-relator rate, then the hipGraph ones)
+    import re
+    steps = [(n, v) for n, v in summary["kernels"].items() if re.search(r"step_kernel<\d+, \d+, \d+, false>", n)]
+    if steps:
+        kname, k = max(steps, key=lambda nv: nv[1]["dispatches"])
+        W, K = bench["warmup"], bench["steps"]
+        idx = list(range(W, W + K))
+        ms = [k["durations_ms"][i] for i in idx]
+        tb = [(k.get("fetch_bytes_corrected") or [None] * (W + K))[i] for i in idx]
+        wb = [(k.get("write_bytes") or [None] * (W + K))[i] for i in idx]
+        per = bench["roofline"]["launch_bytes"]
+        rec = {"kernel": kname, "timed_dispatch_index": [idx[0], idx[-1]], "mean_ms": sum(ms) / K,
+               "bench_event_ms_per_launch": bench["roofline"]["kernel_ms"] / K,
+               "algorithmic_bytes_per_launch": per}
+        if None not in tb and None not in wb:
+            rec.update(fetch_bytes_per_launch=sum(tb) / K, write_bytes_per_launch=sum(wb) / K,
+                       pmc_hbm_bytes_per_launch=(sum(tb) + sum(wb)) / K,
+                       pmc_over_algorithmic=(sum(tb) + sum(wb)) / K / per)
+        rec["agree_pct"] = 100 * abs(rec["mean_ms"] - rec["bench_event_ms_per_launch"]) / rec["bench_event_ms_per_launch"]
+        summary["step_timed_dispatches"] = rec
+        print(json.dumps(rec, indent=1))
 with open(os.path.join(out_dir, f"{tag}_summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
 for src, dst in (("trace/bench_kernel_stats.csv", "kernel_stats.csv"), ("trace/bench_kernel_trace.csv", "kernel_trace.csv"),
