@@ -1031,9 +1031,14 @@ int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap) {
     if (out && n > 0) {
         uint64_t* tmp = nullptr;
         if (hipMalloc((void**)&tmp, (size_t)(n * S->kw) * 8) != hipSuccess) return ACX_E_LAUNCH;
-        bfs_gather_kernel<<<dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB)>>>(S->a, n, tmp);
-        const bool ok = hipGetLastError() == hipSuccess &&
-                        hipMemcpy(out, tmp, (size_t)(n * S->kw) * 8, hipMemcpyDeviceToHost) == hipSuccess;
+        hipStream_t st = nullptr;
+        bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+        if (ok) {
+            bfs_gather_kernel<<<dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(S->a, n, tmp);
+            ok = hipGetLastError() == hipSuccess &&
+                 copy_to_host(out, tmp, (size_t)(n * S->kw) * 8, st) == ACX_OK;
+            (void)hipStreamDestroy(st);
+        }
         (void)hipFree(tmp);
         if (!ok) return ACX_E_LAUNCH;
     }

@@ -4,7 +4,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
+#include "acx.h"
 #include "acx_moves.h"
 
 namespace acx {
@@ -54,6 +56,27 @@ __host__ __device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
     for (int i = 0; i < KWM; ++i)
         if (i < kw) h = fmix64(h ^ k.w[i]) + 0x632be59bd9b4e019ull;
     return fmix64(h);
+}
+
+// device -> pageable host memory through a pinned bounce buffer on `st` (no hipMemcpy into
+// pageable memory: its staged path is a copy whose completion the runtime's tracing never sees)
+static inline int copy_to_host(void* dst, const void* src, size_t n, hipStream_t st) {
+    constexpr size_t BOUNCE = 16u << 20;
+    void* pin = nullptr;
+    const size_t nb = n < BOUNCE ? n : BOUNCE;
+    if (nb == 0) return ACX_OK;
+    if (hipHostMalloc(&pin, nb, hipHostMallocDefault) != hipSuccess) return ACX_E_LAUNCH;
+    int rc = ACX_OK;
+    for (size_t off = 0; off < n && rc == ACX_OK; off += nb) {
+        const size_t m = n - off < nb ? n - off : nb;
+        if (hipMemcpyAsync(pin, (const char*)src + off, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = ACX_E_LAUNCH;
+        else
+            memcpy((char*)dst + off, pin, m);
+    }
+    (void)hipHostFree(pin);
+    return rc;
 }
 
 // LDS written by the wave's lanes is visible to the whole wave after this

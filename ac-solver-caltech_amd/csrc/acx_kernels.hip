@@ -75,6 +75,11 @@ constexpr int STAGE_UNROLL = 8;
 #ifndef ACX_PIPE_LOAD
 #define ACX_PIPE_LOAD 1
 #endif
+// the rollout's int32 observation store split in two halves: step t's second half is issued at
+// the top of step t + 1, ahead of that step's move (FastTile only; A/B knob)
+#ifndef ACX_OBS_SPLIT
+#define ACX_OBS_SPLIT 0
+#endif
 // the step kernel's per-env scalar inputs (move id, step count) loaded before its tile (A/B knob)
 #ifndef ACX_EARLY_SCALARS
 #define ACX_EARLY_SCALARS 1
@@ -321,41 +326,43 @@ struct FastTile {
         wave_sync();
     }
 
-    template <bool NT, bool F32, bool FULL>
+    template <bool NT, bool F32, bool FULL, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_flat(int4* dst, int ln, int nc) const {
 #pragma unroll
-        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+        for (int u0 = UB; u0 < UE; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u)
-                if (u0 + u < CPR && (FULL || ln + (u0 + u) * WAVE < nc)) p[u] = lds[lds_index(ln, u0 + u)];
+                if (u0 + u < UE && (FULL || ln + (u0 + u) * WAVE < nc)) p[u] = lds[lds_index(ln, u0 + u)];
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u)
-                if (u0 + u < CPR && (FULL || ln + (u0 + u) * WAVE < nc))
+                if (u0 + u < UE && (FULL || ln + (u0 + u) * WAVE < nc))
                     out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
         }
     }
 
     // LDS -> R contiguous global rows, EXACTLY CPR store instructions on every path (a partial
     // tile's spare lanes re-store its last chunk, same data to the same address), so the
-    // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load)
-    template <bool NT>
+    // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load).
+    // [UB, UE): a range of the lane's chunk slots only (the rollout's split obs store)
+    static constexpr bool SPLIT_OK = true;
+    template <bool NT, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         int4* dst = reinterpret_cast<int4*>(g);
         const int nc = R * CPR;
         if (R == WAVE) {
-            store_flat<NT, false, true>(dst + ln, ln, nc);
+            store_flat<NT, false, true, UB, UE>(dst + ln, ln, nc);
             return;
         }
 #pragma unroll
-        for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+        for (int u0 = UB; u0 < UE; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
             int cc[STAGE_UNROLL];
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
-                if (u0 + u >= CPR) continue;
+                if (u0 + u >= UE) continue;
                 const int c0 = ln + (u0 + u) * WAVE;
                 const int c = c0 < nc ? c0 : nc - 1;
                 const int r = c / CPR;
@@ -364,7 +371,7 @@ struct FastTile {
             }
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u)
-                if (u0 + u < CPR) out16<NT, false>(dst + cc[u], widen4(p[u]));
+                if (u0 + u < UE) out16<NT, false>(dst + cc[u], widen4(p[u]));
         }
     }
 
@@ -716,6 +723,7 @@ struct CodeTile {
     bool tile_bad = false;
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
+    static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
     __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
         flags[lane] = (uint8_t)code;
         tile_bad = __any(code != 0u);
@@ -1189,6 +1197,7 @@ struct CodeTile {
 
 template <int NW, int LC, int VEC>
 struct GenericTile {
+    static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
     static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
     int L, twoL, rowb;
     char* base;
@@ -1687,6 +1696,13 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
                                                a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
 }
 
+// the first half of a FastTile row's chunk slots, rounded to whole store batches
+template <class Tile>
+constexpr int split_half_chunks() {
+    if constexpr (Tile::SPLIT_OK) return (Tile::CPR / 2 + STAGE_UNROLL - 1) / STAGE_UNROLL * STAGE_UNROLL;
+    else return 0;
+}
+
 struct RolloutArgs {
     int32_t* state;
     const int32_t* actions;
@@ -1745,6 +1761,20 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     __builtin_amdgcn_s_waitcnt(0);
     const int32_t* act_tile = a.actions + w.r0;  // wave-uniform
 
+    // split obs store (ACX_OBS_SPLIT): the trajectory row offset of the step whose second half
+    // is still to be stored, -1 if none (wave-uniform)
+    constexpr bool SPLIT = ACX_OBS_SPLIT != 0 && OBS == 1 && Tile::SPLIT_OK;
+    constexpr int HALF_CH = split_half_chunks<Tile>();
+    int64_t pend_ti = -1;
+    auto flush_half = [&](int lane) {
+        if constexpr (SPLIT) {
+            if (pend_ti >= 0)
+                tile.template store_rows<ACX_NT_OBS != 0, HALF_CH, Tile::CPR>(a.obs_traj + (pend_ti + w.r0) * twoL,
+                                                                          w.R, lane);
+            pend_ti = -1;
+        }
+    };
+
     // One env step of the wave: move, reward/done/truncated, autoreset, obs rows.
     auto step = [&](int t, uint32_t id) {
         const int64_t ti = (int64_t)t * a.B;
@@ -1756,6 +1786,8 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         const int lane = (int)__lane_id();
         int ln = lane;
         asm volatile("" : "+v"(ln));
+        // the previous step's deferred half, from the LDS image before this step changes it
+        flush_half(lane);
         bool reset = false;
         bool both = false;  // the LDS image needs both relators (general move: both reduced)
         bool h1 = false;    // the moved relator (ac_moves.py:167-179: i = (id + 1) & 1)
@@ -1827,8 +1859,14 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 return;
             }
             wave_sync();
-            if constexpr (OBS == 1) tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
-            else tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, lane);
+            if constexpr (SPLIT) {
+                tile.template store_rows<ACX_NT_OBS != 0, 0, HALF_CH>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
+                pend_ti = ti;
+            } else if constexpr (OBS == 1) {
+                tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
+            } else {
+                tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, lane);
+            }
             wave_sync();
         }
     };
@@ -1882,6 +1920,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         for (int k = 0; k < QW; ++k) q[k] = (q[k] >> 4) | (k + 1 < QW ? q[k + 1] << 28 : 0u);
         step(t, id);
     }
+    flush_half(w.lane);
     if (w.active) {
         if (!bad) tile.unpack(w.lane, p);
         a.step_count[env] = cnt;

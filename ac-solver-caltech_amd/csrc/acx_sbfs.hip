@@ -602,9 +602,14 @@ __global__ void sbfs_lookup_kernel(Args a, int64_t g) {
     }
 }
 
+struct RootKey {
+    uint64_t w[ACX_MAX_L / 16 + 2];
+};
+
 template <int KWM>
-__global__ void sbfs_root_kernel(Args a) {
+__global__ void sbfs_root_kernel(Args a, RootKey rk) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int k = 0; k < a.kw; ++k) a.lkeys[k] = rk.w[k];  // passed by value: no host copy
     const Key<KWM> key = kload<KWM>(a.lkeys, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
     a.table[h & a.mask] = (1ull << 32) | (uint32_t)(h >> 32);
@@ -655,9 +660,19 @@ struct InsertLaunch {
 struct RootLaunch {
     Shard* S;
     hipStream_t st;
+    RootKey rk;
     template <int NW>
-    void go() { sbfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a); }
+    void go() { sbfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a, rk); }
 };
+
+// the chunk's control block to its initial values (no host copy)
+__global__ void sbfs_ctl_init_kernel(Ctl* c) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Ctl z;
+    memset(&z, 0, sizeof(z));
+    z.succ_seq = z.err_seq = z.min_len = z.cut_p = NONE;
+    *c = z;
+}
 struct LookupLaunch {
     Shard* S;
     hipStream_t st;
@@ -760,11 +775,8 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
     S->a.nloc = 0;
     if (hipMemsetAsync(S->a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
     if (own == S->rank) {
-        uint64_t root[ACX_MAX_L / 16 + 2];
-        pack_key(presentation, S->L, S->kw, root);
-        if (hipMemcpyAsync(S->a.lkeys, root, (size_t)S->kw * 8, hipMemcpyHostToDevice, st) != hipSuccess)
-            return ACX_E_LAUNCH;
-        RootLaunch rl{S, st};
+        RootLaunch rl{S, st, {}};
+        pack_key(presentation, S->L, S->kw, rl.rk.w);
         by_nw(S->L, rl);
         S->nloc = 1;
     }
@@ -787,11 +799,7 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream
     a.Pr = S->Pr;
     a.lo = S->lo;
     a.nloc = S->nloc;
-    Ctl init;
-    memset(&init, 0, sizeof(init));
-    init.succ_seq = init.err_seq = init.min_len = init.cut_p = NONE;
-    *S->ctl_host = init;
-    if (hipMemcpyAsync(a.ctl, S->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+    sbfs_ctl_init_kernel<<<dim3(1), dim3(64), 0, st>>>(a.ctl);
     if (S->Pr > 0) {
         ExpandLaunch el{S, st};
         by_nw(S->L, el);
@@ -877,8 +885,7 @@ int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream) {
     Shard* S = static_cast<Shard*>(h);
     if (!S) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
-    const uint32_t init = NONE;
-    if (hipMemcpyAsync(&S->a.ctl->min_len, &init, 4, hipMemcpyHostToDevice, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (hipMemsetAsync(&S->a.ctl->min_len, 0xff, 4, st) != hipSuccess) return ACX_E_LAUNCH;  // NONE
     // npar is read on the device; lo was advanced by commit
     Args a = S->a;
     a.lo = S->lo - S->ctl_host->npar;
@@ -911,12 +918,10 @@ int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int6
     sbfs_trace_kernel<<<dim3(1), dim3(1024), 0, st>>>(a, npar, run, e, d_out, d_n);
     int32_t n = 0;
     int64_t res = ACX_E_LAUNCH;
-    if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&n, d_n, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
-        hipStreamSynchronize(st) == hipSuccess) {
+    if (hipGetLastError() == hipSuccess && copy_to_host(&n, d_n, 4, st) == ACX_OK) {
         const int64_t m = n < cap ? n : cap;
         const int64_t mm = m < TRACE_MAX ? m : TRACE_MAX;
-        if (mm == 0 || hipMemcpy(out, d_out, (size_t)(2 * mm) * sizeof(int64_t), hipMemcpyDeviceToHost) == hipSuccess)
-            res = n;
+        if (mm == 0 || copy_to_host(out, d_out, (size_t)(2 * mm) * sizeof(int64_t), st) == ACX_OK) res = n;
     }
     (void)hipFree(d_out);
     (void)hipFree(d_n);
@@ -943,10 +948,15 @@ int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap) 
     Shard* S = static_cast<Shard*>(h);
     if (!S) return ACX_E_ARG;
     const int64_t n = S->nloc < cap ? S->nloc : cap;
-    if (n > 0 && keys && hipMemcpy(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return ACX_E_LAUNCH;
-    if (n > 0 && gids && hipMemcpy(gids, S->a.lgid, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return ACX_E_LAUNCH;
+    if (n > 0 && (keys || gids)) {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ACX_E_LAUNCH;
+        // the search's stream is idle here (every acx_sbfs_* call that enqueues work waits)
+        const bool ok = (!keys || copy_to_host(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, st) == ACX_OK) &&
+                        (!gids || copy_to_host(gids, S->a.lgid, (size_t)n * 8, st) == ACX_OK);
+        (void)hipStreamDestroy(st);
+        if (!ok) return ACX_E_LAUNCH;
+    }
     return S->nloc;
 }
 
