@@ -160,6 +160,8 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
         dev = torch.device("cuda", torch.cuda.current_device())
     comm = _Comm(group, dev, always=always_exchange)
     chunk = int(chunk) if chunk else 1 << 19
+    if not 1 <= chunk <= (1 << 19):
+        raise ValueError("sharded bfs chunks are 1 .. 2^19 parents")
     lcap = local_capacity(max_nodes, comm.world)
     lib = _lib.load()
     # A failure on one rank must fail every rank at the same point, or its peers would block in

@@ -17,10 +17,12 @@
 //
 // Per chunk on rank r:
 //   expand  -- its parents' 12 children (keys action-major), owner per child, per-owner counts;
-//   pack    -- children into the send buffer grouped by owner: record = kw key words + seq;
-//   insert  -- (received records) seq -> record map; probe / claim / join the owner's hash table
-//              with atomicMin on seq (first occurrence wins, as in acx_bfs.hip); mark
-//              survivors as bit (s % 12) of mask[s / 12];
+//   pack    -- children owned by other ranks into the send buffer grouped by owner: record =
+//              kw key words + seq (the rank's own children stay where the expansion wrote them);
+//   insert  -- its own children in place and the received records: probe / claim / join the
+//              owner's hash table with atomicMin on (seq, record) (first occurrence wins, as in
+//              acx_bfs.hip; a displaced child is marked lost); survivors -> bit (s % 12) of
+//              mask[s / 12];
 //   commit  -- after the mask all-reduce every rank knows all survivors: a prefix sum over
 //              parents gives each survivor's global id g and the node-budget cut (identical on
 //              all ranks); a second prefix sum over the survivors this rank owns gives their
@@ -67,8 +69,11 @@ struct Args {
     uint64_t* ckeys;  // (12, Pr) keys of the local parents' children, action-major
     uint8_t* cown;    // (12, Pr) owner of each child, 0xff: parent not in the chunk
     uint16_t* pmin;   // (Pr) min child total per local parent (totals reach 2L = 256)
-    uint32_t* map;    // (12 P) seq -> received record, NONE if not received here
-    uint32_t* rslot;  // (rcap) slot claimed/joined by a received child, SEEN if known
+    uint32_t* sslot;  // (12 P) per chunk seq: table slot its child claimed / joined as the first
+                      // occurrence, SEEN if none (a known state, past the end, or not owned here)
+    uint32_t* sfp;    // (12 P) per chunk seq: the child's 32-bit fingerprint
+    uint8_t* lost;    // (12 P) per chunk seq: a smaller seq of the same state took its entry
+    uint32_t* mine;   // (P) this rank's survivors per parent (bits by action)
     uint32_t* bsum;   // (nb) all survivors per block of parents -> exclusive offsets
     uint32_t* lbsum;  // (nb) own survivors per block -> exclusive offsets
     uint64_t* table;  // (mask + 1)
@@ -80,9 +85,24 @@ struct Args {
     uint32_t* xblk;        // (expand blocks, 2 + world) per-block min child total, parents, owner counts
     uint64_t mask;
     int64_t head, n_before, need, lcap, nloc, lo, nrecv;
-    int P, Pr, L, kw, cyc, world;
+    int P, Pr, L, kw, cyc, world, rank;
     uint32_t end;
 };
+
+// Table entries.  A committed node: (local slot + 1) << 32 | 32-bit fingerprint (bit 63 clear).
+// A child claimed in the running chunk: CHUNK | seq << 40 | record << 16 | 16-bit fingerprint;
+// atomicMin on the whole word keeps the smallest seq -- the reference's first occurrence -- and
+// its record, so a probe compares keys with the entry's own record (no seq -> record map).
+// Records: r < 12 Pr is this rank's own child in ckeys (r = action * Pr + local parent), others
+// are received records r - 12 Pr.  Chunks are <= 2^19 parents: seq < 12 * 2^19 < 2^23, r < 2^24.
+constexpr int SEQ_SHIFT = 40, REC_SHIFT = 16;
+constexpr int64_t MAX_CHUNK = 1 << 19;
+__device__ __forceinline__ uint32_t entry_seq(uint64_t v) { return (uint32_t)(v >> SEQ_SHIFT) & 0x7fffffu; }
+__device__ __forceinline__ uint32_t entry_rec(uint64_t v) { return (uint32_t)(v >> REC_SHIFT) & 0xffffffu; }
+__device__ __forceinline__ const uint64_t* rec_key(const Args& a, uint32_t r) {
+    const uint32_t n_own = 12u * (uint32_t)a.Pr;
+    return r < n_own ? a.ckeys + (int64_t)r * a.kw : a.recv + (int64_t)(r - n_own) * (a.kw + 1);
+}
 
 __device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
     return (uint32_t)(((h >> 32) * (uint64_t)world) >> 32);
@@ -256,11 +276,13 @@ __global__ __launch_bounds__(1024) void sbfs_expand_reduce_kernel(Args a, int nb
     }
     __syncthreads();
     if (t == 0) {
+        // the rank's own children are inserted where the expansion wrote them: no send group
         uint32_t run = 0;
         for (int o = 0; o < a.world; ++o) {
-            a.ctl->cnt[o] = tot[o];
+            const uint32_t c = o == a.rank ? 0u : tot[o];
+            a.ctl->cnt[o] = c;
             a.ctl->cur[o] = run;
-            run += tot[o];
+            run += c;
         }
     }
 }
@@ -283,9 +305,11 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
 #pragma unroll 1
     for (int jj = 0; jj < SAPW; ++jj) {
         const int act = wid * SAPW + jj;
-        const uint32_t o = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : 0xffu;
+        uint32_t o = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : 0xffu;
+        if (o == (uint32_t)a.rank) o = 0xffu;  // inserted in place, not sent
         uint32_t pos = 0;
         for (uint32_t w = 0; w < (uint32_t)a.world; ++w) {
+            if (w == (uint32_t)a.rank) continue;
             const uint64_t m = __ballot(o == w);
             if (!m) continue;
             uint32_t b = lane == 0 ? atomicAdd(&hist[w], (uint32_t)__popcll(m)) : 0u;  // LDS
@@ -300,30 +324,33 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
     }
 }
 
-// (3a) seq -> received record
-__global__ __launch_bounds__(TPB) void sbfs_map_kernel(Args a) {
-    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i >= a.nrecv) return;
-    a.map[(uint32_t)a.recv[i * (a.kw + 1) + a.kw]] = (uint32_t)i;
-}
-
-// (3b) probe / claim / join, one lane per received child (acx_bfs.hip bfs_insert_kernel)
+// (3a) probe / claim / join, one lane per child this rank owns: its own children in place
+// (records r < 12 Pr, ckeys) and the received ones; as acx_bfs.hip's bfs_insert_kernel, the first
+// occurrence of a state within the chunk keeps the entry (atomicMin), a child it displaces is
+// marked lost
 template <int KWM>
 __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 waves/SIMD (latency-bound)
-    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i >= a.nrecv) return;
-    const int rw = a.kw + 1;
-    const uint64_t* rec = a.recv + i * rw;
-    const uint32_t s = (uint32_t)rec[a.kw];
-    if (s > a.end) {  // after the search's last child
-        a.rslot[i] = SEEN;
-        return;
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    const int64_t n_own = 12 * (int64_t)a.Pr;
+    if (r >= n_own + a.nrecv) return;
+    uint32_t s;
+    const uint64_t* kp;
+    if (r < n_own) {
+        if (a.cown[r] != (uint8_t)a.rank) return;  // another rank's child, or a parent past the chunk
+        const int act = (int)(r / a.Pr);
+        const int j = (int)(r - (int64_t)act * a.Pr);
+        s = (uint32_t)(a.lgid[a.lo + j] - a.head) * 12u + (uint32_t)act;
+        kp = a.ckeys + r * a.kw;
+    } else {
+        kp = a.recv + (r - n_own) * (a.kw + 1);
+        s = (uint32_t)kp[a.kw];
     }
-    const Key<KWM> key = kload<KWM>(rec, a.kw);
+    if (s > a.end) return;  // after the search's last child (its sslot stays SEEN)
+    const Key<KWM> key = kload<KWM>(kp, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
     const uint32_t fp = (uint32_t)(h >> 32);
     uint64_t idx = h & a.mask;
-    const uint64_t my = CHUNK | ((uint64_t)s << 32) | fp;
+    const uint64_t my = CHUNK | ((uint64_t)s << SEQ_SHIFT) | ((uint64_t)r << REC_SHIFT) | (fp & 0xffffu);
     uint32_t res = SEEN;
     for (uint64_t it = 0;; ++it) {
         if (it > a.mask) {
@@ -339,43 +366,37 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
             }
             v = old;
         }
-        if ((uint32_t)v == fp) {
-            const uint32_t hi = (uint32_t)(v >> 32);
-            if (v & CHUNK) {
-                const uint32_t i2 = a.map[hi & 0x7fffffffu];
-                if (keq<KWM>(a.recv + (int64_t)i2 * rw, key, a.kw)) {
-                    atomicMin((unsigned long long*)(a.table + idx), (unsigned long long)my);
+        if (v & CHUNK) {
+            if ((uint32_t)(v & 0xffffu) == (fp & 0xffffu) && keq<KWM>(rec_key(a, entry_rec(v)), key, a.kw)) {
+                const uint64_t old = atomicMin((unsigned long long*)(a.table + idx), (unsigned long long)my);
+                if (old > my) {  // this child is the first occurrence so far: the previous holder lost
+                    a.lost[entry_seq(old)] = 1;
                     res = (uint32_t)idx;
-                    break;
                 }
-            } else if (keq<KWM>(a.lkeys + (int64_t)(hi - 1) * a.kw, key, a.kw)) {
-                break;  // already a node
+                break;
             }
+        } else if ((uint32_t)v == fp && keq<KWM>(a.lkeys + (int64_t)((v >> 32) - 1) * a.kw, key, a.kw)) {
+            break;  // already a node
         }
         idx = (idx + 1) & a.mask;
     }
-    a.rslot[i] = res;
+    a.sslot[s] = res;
+    a.sfp[s] = fp;
 }
 
-// (3c) survivors (the slot still holds their own seq) -> mask bits
-__global__ __launch_bounds__(TPB) void sbfs_mark_kernel(Args a) {
-    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i >= a.nrecv) return;
-    const uint32_t si = a.rslot[i];
-    if (si == SEEN) return;
-    const uint32_t s = (uint32_t)a.recv[i * (a.kw + 1) + a.kw];
-    if ((a.table[si] >> 32) == ((CHUNK >> 32) | s)) atomicOr(&a.gmask[s / 12u], 1u << (s % 12u));
-}
-
-// bits of m whose child this rank received (hence owns, if it survived)
-__device__ __forceinline__ uint32_t own_bits(const Args& a, uint32_t p, uint32_t m) {
-    uint32_t r = 0, mm = m;
-    while (mm) {
-        const int act = __builtin_ctz(mm);
-        mm &= mm - 1;
-        if (a.map[p * 12u + act] != NONE) r |= 1u << act;
+// (3b) this rank's survivors per parent -> mask bits (gmask, all-reduced next; mine, kept):
+// a child survives if it holds its entry and was not displaced by a smaller seq
+__global__ __launch_bounds__(TPB) void sbfs_mask_kernel(Args a) {
+    const int p = blockIdx.x * TPB + threadIdx.x;
+    if (p >= a.P) return;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int act = 0; act < 12; ++act) {
+        const uint32_t s = (uint32_t)p * 12u + (uint32_t)act;
+        if (a.sslot[s] != SEEN && !a.lost[s]) bits |= 1u << act;
     }
-    return r;
+    a.gmask[p] = bits;
+    a.mine[p] = bits;
 }
 
 // (4a) per-block counts of all survivors and of this rank's
@@ -383,7 +404,7 @@ __global__ __launch_bounds__(TPB) void sbfs_count_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
     const int p = blockIdx.x * TPB + threadIdx.x;
     const uint32_t m = p < a.P ? a.gmask[p] : 0u;
-    const uint32_t mine = p < a.P ? own_bits(a, (uint32_t)p, m) : 0u;
+    const uint32_t mine = p < a.P ? a.mine[p] : 0u;
     uint32_t tot, ltot;
     block_excl_scan(__popc(m), sh, tot);
     __syncthreads();
@@ -432,11 +453,11 @@ __global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, int nb, ui
 constexpr int CMAX = TPB * 12;  // own survivors a block can stage
 __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
-    __shared__ uint32_t srec[CMAX];  // received-record index of the k-th own survivor
+    __shared__ uint32_t srec[CMAX];  // record of the k-th own survivor (rec_key)
     __shared__ uint32_t sinf[CMAX];  // parent within the block (8 bits) | move (4) | id offset (12)
     const int p = blockIdx.x * TPB + threadIdx.x;
     const uint32_t m = p < a.P ? a.gmask[p] : 0u;
-    const uint32_t mine = p < a.P ? own_bits(a, (uint32_t)p, m) : 0u;
+    const uint32_t mine = p < a.P ? a.mine[p] : 0u;
     uint32_t tot;
     const uint32_t bex = block_excl_scan(__popc(m), sh, tot);  // survivors of the block before p
     const int64_t base = (int64_t)a.bsum[blockIdx.x] + bex;
@@ -454,7 +475,7 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     while (mm) {
         const int act = __builtin_ctz(mm);
         mm &= mm - 1;
-        srec[k] = a.map[(uint32_t)p * 12u + act];
+        srec[k] = entry_rec(a.table[a.sslot[(uint32_t)p * 12u + act]]);  // still the chunk entry
         sinf[k] = (uint32_t)threadIdx.x << 16 | (uint32_t)act << 12 | (bex + __popc(m & ((1u << act) - 1u)));
         ++k;
     }
@@ -464,7 +485,8 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     const int64_t g0 = a.n_before + (int64_t)a.bsum[blockIdx.x];  // id of the block's first survivor
     const int64_t keep_below = a.n_before + a.need + 12;
     const int64_t li0 = a.nloc + (int64_t)a.lbsum[blockIdx.x];
-    const int rw = a.kw + 1;
+    // every block has read its survivors' chunk entries before any entry becomes a node entry
+    // below (a slot has one survivor: no block reads another block's slot)
     uint32_t stored = 0;
     for (uint32_t i = threadIdx.x; i < ltot; i += TPB) {
         const uint32_t inf = sinf[i];
@@ -476,19 +498,20 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
             continue;
         }
         ++stored;
+        const int64_t pp = (int64_t)blockIdx.x * TPB + (inf >> 16);
+        const uint32_t act = (inf >> 12) & 0xfu;
         a.lgid[li] = gid;
-        a.lpar[li] = a.head + (int64_t)blockIdx.x * TPB + (inf >> 16);
-        a.lact[li] = (uint8_t)((inf >> 12) & 0xfu);
-        const uint32_t r = srec[i];
-        const uint32_t si = a.rslot[r];
-        a.table[si] = ((uint64_t)(li + 1) << 32) | (uint32_t)a.table[si];
+        a.lpar[li] = a.head + pp;
+        a.lact[li] = (uint8_t)act;
+        const uint32_t sq = (uint32_t)pp * 12u + act;
+        a.table[a.sslot[sq]] = ((uint64_t)(li + 1) << 32) | a.sfp[sq];
     }
     // keys: word w of the block's slot range comes from word w % kw of record srec[w / kw]
     for (uint32_t w = threadIdx.x; w < ltot * (uint32_t)a.kw; w += TPB) {
         const uint32_t i = w / (uint32_t)a.kw, c = w - i * (uint32_t)a.kw;
         const int64_t li = li0 + i;
         if (g0 + (sinf[i] & 0xfffu) >= keep_below || li >= a.lcap) continue;
-        a.lkeys[li * a.kw + c] = a.recv[(int64_t)srec[i] * rw + c];
+        a.lkeys[li * a.kw + c] = rec_key(a, srec[i])[c];
     }
     uint32_t bs;
     block_excl_scan(stored, sh, bs);
@@ -629,8 +652,8 @@ struct Shard {
     int64_t* look_host = nullptr;
 
     ~Shard() {
-        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.map,
-                        a.rslot, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
+        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.sslot, a.sfp,
+                        a.lost, a.mine, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
@@ -655,7 +678,7 @@ struct InsertLaunch {
     Shard* S;
     hipStream_t st;
     template <int NW>
-    void go() { sbfs_insert_kernel<NW + 1><<<dim3(nblocks(S->nrecv)), dim3(TPB), 0, st>>>(S->a); }
+    void go() { sbfs_insert_kernel<NW + 1><<<dim3(nblocks(12 * (int64_t)S->Pr + S->nrecv)), dim3(TPB), 0, st>>>(S->a); }
 };
 struct RootLaunch {
     Shard* S;
@@ -713,8 +736,8 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     S->rank = rank;
     S->world = world;
     S->lcap = local_cap;
-    if (chunk_parents <= 0) chunk_parents = 1 << 19;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
-    if (chunk_parents > (1 << 24)) { delete S; return nullptr; }
+    if (chunk_parents <= 0) chunk_parents = MAX_CHUNK;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
+    if (chunk_parents > MAX_CHUNK) { delete S; return nullptr; }  // the chunk entry's seq / record fields
     S->pmax = chunk_parents;
     S->rcap = 12 * S->pmax;  // every child of a chunk may have this owner
     uint64_t ts = 1024;
@@ -727,7 +750,9 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     bool ok = dalloc(a.lkeys, (size_t)(S->lcap * S->kw)) && dalloc(a.lgid, (size_t)S->lcap) &&
               dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
               dalloc(a.ckeys, (size_t)(12 * pl * S->kw)) && dalloc(a.cown, (size_t)(12 * pl)) &&
-              dalloc(a.pmin, (size_t)pl) && dalloc(a.map, (size_t)S->rcap) && dalloc(a.rslot, (size_t)S->rcap) &&
+              dalloc(a.pmin, (size_t)pl) && dalloc(a.sslot, (size_t)(12 * S->pmax)) &&
+              dalloc(a.sfp, (size_t)(12 * S->pmax)) && dalloc(a.lost, (size_t)(12 * S->pmax)) &&
+              dalloc(a.mine, (size_t)S->pmax) &&
               dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
               dalloc(a.xblk, (size_t)((pl + STILE - 1) / STILE + 1) * (2 + world)) &&
@@ -744,6 +769,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     a.kw = S->kw;
     a.cyc = S->cyc;
     a.world = world;
+    a.rank = rank;
     return S;
 }
 
@@ -821,14 +847,16 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream
 int acx_sbfs_pack(void* h, uint64_t* send, void* stream) {
     Shard* S = static_cast<Shard*>(h);
     if (!S || !send) return ACX_E_ARG;
-    if (S->Pr == 0) return ACX_OK;
+    uint64_t nsend = 0;  // the counts acx_sbfs_expand read back (the rank's own group is empty)
+    for (int o = 0; o < S->world; ++o) nsend += S->ctl_host->cnt[o];
+    if (S->Pr == 0 || nsend == 0) return ACX_OK;
     S->a.send = send;
     sbfs_pack_kernel<<<dim3((unsigned)((S->Pr + STILE - 1) / STILE)), dim3(TPB), 0, (hipStream_t)stream>>>(S->a);
     return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 
-// received records ((nrecv, kw + 1) uint64) -> probe / insert; this rank's survivors as bits
-// of gmask ((P) int32, zeroed here).  end = min(success seq, move-error seq) over all ranks.
+// this rank's own children (in place) and the received records ((nrecv, kw + 1) uint64) ->
+// probe / insert; this rank's survivors as bits of gmask ((P) int32, written here).  end = min(success seq, move-error seq) over all ranks.
 int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, uint32_t* gmask, void* stream) {
     Shard* S = static_cast<Shard*>(h);
     if (!S || !gmask || nrecv < 0 || nrecv > S->rcap || (nrecv > 0 && !recv)) return ACX_E_ARG;
@@ -839,14 +867,13 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
     a.gmask = gmask;
     a.end = end < 0 || end > (int64_t)NONE ? NONE : (uint32_t)end;
     S->nrecv = nrecv;
-    if (hipMemsetAsync(a.map, 0xff, (size_t)12 * S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;
-    if (hipMemsetAsync(gmask, 0, (size_t)S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;
-    if (nrecv > 0) {
-        sbfs_map_kernel<<<dim3(nblocks(nrecv)), dim3(TPB), 0, st>>>(a);
+    if (hipMemsetAsync(a.sslot, 0xff, (size_t)12 * S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;  // SEEN
+    if (hipMemsetAsync(a.lost, 0, (size_t)12 * S->P, st) != hipSuccess) return ACX_E_LAUNCH;
+    if (12 * (int64_t)S->Pr + nrecv > 0) {
         InsertLaunch il{S, st};
         by_nw(S->L, il);
-        sbfs_mark_kernel<<<dim3(nblocks(nrecv)), dim3(TPB), 0, st>>>(a);
     }
+    sbfs_mask_kernel<<<dim3(nblocks(S->P)), dim3(TPB), 0, st>>>(a);
     return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 

@@ -302,17 +302,20 @@ int64_t acx_bfs_min_trace(void* h, int32_t* out, int64_t cap);
  * reference bfs (breadth_first.py:15-97).  The caller runs the same chunk loop on every rank
  * (acx/search/_sharded_bfs.py) and does the exchanges between the calls:
  *   acx_sbfs_create    workspace on the current device: this rank's node store (local_cap
- *                      nodes), chunks of <= chunk_parents parents (<= 0: 2^19); NULL on failure
+ *                      nodes), chunks of <= chunk_parents parents (<= 0 or the maximum: 2^19);
+ *                      NULL on failure
  *   acx_sbfs_owner     owner rank of a presentation's key (HOST pointer)
  *   acx_sbfs_reset     new search from `presentation` (HOST); returns the root's owner rank
  *   acx_sbfs_expand    expands this rank's parents among global ids [head, head + P);
  *                      out int64[5 + world] = success seq, move-error seq (0xffffffff: none),
  *                      min child total, local parents, overflow, children per owner
- *   acx_sbfs_pack      those children into `send` ((n, kw + 1) uint64: key words, chunk seq),
- *                      grouped by owner in rank order
+ *   acx_sbfs_pack      the children other ranks own into `send` ((n, kw + 1) uint64: key
+ *                      words, chunk seq), grouped by owner in rank order (the count for the
+ *                      rank itself is 0: its own children are inserted in place)
  *   -- all_to_all of the records: recv holds the records every rank sent to this one --
- *   acx_sbfs_insert    probe / claim the visited set with the received records up to seq
- *                      `end`; survivors as bits of gmask ((P) uint32, zeroed by the call)
+ *   acx_sbfs_insert    probe / claim the visited set with this rank's own children and the
+ *                      received records, up to seq `end`; survivors as bits of gmask ((P)
+ *                      uint32, written by the call)
  *   -- all_reduce (sum) of gmask over the ranks --
  *   acx_sbfs_commit    global ids, the node-budget cut and the appends; out int64[5] = nodes
  *                      appended (all ranks), cut parent (-1: none), nodes after the cut
