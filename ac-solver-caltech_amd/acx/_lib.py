@@ -76,7 +76,7 @@ SIGNATURES = {
     "acx_bfs_create": ([_I32, _I64, _I64, _I32], ctypes.c_void_p),
     "acx_bfs_run": ([_P, _P, _I64, _P, _P, _I64, _P, _P], ctypes.c_int),
     "acx_bfs_destroy": ([_P], None),
-    "acx_bfs_node_keys": ([_P, _P, _I64], ctypes.c_int64),
+    "acx_bfs_node_keys": ([_P, _P, _I64, _P], ctypes.c_int64),
     "acx_bfs_min_trace": ([_P, _P, _I64], ctypes.c_int64),
     # owner-partitioned multi-GPU BFS (ac-solver-caltech_amd/csrc/acx_sbfs.hip)
     "acx_sbfs_create": ([_I32, _I64, _I64, _I32, _I32, _I32], ctypes.c_void_p),
@@ -91,7 +91,7 @@ SIGNATURES = {
     "acx_sbfs_min_len": ([_P, _I64, _P], ctypes.c_int64),
     "acx_sbfs_lookup": ([_P, _I64, _P, _P], ctypes.c_int),
     "acx_sbfs_trace": ([_P, _I64, _I64, _P, _I64, _P], ctypes.c_int64),
-    "acx_sbfs_node_keys": ([_P, _P, _P, _I64], ctypes.c_int64),
+    "acx_sbfs_node_keys": ([_P, _P, _P, _I64, _P], ctypes.c_int64),
 }
 
 _lib = None

@@ -77,10 +77,13 @@ def device_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclical
     LAST_STATS.update(nodes=int(stats[0]), parents=int(stats[1]), chunks=int(stats[2]), min_length=int(stats[3]),
                       status=int(st))
     if keep_node_keys:
-        n = lib.acx_bfs_node_keys(h, None, 0)
+        n = lib.acx_bfs_node_keys(h, None, 0, stream)
         nk = np.zeros((max(n, 0), _lib.key_words(L)), np.uint64)
         if n > 0:
-            lib.acx_bfs_node_keys(h, nk.ctypes.data, n)
+            with torch.cuda.device(dev):
+                r = lib.acx_bfs_node_keys(h, nk.ctypes.data, n, stream)
+            if r < 0:
+                _lib.check(r, "acx_bfs_node_keys")
         LAST_STATS["node_keys"] = nk
     ntr = lib.acx_bfs_min_trace(h, None, 0)
     trace = np.zeros(max(ntr, 1), np.int32)

@@ -286,11 +286,14 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
                       status=int(status), rank=comm.rank, world=W,
                       exchange="local" if comm.local else "device" if comm.device_collectives else "host")
     if keep_node_keys:
-        n = lib.acx_sbfs_node_keys(h, None, None, 0)
+        n = lib.acx_sbfs_node_keys(h, None, None, 0, stream)
         nk = np.zeros((max(n, 0), kw), np.uint64)
         ng = np.zeros(max(n, 0), np.int64)
         if n > 0:
-            lib.acx_sbfs_node_keys(h, nk.ctypes.data, ng.ctypes.data, n)
+            with torch.cuda.device(dev):
+                r = lib.acx_sbfs_node_keys(h, nk.ctypes.data, ng.ctypes.data, n, stream)
+            if r < 0:
+                _lib.check(r, "acx_sbfs_node_keys")
         LAST_STATS["node_keys"], LAST_STATS["node_ids"] = nk, ng
     LAST_STATS["min_trace"] = list(trace_lines)
     if verbose and comm.rank == 0:

@@ -747,13 +747,17 @@ struct Search {
     int32_t* path_dev = nullptr;    // pinned, coherent host memory: bfs_path_kernel writes the path
     int64_t* path_n_dev = nullptr;  // there directly (no device-to-host copy)
     std::vector<int32_t> trace;  // new minima of the last run, in order
+    uint64_t* gather = nullptr;  // acx_bfs_node_keys: the keys in FIFO order (grown on demand)
+    int64_t gather_cap = 0;
+    void* bounce = nullptr;      // pinned (copy_to_host)
 
     ~Search() {
         if (fin_pending) (void)hipEventSynchronize(fin);
         void* ptrs[] = {a.store, a.queue, a.cand, a.lost, a.pmin, a.tsum, a.tmin, a.table, a.ctl, a.trace, a.live};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
-        void* hptrs[] = {mirror, trace_host, path_dev, path_n_dev};
+        if (gather) (void)hipFree(gather);
+        void* hptrs[] = {mirror, trace_host, path_dev, path_n_dev, bounce};
         for (void* p : hptrs)
             if (p) (void)hipHostFree(p);
         if (fin) (void)hipEventDestroy(fin);
@@ -1024,23 +1028,23 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
     return status;
 }
 
-int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap) {
+int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap, void* stream) {
     Search* S = static_cast<Search*>(h);
     if (!S) return ACX_E_ARG;
     const int64_t n = S->last_nodes < cap ? S->last_nodes : cap;
     if (out && n > 0) {
-        uint64_t* tmp = nullptr;
-        if (hipMalloc((void**)&tmp, (size_t)(n * S->kw) * 8) != hipSuccess) return ACX_E_LAUNCH;
-        hipStream_t st = nullptr;
-        bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-        if (ok) {
-            bfs_gather_kernel<<<dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(S->a, n, tmp);
-            ok = hipGetLastError() == hipSuccess &&
-                 copy_to_host(out, tmp, (size_t)(n * S->kw) * 8, st) == ACX_OK;
-            (void)hipStreamDestroy(st);
+        hipStream_t st = (hipStream_t)stream;
+        if (n > S->gather_cap) {
+            if (S->gather && hipFree(S->gather) != hipSuccess) return ACX_E_LAUNCH;
+            S->gather = nullptr;
+            S->gather_cap = 0;
+            if (hipMalloc((void**)&S->gather, (size_t)(n * S->kw) * 8) != hipSuccess) return ACX_E_LAUNCH;
+            S->gather_cap = n;
         }
-        (void)hipFree(tmp);
-        if (!ok) return ACX_E_LAUNCH;
+        bfs_gather_kernel<<<dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, st>>>(S->a, n, S->gather);
+        if (hipGetLastError() != hipSuccess ||
+            copy_to_host(out, S->gather, (size_t)(n * S->kw) * 8, st, &S->bounce) != ACX_OK)
+            return ACX_E_LAUNCH;
     }
     return S->last_nodes;
 }

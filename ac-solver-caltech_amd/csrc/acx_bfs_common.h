@@ -58,25 +58,25 @@ __host__ __device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
     return fmix64(h);
 }
 
-// device -> pageable host memory through a pinned bounce buffer on `st` (no hipMemcpy into
-// pageable memory: its staged path is a copy whose completion the runtime's tracing never sees)
-static inline int copy_to_host(void* dst, const void* src, size_t n, hipStream_t st) {
-    constexpr size_t BOUNCE = 16u << 20;
-    void* pin = nullptr;
-    const size_t nb = n < BOUNCE ? n : BOUNCE;
-    if (nb == 0) return ACX_OK;
-    if (hipHostMalloc(&pin, nb, hipHostMallocDefault) != hipSuccess) return ACX_E_LAUNCH;
-    int rc = ACX_OK;
-    for (size_t off = 0; off < n && rc == ACX_OK; off += nb) {
-        const size_t m = n - off < nb ? n - off : nb;
-        if (hipMemcpyAsync(pin, (const char*)src + off, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            rc = ACX_E_LAUNCH;
-        else
-            memcpy((char*)dst + off, pin, m);
+// device -> pageable host memory on the caller's stream, through a pinned bounce buffer the
+// workspace keeps (*pin, allocated on first use, BOUNCE bytes; freed with the workspace): no
+// hipMemcpy on the null stream, no pageable destination, nothing freed while a copy may be
+// in flight
+constexpr size_t BOUNCE = 16u << 20;
+static inline int copy_to_host(void* dst, const void* src, size_t n, hipStream_t st, void** pin) {
+    if (n == 0) return ACX_OK;
+    if (!*pin && hipHostMalloc(pin, BOUNCE, hipHostMallocDefault) != hipSuccess) {
+        *pin = nullptr;
+        return ACX_E_LAUNCH;
     }
-    (void)hipHostFree(pin);
-    return rc;
+    for (size_t off = 0; off < n; off += BOUNCE) {
+        const size_t m = n - off < BOUNCE ? n - off : BOUNCE;
+        if (hipMemcpyAsync(*pin, (const char*)src + off, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return ACX_E_LAUNCH;
+        memcpy((char*)dst + off, *pin, m);
+    }
+    return ACX_OK;
 }
 
 // LDS written by the wave's lanes is visible to the whole wave after this

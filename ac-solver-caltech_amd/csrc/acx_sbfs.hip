@@ -71,7 +71,7 @@ struct Args {
     uint16_t* pmin;   // (Pr) min child total per local parent (totals reach 2L = 256)
     uint32_t* sslot;  // (12 P) per chunk seq: table slot its child claimed / joined as the first
                       // occurrence, SEEN if none (a known state, past the end, or not owned here)
-    uint32_t* sfp;    // (12 P) per chunk seq: the child's 32-bit fingerprint
+    uint64_t* srf;    // (12 P) per chunk seq: the child's record << 32 | its 32-bit fingerprint
     uint8_t* lost;    // (12 P) per chunk seq: a smaller seq of the same state took its entry
     uint32_t* mine;   // (P) this rank's survivors per parent (bits by action)
     uint32_t* bsum;   // (nb) all survivors per block of parents -> exclusive offsets
@@ -330,15 +330,19 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
 // marked lost
 template <int KWM>
 __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 waves/SIMD (latency-bound)
-    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
     const int64_t n_own = 12 * (int64_t)a.Pr;
-    if (r >= n_own + a.nrecv) return;
+    if (t >= n_own + a.nrecv) return;
     uint32_t s;
+    int64_t r = t;  // the record
     const uint64_t* kp;
-    if (r < n_own) {
+    if (t < n_own) {
+        // own children, lanes in (parent, action) order: consecutive lanes write consecutive seqs
+        // (sslot, srf); their keys come from 12 action rows of ckeys, a few parents each
+        const int j = (int)(t / 12);
+        const int act = (int)(t - 12 * (int64_t)j);
+        r = (int64_t)act * a.Pr + j;
         if (a.cown[r] != (uint8_t)a.rank) return;  // another rank's child, or a parent past the chunk
-        const int act = (int)(r / a.Pr);
-        const int j = (int)(r - (int64_t)act * a.Pr);
         s = (uint32_t)(a.lgid[a.lo + j] - a.head) * 12u + (uint32_t)act;
         kp = a.ckeys + r * a.kw;
     } else {
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
         idx = (idx + 1) & a.mask;
     }
     a.sslot[s] = res;
-    a.sfp[s] = fp;
+    a.srf[s] = (uint64_t)r << 32 | fp;
 }
 
 // (3b) this rank's survivors per parent -> mask bits (gmask, all-reduced next; mine, kept):
@@ -475,7 +479,7 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     while (mm) {
         const int act = __builtin_ctz(mm);
         mm &= mm - 1;
-        srec[k] = entry_rec(a.table[a.sslot[(uint32_t)p * 12u + act]]);  // still the chunk entry
+        srec[k] = (uint32_t)(a.srf[(uint32_t)p * 12u + act] >> 32);
         sinf[k] = (uint32_t)threadIdx.x << 16 | (uint32_t)act << 12 | (bex + __popc(m & ((1u << act) - 1u)));
         ++k;
     }
@@ -485,8 +489,6 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     const int64_t g0 = a.n_before + (int64_t)a.bsum[blockIdx.x];  // id of the block's first survivor
     const int64_t keep_below = a.n_before + a.need + 12;
     const int64_t li0 = a.nloc + (int64_t)a.lbsum[blockIdx.x];
-    // every block has read its survivors' chunk entries before any entry becomes a node entry
-    // below (a slot has one survivor: no block reads another block's slot)
     uint32_t stored = 0;
     for (uint32_t i = threadIdx.x; i < ltot; i += TPB) {
         const uint32_t inf = sinf[i];
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
         a.lpar[li] = a.head + pp;
         a.lact[li] = (uint8_t)act;
         const uint32_t sq = (uint32_t)pp * 12u + act;
-        a.table[a.sslot[sq]] = ((uint64_t)(li + 1) << 32) | a.sfp[sq];
+        a.table[a.sslot[sq]] = ((uint64_t)(li + 1) << 32) | (uint32_t)a.srf[sq];
     }
     // keys: word w of the block's slot range comes from word w % kw of record srec[w / kw]
     for (uint32_t w = threadIdx.x; w < ltot * (uint32_t)a.kw; w += TPB) {
@@ -650,14 +652,16 @@ struct Shard {
     Args a{};
     Ctl* ctl_host = nullptr;
     int64_t* look_host = nullptr;
+    void* bounce = nullptr;  // pinned (copy_to_host)
 
     ~Shard() {
-        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.sslot, a.sfp,
+        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.sslot, a.srf,
                         a.lost, a.mine, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
         if (look_host) (void)hipHostFree(look_host);
+        if (bounce) (void)hipHostFree(bounce);
     }
 };
 
@@ -751,7 +755,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
               dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
               dalloc(a.ckeys, (size_t)(12 * pl * S->kw)) && dalloc(a.cown, (size_t)(12 * pl)) &&
               dalloc(a.pmin, (size_t)pl) && dalloc(a.sslot, (size_t)(12 * S->pmax)) &&
-              dalloc(a.sfp, (size_t)(12 * S->pmax)) && dalloc(a.lost, (size_t)(12 * S->pmax)) &&
+              dalloc(a.srf, (size_t)(12 * S->pmax)) && dalloc(a.lost, (size_t)(12 * S->pmax)) &&
               dalloc(a.mine, (size_t)S->pmax) &&
               dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
@@ -945,10 +949,11 @@ int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int6
     sbfs_trace_kernel<<<dim3(1), dim3(1024), 0, st>>>(a, npar, run, e, d_out, d_n);
     int32_t n = 0;
     int64_t res = ACX_E_LAUNCH;
-    if (hipGetLastError() == hipSuccess && copy_to_host(&n, d_n, 4, st) == ACX_OK) {
+    if (hipGetLastError() == hipSuccess && copy_to_host(&n, d_n, 4, st, &S->bounce) == ACX_OK) {
         const int64_t m = n < cap ? n : cap;
         const int64_t mm = m < TRACE_MAX ? m : TRACE_MAX;
-        if (mm == 0 || copy_to_host(out, d_out, (size_t)(2 * mm) * sizeof(int64_t), st) == ACX_OK) res = n;
+        if (mm == 0 || copy_to_host(out, d_out, (size_t)(2 * mm) * sizeof(int64_t), st, &S->bounce) == ACX_OK)
+            res = n;
     }
     (void)hipFree(d_out);
     (void)hipFree(d_n);
@@ -971,19 +976,15 @@ int acx_sbfs_lookup(void* h, int64_t g, int64_t* out, void* stream) {
 }
 
 // this rank's stored nodes: keys (cap, kw) and global ids (cap), ascending id; returns the count
-int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap) {
+int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap, void* stream) {
     Shard* S = static_cast<Shard*>(h);
     if (!S) return ACX_E_ARG;
     const int64_t n = S->nloc < cap ? S->nloc : cap;
-    if (n > 0 && (keys || gids)) {
-        hipStream_t st = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ACX_E_LAUNCH;
-        // the search's stream is idle here (every acx_sbfs_* call that enqueues work waits)
-        const bool ok = (!keys || copy_to_host(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, st) == ACX_OK) &&
-                        (!gids || copy_to_host(gids, S->a.lgid, (size_t)n * 8, st) == ACX_OK);
-        (void)hipStreamDestroy(st);
-        if (!ok) return ACX_E_LAUNCH;
-    }
+    hipStream_t st = (hipStream_t)stream;
+    if (n > 0 && keys && copy_to_host(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, st, &S->bounce) != ACX_OK)
+        return ACX_E_LAUNCH;
+    if (n > 0 && gids && copy_to_host(gids, S->a.lgid, (size_t)n * 8, st, &S->bounce) != ACX_OK)
+        return ACX_E_LAUNCH;
     return S->nloc;
 }
 

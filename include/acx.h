@@ -290,7 +290,7 @@ int acx_bfs_run(void* h, const int32_t* presentation, int64_t max_nodes, int32_t
 void acx_bfs_destroy(void* h);
 /* packed keys (acx.h key format) of the first min(cap, n) nodes of the last run in discovery
    (FIFO) order, n = nodes held (<= max_nodes + 12); returns n */
-int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap);
+int64_t acx_bfs_node_keys(void* h, uint64_t* out, int64_t cap, void* stream);
 /* the new minimal total lengths of the last run in the order the reference finds them (its
    verbose "New minimal length found: m" lines, breadth_first.py:79-82): writes the first cap,
    returns how many there are */
@@ -343,7 +343,7 @@ int acx_sbfs_lookup(void* h, int64_t g, int64_t* out, void* stream);
  * rank, as (seq, total) int64 pairs into out (HOST, 2 * cap); returns their count.  The caller
  * merges every rank's records in seq order to print the reference's new-minimum lines. */
 int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int64_t cap, void* stream);
-int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap);
+int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap, void* stream);
 
 /*
  * Scoring inputs for value-guided search (value_search/): exactly one of `states` ((M,2L) int32)
