@@ -58,6 +58,15 @@ __host__ __device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
     return fmix64(h);
 }
 
+// n bytes (n % 4 == 0) device -> pinned host memory by a kernel (no DMA-engine copy: rocprofv3's
+// memory-copy tracing never receives the completion of a device-to-host engine copy on this
+// stack -- profiles/r04/bfs_trace_c: one undelivered callback per copy -- so the exports below
+// write host memory from a kernel instead)
+static __global__ void d2h_copy_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 // device -> pageable host memory on the caller's stream, through a pinned bounce buffer the
 // workspace keeps (*pin, allocated on first use, BOUNCE bytes; freed with the workspace): no
 // hipMemcpy on the null stream, no pageable destination, nothing freed while a copy may be
@@ -65,15 +74,16 @@ __host__ __device__ __forceinline__ uint64_t khash(const Key<KWM>& k, int kw) {
 constexpr size_t BOUNCE = 16u << 20;
 static inline int copy_to_host(void* dst, const void* src, size_t n, hipStream_t st, void** pin) {
     if (n == 0) return ACX_OK;
+    if (n % 4) return ACX_E_ARG;
     if (!*pin && hipHostMalloc(pin, BOUNCE, hipHostMallocDefault) != hipSuccess) {
         *pin = nullptr;
         return ACX_E_LAUNCH;
     }
     for (size_t off = 0; off < n; off += BOUNCE) {
         const size_t m = n - off < BOUNCE ? n - off : BOUNCE;
-        if (hipMemcpyAsync(*pin, (const char*)src + off, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return ACX_E_LAUNCH;
+        d2h_copy_kernel<<<dim3(1024), dim3(256), 0, st>>>(static_cast<uint32_t*>(*pin),
+                                                           reinterpret_cast<const uint32_t*>((const char*)src + off), m / 4);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
         memcpy((char*)dst + off, *pin, m);
     }
     return ACX_OK;

@@ -33,6 +33,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
 
 #include "acx.h"
@@ -643,6 +644,11 @@ __global__ void sbfs_root_kernel(Args a, RootKey rk) {
     a.lact[0] = 0xff;
 }
 
+struct Pub {
+    Ctl c;
+    uint64_t seq;  // the read-back number once c holds that read-back's control block
+};
+
 struct Shard {
     int dev = 0, L = 0, kw = 0, cyc = 0, rank = 0, world = 1;
     int64_t lcap = 0, pmax = 0, rcap = 0, nloc = 0, lo = 0;
@@ -650,7 +656,9 @@ struct Shard {
     int64_t head = 0, nrecv = 0;
     uint64_t tsize = 0;
     Args a{};
-    Ctl* ctl_host = nullptr;
+    Ctl* ctl_host = nullptr;  // the last read-back (host copy)
+    Pub* pub = nullptr;       // pinned, coherent: sbfs_publish_kernel writes it
+    uint64_t pub_seq = 0;
     int64_t* look_host = nullptr;
     void* bounce = nullptr;  // pinned (copy_to_host)
 
@@ -659,7 +667,8 @@ struct Shard {
                         a.lost, a.mine, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
-        if (ctl_host) (void)hipHostFree(ctl_host);
+        delete ctl_host;
+        if (pub) (void)hipHostFree(pub);
         if (look_host) (void)hipHostFree(look_host);
         if (bounce) (void)hipHostFree(bounce);
     }
@@ -708,16 +717,42 @@ struct LookupLaunch {
     void go() { sbfs_lookup_kernel<NW><<<dim3(1), dim3(64), 0, st>>>(S->a, g); }
 };
 
+// the control block published to pinned, coherent host memory by a one-wave kernel (the
+// sequence number written last, system scope) -- a hipMemcpyAsync of it was a ~9 us blit per
+// read-back, two per chunk -- and read by the host's poll
+__global__ void sbfs_publish_kernel(const Ctl* c, Pub* host, uint64_t seq) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(c);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&host->c);
+    for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += WAVE) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&host->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// every read-back: publish, then poll the sequence number (hipStreamSynchronize may sleep and
+// wake late; two waits per chunk are on the search's critical path).  Every 4096 polls the
+// stream is queried (a failed launch), and a control block not published within 30 s (a kernel
+// that does not finish) is an error.
 static int sync_ctl(Shard* S, hipStream_t st) {
     if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
-    if (hipMemcpyAsync(S->ctl_host, S->a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st) != hipSuccess)
-        return ACX_E_LAUNCH;
-    // poll: hipStreamSynchronize may sleep and wake late, and two waits per chunk are on the
-    // search's critical path
-    hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    const uint64_t want = ++S->pub_seq;
+    sbfs_publish_kernel<<<dim3(1), dim3(WAVE), 0, st>>>(S->a.ctl, S->pub, want);
+    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(&S->pub->seq, __ATOMIC_ACQUIRE) == want) break;
+        if ((it & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {  // idle: the slot is final now
+                if (__atomic_load_n(&S->pub->seq, __ATOMIC_ACQUIRE) == want) break;
+                return ACX_E_LAUNCH;
+            }
+            if (e != hipErrorNotReady) return ACX_E_LAUNCH;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return ACX_E_LAUNCH;
+        }
     }
-    return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+    memcpy(S->ctl_host, (const void*)&S->pub->c, sizeof(Ctl));
+    return ACX_OK;
 }
 
 }  // namespace sbfs
@@ -760,13 +795,15 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
               dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
               dalloc(a.xblk, (size_t)((pl + STILE - 1) / STILE + 1) * (2 + world)) &&
-              hipHostMalloc((void**)&S->ctl_host, sizeof(Ctl), hipHostMallocDefault) == hipSuccess &&
+              (S->ctl_host = new (std::nothrow) Ctl()) != nullptr &&
+              hipHostMalloc((void**)&S->pub, sizeof(Pub), hipHostMallocCoherent) == hipSuccess &&
               hipHostMalloc((void**)&S->look_host, 4 * sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         delete S;
         return nullptr;
     }
+    memset((void*)S->pub, 0, sizeof(Pub));
     a.mask = ts - 1;
     a.lcap = S->lcap;
     a.L = L;
