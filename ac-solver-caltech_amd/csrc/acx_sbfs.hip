@@ -67,8 +67,8 @@ struct Args {
     int64_t* lgid;    // (lcap) global node id
     int64_t* lpar;    // (lcap) global id of the parent, -1 for the root
     uint8_t* lact;    // (lcap) move id that produced the node
-    uint64_t* ckeys;  // (12, Pr) keys of the local parents' children, action-major
-    uint8_t* cown;    // (12, Pr) owner of each child, 0xff: parent not in the chunk
+    uint64_t* ckeys;  // (Pr, 12) keys of the local parents' children, parent-major (seq order)
+    uint8_t* cown;    // (Pr, 12) owner of each child, 0xff: parent not in the chunk
     uint16_t* pmin;   // (Pr) min child total per local parent (totals reach 2L = 256)
     uint32_t* sslot;  // (12 P) per chunk seq: table slot its child claimed / joined as the first
                       // occurrence, SEEN if none (a known state, past the end, or not owned here)
@@ -94,7 +94,7 @@ struct Args {
 // A child claimed in the running chunk: CHUNK | seq << 40 | record << 16 | 16-bit fingerprint;
 // atomicMin on the whole word keeps the smallest seq -- the reference's first occurrence -- and
 // its record, so a probe compares keys with the entry's own record (no seq -> record map).
-// Records: r < 12 Pr is this rank's own child in ckeys (r = action * Pr + local parent), others
+// Records: r < 12 Pr is this rank's own child in ckeys (r = 12 * local parent + action), others
 // are received records r - 12 Pr.  Chunks are <= 2^19 parents: seq < 12 * 2^19 < 2^23, r < 2^24.
 constexpr int SEQ_SHIFT = 40, REC_SHIFT = 16;
 constexpr int64_t MAX_CHUNK = 1 << 19;
@@ -112,13 +112,21 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
 // (1) block per tile of 64 candidate local parents lo + j (j < Pr = min(P, nloc - lo); the
 // parents of the chunk are the prefix with gid < head + P); wave w makes the children of actions
 // 3w..3w+2 of the same 64 parents (as acx_bfs.hip's bfs_expand_kernel: 4x the lanes of a
-// lane-per-parent loop over 12 serial moves), child keys staged in LDS and written action-major
-// as coalesced runs, owners counted by ballots
+// lane-per-parent loop over 12 serial moves), owners counted by ballots.  The block's 64 x 12
+// child keys and owners are staged in LDS and written parent-major (the chunk's sequence order)
+// as one contiguous run, so the insert and the commit read them in order; for NW > 4 (L > 64,
+// 55 KB of keys per block) each lane writes its children directly
 constexpr int STILE = 64;
 constexpr int SAPW = 12 / (TPB / WAVE);  // actions per wave (3)
 template <int NW>
-__global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void sbfs_expand_kernel(Args a) {
-    __shared__ uint64_t kst[TPB / WAVE][STILE * (NW + 1)];
+struct ExpandStage {
+    static constexpr bool LDS = NW <= 4;
+    static constexpr int WORDS = LDS ? STILE * 12 * (NW + 1) : 1;
+};
+template <int NW>
+__global__ __launch_bounds__(TPB, NW <= 4 ? 6 : 4) void sbfs_expand_kernel(Args a) {
+    __shared__ uint64_t kst[ExpandStage<NW>::WORDS];
+    __shared__ uint8_t cst[STILE * 12];
     __shared__ uint32_t hist[MAXW];
     __shared__ uint32_t smin[STILE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
@@ -141,7 +149,6 @@ __global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void sbfs_expand_kernel(Args 
     uint32_t succ = NONE, err = NONE, mn = 0xffffu;
     uint32_t ownp = 0xffffffu;  // owner byte of action 3w + jj at bits 8 jj (a runtime-indexed
                                 // array here would live in scratch: the loop is not unrolled)
-    uint64_t* st = kst[wid];
     const int nrow = min(STILE, a.Pr - j0);  // the tile's lanes with a local parent slot
 #pragma unroll 1
     for (int jj = 0; jj < SAPW; ++jj) {
@@ -163,17 +170,28 @@ __global__ __launch_bounds__(TPB, NW <= 4 ? 8 : 4) void sbfs_expand_kernel(Args 
             make_key<NW>(a.L, q, key.w);
             own = owner_of(khash<NW + 1>(key, kw), a.world);
             ownp = (ownp & ~(0xffu << (8 * jj))) | (own << (8 * jj));
+            if constexpr (ExpandStage<NW>::LDS) {
 #pragma unroll
-            for (int k = 0; k < NW + 1; ++k)
-                if (k < kw) st[lane * kw + k] = key.w[k];
+                for (int k = 0; k < NW + 1; ++k)
+                    if (k < kw) kst[(lane * 12 + act) * kw + k] = key.w[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < NW + 1; ++k)
+                    if (k < kw) a.ckeys[((int64_t)j * 12 + act) * kw + k] = key.w[k];
+            }
         }
-        wsync();
-        // the tile's keys of this action: one contiguous run (lanes past Pr have no slot; a lane
-        // whose parent is past the chunk writes a stale key its owner byte 0xff tells pack to skip)
-        uint64_t* o = a.ckeys + ((int64_t)act * a.Pr + j0) * kw;
-        for (int i = lane; i < nrow * kw; i += WAVE) o[i] = st[i];
-        if (j < a.Pr) a.cown[(int64_t)act * a.Pr + j] = (uint8_t)own;
-        wsync();
+        // a lane whose parent is past the chunk (or has no slot) leaves a stale key; its owner
+        // byte 0xff tells pack and insert to skip it
+        if constexpr (ExpandStage<NW>::LDS) cst[lane * 12 + act] = (uint8_t)own;
+        else if (j < a.Pr) a.cown[(int64_t)j * 12 + act] = (uint8_t)own;
+    }
+    if constexpr (ExpandStage<NW>::LDS) {
+        __syncthreads();
+        // the block's children in sequence order: one contiguous run of keys and of owners
+        uint64_t* o = a.ckeys + (int64_t)j0 * 12 * kw;
+        for (int i = threadIdx.x; i < nrow * 12 * kw; i += TPB) o[i] = kst[i];
+        uint8_t* oc = a.cown + (int64_t)j0 * 12;
+        for (int i = threadIdx.x; i < nrow * 12; i += TPB) oc[i] = cst[i];
     }
     // per-owner counts: one ballot per (action, owner) and one LDS add per wave
     for (int o = 0; o < a.world; ++o) {
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
 #pragma unroll 1
     for (int jj = 0; jj < SAPW; ++jj) {
         const int act = wid * SAPW + jj;
-        uint32_t o = j < a.Pr ? a.cown[(int64_t)act * a.Pr + j] : 0xffu;
+        uint32_t o = j < a.Pr ? a.cown[(int64_t)j * 12 + act] : 0xffu;
         if (o == (uint32_t)a.rank) o = 0xffu;  // inserted in place, not sent
         uint32_t pos = 0;
         for (uint32_t w = 0; w < (uint32_t)a.world; ++w) {
@@ -318,7 +336,7 @@ __global__ __launch_bounds__(TPB) void sbfs_pack_kernel(Args a) {
             if (o == w) pos = a.ctl->cur[w] + x[w] + b + (uint32_t)__popcll(m & below);
         }
         if (o == 0xffu) continue;
-        const uint64_t* src = a.ckeys + ((int64_t)act * a.Pr + j) * a.kw;
+        const uint64_t* src = a.ckeys + ((int64_t)j * 12 + act) * a.kw;
         uint64_t* dst = a.send + (int64_t)pos * rw;
         for (int k = 0; k < a.kw; ++k) dst[k] = src[k];
         dst[a.kw] = (uint64_t)(p * 12u + (uint32_t)act);
@@ -338,11 +356,10 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
     int64_t r = t;  // the record
     const uint64_t* kp;
     if (t < n_own) {
-        // own children, lanes in (parent, action) order: consecutive lanes write consecutive seqs
-        // (sslot, srf); their keys come from 12 action rows of ckeys, a few parents each
+        // own children in (parent, action) order: consecutive lanes read consecutive keys and
+        // write consecutive seqs (sslot, srf)
         const int j = (int)(t / 12);
         const int act = (int)(t - 12 * (int64_t)j);
-        r = (int64_t)act * a.Pr + j;
         if (a.cown[r] != (uint8_t)a.rank) return;  // another rank's child, or a parent past the chunk
         s = (uint32_t)(a.lgid[a.lo + j] - a.head) * 12u + (uint32_t)act;
         kp = a.ckeys + r * a.kw;
@@ -559,7 +576,7 @@ __global__ __launch_bounds__(1024) void sbfs_trace_kernel(Args a, int npar, uint
     const int per = (npar + 1023) / 1024;
     const int j0 = min(npar, t * per), j1 = min(npar, j0 + per);
     auto child_total = [&](int j, int act) -> uint32_t {
-        return key_total(a.ckeys + ((int64_t)act * a.Pr + j) * a.kw, a.L);
+        return key_total(a.ckeys + ((int64_t)j * 12 + act) * a.kw, a.L);
     };
     auto parent_seq = [&](int j) -> uint32_t { return (uint32_t)(a.lgid[a.lo + j] - a.head) * 12u; };
     uint32_t mn = NONE;
