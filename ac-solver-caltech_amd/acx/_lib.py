@@ -84,7 +84,7 @@ SIGNATURES = {
     "acx_sbfs_max_records": ([_P], ctypes.c_int64),
     "acx_sbfs_owner": ([_P, _I32, _I32], ctypes.c_int32),
     "acx_sbfs_reset": ([_P, _P, _P], ctypes.c_int),
-    "acx_sbfs_expand": ([_P, _I64, _I32, _P, _P], ctypes.c_int),
+    "acx_sbfs_expand": ([_P, _I64, _I32, _P, _I32, _P], ctypes.c_int),
     "acx_sbfs_pack": ([_P, _P, _P], ctypes.c_int),
     "acx_sbfs_insert": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),
     "acx_sbfs_commit": ([_P, _P, _I64, _I64, _P, _P], ctypes.c_int),

@@ -182,7 +182,7 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
     stream = torch.cuda.current_stream(dev).cuda_stream
     W = comm.world
     exp_out = np.zeros(6 + W, np.int64)  # acx_sbfs_expand's 5 + W values, then this rank's failure flag
-    com_out = np.zeros(5, np.int64)
+    com_out = np.zeros(9, np.int64)  # acx_sbfs_commit's 5 values, then the chunk's expansion (4)
     trace_buf = np.zeros(2 * TRACE_CAP, np.int64)
     trace_min = total0  # breadth_first.py:59,79-82: the running minimum the verbose lines follow
     trace_lines = []
@@ -204,32 +204,46 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
         status, succ_node, succ_act = _lib.BFS_EXHAUSTED, -1, -1
         while head < n_nodes:
             P = min(n_nodes - head, chunk)
-            ok(lib.acx_sbfs_expand(h, head, P, exp_out.ctypes.data, stream), "acx_sbfs_expand")
-            exp_out[5 + W] = len(failed)
-            rows = comm.all_gather_rows(exp_out)  # (W, 6 + W)
-            agree(rows[:, 5 + W].sum(), "a C call")
-            if rows[:, 4].any():
-                raise _lib.ACXError("sharded bfs: hash table overflow")
-            succ_seq, err_seq = int(rows[:, 0].min()), int(rows[:, 1].min())
-            chunk_min = int(rows[:, 2].min())
-            send_counts = rows[comm.rank, 5 : 5 + W]
-            recv_counts = rows[:, 5 + comm.rank]
-            nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
-            ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
-            if not comm.local:
-                comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
-                                [int(c) * rw for c in send_counts])
-            src = send if comm.local else recv  # one rank alone: the records it sent are the ones it owns
-            end = min(succ_seq, err_seq)
-            ok(lib.acx_sbfs_insert(h, src.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
-            comm.all_reduce_sum_(gmask[:P])
+            if comm.local:
+                # one rank, nothing to exchange: the chunk runs on one read-back (the commit's); the
+                # insert takes the chunk's first success / move error from the control block
+                ok(lib.acx_sbfs_expand(h, head, P, exp_out.ctypes.data, 0, stream), "acx_sbfs_expand")
+                ok(lib.acx_sbfs_insert(h, send.data_ptr(), 0, -1, gmask.data_ptr(), stream), "acx_sbfs_insert")
+            else:
+                ok(lib.acx_sbfs_expand(h, head, P, exp_out.ctypes.data, 1, stream), "acx_sbfs_expand")
+                exp_out[5 + W] = len(failed)
+                rows = comm.all_gather_rows(exp_out)  # (W, 6 + W)
+                agree(rows[:, 5 + W].sum(), "a C call")
+                if rows[:, 4].any():
+                    raise _lib.ACXError("sharded bfs: hash table overflow")
+                succ_seq, err_seq = int(rows[:, 0].min()), int(rows[:, 1].min())
+                chunk_min = int(rows[:, 2].min())
+                send_counts = rows[comm.rank, 5 : 5 + W]
+                recv_counts = rows[:, 5 + comm.rank]
+                nsend, nrecv = int(send_counts.sum()), int(recv_counts.sum())
+                if rows[:, 5: 5 + W].any():  # the same on every rank: skip an all-empty exchange together
+                    ok(lib.acx_sbfs_pack(h, send.data_ptr(), stream), "acx_sbfs_pack")
+                    comm.all_to_all(recv[:nrecv * rw], send[:nsend * rw], [int(c) * rw for c in recv_counts],
+                                    [int(c) * rw for c in send_counts])
+                end = min(succ_seq, err_seq)
+                ok(lib.acx_sbfs_insert(h, recv.data_ptr(), nrecv, end, gmask.data_ptr(), stream), "acx_sbfs_insert")
+                comm.all_reduce_sum_(gmask[:P])
             ok(lib.acx_sbfs_commit(h, gmask.data_ptr(), n_nodes, max_nodes - n_nodes, com_out.ctypes.data, stream),
                "acx_sbfs_commit")
             chunks += 1
-            st_rows = comm.sum_rows([com_out[4], len(failed)])
-            agree(st_rows[1], "a C call")
-            if st_rows[0]:
-                raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
+            if comm.local:
+                if failed:
+                    _lib.check(failed[0][1], failed[0][0])
+                if com_out[4] & 1:
+                    raise _lib.ACXError("sharded bfs: hash table overflow")
+                if com_out[4]:
+                    raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
+                succ_seq, err_seq, chunk_min = int(com_out[5]), int(com_out[6]), int(com_out[7])
+            else:
+                st_rows = comm.sum_rows([com_out[4], len(failed)])
+                agree(st_rows[1], "a C call")
+                if st_rows[0]:
+                    raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
             total_new, cut_p, nodes_at_cut = int(com_out[0]), int(com_out[1]), int(com_out[2])
             cut = cut_p if cut_p >= 0 else None
             err_p = err_seq // 12 if err_seq != NONE else None

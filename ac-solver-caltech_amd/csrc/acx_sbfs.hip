@@ -62,6 +62,13 @@ struct Ctl {
     uint32_t cur[MAXW];  // pack cursors
 };
 
+__device__ __forceinline__ void ctl_init(Ctl* c) {
+    Ctl z;
+    memset(&z, 0, sizeof(z));
+    z.succ_seq = z.err_seq = z.min_len = z.cut_p = NONE;
+    *c = z;
+}
+
 struct Args {
     uint64_t* lkeys;  // (lcap, kw) owned nodes, ascending global id
     int64_t* lgid;    // (lcap) global node id
@@ -88,6 +95,7 @@ struct Args {
     int64_t head, n_before, need, lcap, nloc, lo, nrecv;
     int P, Pr, L, kw, cyc, world, rank;
     uint32_t end;
+    int end_from_ctl;
 };
 
 // Table entries.  A committed node: (local slot + 1) << 32 | 32-bit fingerprint (bit 63 clear).
@@ -367,7 +375,10 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
         kp = a.recv + (r - n_own) * (a.kw + 1);
         s = (uint32_t)kp[a.kw];
     }
-    if (s > a.end) return;  // after the search's last child (its sslot stays SEEN)
+    // after the search's last child (its sslot stays SEEN); end_from_ctl: this rank's own first
+    // success / move error is the chunk's (one rank: no exchange, no read-back before the insert)
+    const uint32_t end = a.end_from_ctl ? min(a.ctl->succ_seq, a.ctl->err_seq) : a.end;
+    if (s > end) return;
     const Key<KWM> key = kload<KWM>(kp, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
     const uint32_t fp = (uint32_t)(h >> 32);
@@ -534,16 +545,24 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
         a.lkeys[li * a.kw + c] = rec_key(a, srec[i])[c];
     }
     uint32_t bs;
-    block_excl_scan(stored, sh, bs);
+    block_excl_scan(stored, sh, bs);  // (its barrier: every read of the block's sslot / srf is done)
     if (threadIdx.x == 0 && bs) atomicAdd(&a.ctl->stored, bs);
+    // the block's seqs back to SEEN / not lost for the next chunk (no per-chunk memset)
+    if (p < a.P) {
+#pragma unroll
+        for (int act = 0; act < 12; ++act) {
+            a.sslot[(uint32_t)p * 12u + act] = SEEN;
+            a.lost[(uint32_t)p * 12u + act] = 0;
+        }
+    }
 }
 
 // min child total over the local parents of the chunk with p <= last
-__global__ __launch_bounds__(TPB) void sbfs_minlen_kernel(Args a, int64_t last) {
+__global__ __launch_bounds__(TPB) void sbfs_minlen_kernel(Args a, int64_t last, int npar) {
     __shared__ uint32_t sh[TPB / WAVE];
     const int j = blockIdx.x * TPB + threadIdx.x;
     uint32_t v = NONE;
-    if (j < (int)a.ctl->npar && a.lgid[a.lo + j] - a.head <= last) v = a.pmin[j];
+    if (j < npar && a.lgid[a.lo + j] - a.head <= last) v = a.pmin[j];
     v = block_min(v, sh);
     if (threadIdx.x == 0 && v != NONE) atomicMin(&a.ctl->min_len, v);
 }
@@ -676,6 +695,7 @@ struct Shard {
     Ctl* ctl_host = nullptr;  // the last read-back (host copy)
     Pub* pub = nullptr;       // pinned, coherent: sbfs_publish_kernel writes it
     uint64_t pub_seq = 0;
+    int chunk_npar = 0;       // local parents of the last committed chunk
     int64_t* look_host = nullptr;
     void* bounce = nullptr;  // pinned (copy_to_host)
 
@@ -718,13 +738,11 @@ struct RootLaunch {
     void go() { sbfs_root_kernel<NW + 1><<<dim3(1), dim3(64), 0, st>>>(S->a, rk); }
 };
 
-// the chunk's control block to its initial values (no host copy)
+// the chunk's control block to its initial values (no host copy): at a search's start, and
+// after every chunk's commit read-back (sbfs_publish_kernel)
 __global__ void sbfs_ctl_init_kernel(Ctl* c) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Ctl z;
-    memset(&z, 0, sizeof(z));
-    z.succ_seq = z.err_seq = z.min_len = z.cut_p = NONE;
-    *c = z;
+    ctl_init(c);
 }
 struct LookupLaunch {
     Shard* S;
@@ -737,23 +755,26 @@ struct LookupLaunch {
 // the control block published to pinned, coherent host memory by a one-wave kernel (the
 // sequence number written last, system scope) -- a hipMemcpyAsync of it was a ~9 us blit per
 // read-back, two per chunk -- and read by the host's poll
-__global__ void sbfs_publish_kernel(const Ctl* c, Pub* host, uint64_t seq) {
+__global__ void sbfs_publish_kernel(Ctl* c, Pub* host, uint64_t seq, int reset) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(c);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&host->c);
     for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += WAVE) dst[i] = src[i];
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&host->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&host->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (reset) ctl_init(c);  // after a chunk's commit: the next chunk's initial values
+    }
 }
 
 // every read-back: publish, then poll the sequence number (hipStreamSynchronize may sleep and
 // wake late; two waits per chunk are on the search's critical path).  Every 4096 polls the
 // stream is queried (a failed launch), and a control block not published within 30 s (a kernel
 // that does not finish) is an error.
-static int sync_ctl(Shard* S, hipStream_t st) {
+static int sync_ctl(Shard* S, hipStream_t st, int reset = 0) {
     if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
     const uint64_t want = ++S->pub_seq;
-    sbfs_publish_kernel<<<dim3(1), dim3(WAVE), 0, st>>>(S->a.ctl, S->pub, want);
+    sbfs_publish_kernel<<<dim3(1), dim3(WAVE), 0, st>>>(S->a.ctl, S->pub, want, reset);
     if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t it = 1;; ++it) {
@@ -858,6 +879,12 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
     S->lo = 0;
     S->a.nloc = 0;
     if (hipMemsetAsync(S->a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
+    // the per-seq arrays are clean between chunks (each commit resets what its chunk used); a
+    // search that ended on an error may not have got there
+    if (hipMemsetAsync(S->a.sslot, 0xff, (size_t)12 * S->pmax * 4, st) != hipSuccess ||
+        hipMemsetAsync(S->a.lost, 0, (size_t)12 * S->pmax, st) != hipSuccess)
+        return ACX_E_LAUNCH;
+    sbfs_ctl_init_kernel<<<dim3(1), dim3(64), 0, st>>>(S->a.ctl);
     if (own == S->rank) {
         RootLaunch rl{S, st, {}};
         pack_key(presentation, S->L, S->kw, rl.rk.w);
@@ -869,9 +896,9 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
 }
 
 // out (int64[5 + world]): succ_seq, err_seq, min_len, local parents, overflow, send counts
-int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream) {
+int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, int32_t read_back, void* stream) {
     Shard* S = static_cast<Shard*>(h);
-    if (!S || !out || P < 1 || P > S->pmax || head < 0) return ACX_E_ARG;
+    if (!S || (read_back && !out) || P < 1 || P > S->pmax || head < 0) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;
     S->head = head;
@@ -883,12 +910,14 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream
     a.Pr = S->Pr;
     a.lo = S->lo;
     a.nloc = S->nloc;
-    sbfs_ctl_init_kernel<<<dim3(1), dim3(64), 0, st>>>(a.ctl);
+    // the control block holds its initial values (the search's reset, or the previous chunk's
+    // commit read-back re-initialised it)
     if (S->Pr > 0) {
         ExpandLaunch el{S, st};
         by_nw(S->L, el);
         sbfs_expand_reduce_kernel<<<dim3(1), dim3(1024), 0, st>>>(a, (S->Pr + STILE - 1) / STILE);
     }
+    if (!read_back) return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
     const int r = sync_ctl(S, st);
     if (r != ACX_OK) return r;
     const Ctl& c = *S->ctl_host;
@@ -923,10 +952,10 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
     a.recv = recv;
     a.nrecv = nrecv;
     a.gmask = gmask;
+    a.end_from_ctl = end < 0;
     a.end = end < 0 || end > (int64_t)NONE ? NONE : (uint32_t)end;
     S->nrecv = nrecv;
-    if (hipMemsetAsync(a.sslot, 0xff, (size_t)12 * S->P * 4, st) != hipSuccess) return ACX_E_LAUNCH;  // SEEN
-    if (hipMemsetAsync(a.lost, 0, (size_t)12 * S->P, st) != hipSuccess) return ACX_E_LAUNCH;
+    // sslot / lost are SEEN / 0 here: the previous chunk's commit (or the search's reset) cleared them
     if (12 * (int64_t)S->Pr + nrecv > 0) {
         InsertLaunch il{S, st};
         by_nw(S->L, il);
@@ -952,7 +981,7 @@ int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t ne
     sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.bsum, nb, &a.ctl->total_new);
     sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.lbsum, nb, &a.ctl->local_new);
     sbfs_commit_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
-    const int r = sync_ctl(S, st);
+    const int r = sync_ctl(S, st, 1);  // and re-initialise the control block for the next chunk
     if (r != ACX_OK) return r;
     const Ctl& c = *S->ctl_host;
     out[0] = (int64_t)c.total_new;
@@ -960,8 +989,13 @@ int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t ne
     out[2] = (int64_t)c.nodes_at_cut;
     out[3] = (int64_t)c.local_new;
     out[4] = c.overflow;
+    out[5] = c.succ_seq;  // the chunk's expansion, as acx_sbfs_expand reads it back
+    out[6] = c.err_seq;
+    out[7] = c.min_len;
+    out[8] = c.npar;
     S->nloc += c.stored;
     S->lo += c.npar;
+    S->chunk_npar = (int)c.npar;
     return ACX_OK;
 }
 
@@ -971,10 +1005,10 @@ int64_t acx_sbfs_min_len(void* h, int64_t last, void* stream) {
     if (!S) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(&S->a.ctl->min_len, 0xff, 4, st) != hipSuccess) return ACX_E_LAUNCH;  // NONE
-    // npar is read on the device; lo was advanced by commit
+    // lo was advanced by commit past the chunk's local parents
     Args a = S->a;
-    a.lo = S->lo - S->ctl_host->npar;
-    if (S->Pr > 0) sbfs_minlen_kernel<<<dim3(nblocks(S->Pr)), dim3(TPB), 0, st>>>(a, last);
+    a.lo = S->lo - S->chunk_npar;
+    if (S->Pr > 0) sbfs_minlen_kernel<<<dim3(nblocks(S->Pr)), dim3(TPB), 0, st>>>(a, last, S->chunk_npar);
     const int r = sync_ctl(S, st);
     if (r != ACX_OK) return r;
     return S->ctl_host->min_len == NONE ? 255 : (int64_t)S->ctl_host->min_len;
@@ -988,7 +1022,7 @@ int64_t acx_sbfs_trace(void* h, int64_t running, int64_t end, int64_t* out, int6
     if (!S || !out || cap < 0) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     Args a = S->a;
-    const int npar = (int)S->ctl_host->npar;
+    const int npar = S->chunk_npar;
     a.lo = S->lo - npar;  // commit advanced lo past the chunk's local parents
     if (npar == 0) return 0;
     int64_t* d_out = nullptr;

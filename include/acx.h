@@ -307,19 +307,23 @@ int64_t acx_bfs_min_trace(void* h, int32_t* out, int64_t cap);
  *   acx_sbfs_owner     owner rank of a presentation's key (HOST pointer)
  *   acx_sbfs_reset     new search from `presentation` (HOST); returns the root's owner rank
  *   acx_sbfs_expand    expands this rank's parents among global ids [head, head + P);
- *                      out int64[5 + world] = success seq, move-error seq (0xffffffff: none),
- *                      min child total, local parents, overflow, children per owner
+ *                      read_back != 0: waits for it and writes out int64[5 + world] = success
+ *                      seq, move-error seq (0xffffffff: none), min child total, local parents,
+ *                      overflow, children per owner; read_back = 0 (one rank: nothing to
+ *                      exchange) returns at once -- the same fields come back from the commit
  *   acx_sbfs_pack      the children other ranks own into `send` ((n, kw + 1) uint64: key
  *                      words, chunk seq), grouped by owner in rank order (the count for the
  *                      rank itself is 0: its own children are inserted in place)
  *   -- all_to_all of the records: recv holds the records every rank sent to this one --
  *   acx_sbfs_insert    probe / claim the visited set with this rank's own children and the
- *                      received records, up to seq `end`; survivors as bits of gmask ((P)
+ *                      received records, up to seq `end` (end < 0: this rank's own first
+ *                      success / move error, i.e. one rank's); survivors as bits of gmask ((P)
  *                      uint32, written by the call)
  *   -- all_reduce (sum) of gmask over the ranks --
- *   acx_sbfs_commit    global ids, the node-budget cut and the appends; out int64[5] = nodes
+ *   acx_sbfs_commit    global ids, the node-budget cut and the appends; out int64[9] = nodes
  *                      appended (all ranks), cut parent (-1: none), nodes after the cut
- *                      parent, nodes appended here, overflow flags
+ *                      parent, nodes appended here, overflow flags, then this rank's expansion
+ *                      of the chunk: success seq, move-error seq, min child total, local parents
  *   acx_sbfs_min_len   min child total over this rank's parents of the last chunk up to `last`
  *   acx_sbfs_lookup    out int64[4] = found, parent id, action, total of the node with id g
  *   acx_sbfs_node_keys this rank's nodes (keys, global ids; ascending id); returns the count
@@ -332,7 +336,7 @@ void acx_sbfs_destroy(void* h);
 int64_t acx_sbfs_max_records(void* h);
 int32_t acx_sbfs_owner(const int32_t* presentation, int32_t L, int32_t world);
 int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream);
-int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, void* stream);
+int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, int32_t read_back, void* stream);
 int acx_sbfs_pack(void* h, uint64_t* send, void* stream);
 int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, uint32_t* gmask, void* stream);
 int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t need, int64_t* out, void* stream);
