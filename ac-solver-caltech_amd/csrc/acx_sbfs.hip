@@ -448,9 +448,9 @@ __global__ __launch_bounds__(TPB) void sbfs_count_kernel(Args a) {
     }
 }
 
-// (4b) exclusive scan of x[0..nb) in place, one block of 1024; the total into *total
-__global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, int nb, uint64_t* total) {
-    __shared__ uint32_t sh[1024 / WAVE];
+// (4b) exclusive scans of x[0..nb) and y[0..nb) in place, one block of 1024 (both arrays in one
+// launch); the totals into *tx, *ty
+__device__ __forceinline__ void scan_1024(uint32_t* x, int nb, uint64_t* total, uint32_t* sh) {
     const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
     const int per = (nb + 1023) / 1024;
     const int b0 = t * per, b1 = min(nb, b0 + per);
@@ -476,6 +476,12 @@ __global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, int nb, ui
         run += c;
     }
     if (t == 0) *total = tot;
+    __syncthreads();  // sh reuse
+}
+__global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, uint32_t* y, int nb, uint64_t* tx, uint64_t* ty) {
+    __shared__ uint32_t sh[1024 / WAVE];
+    scan_1024(x, nb, tx, sh);
+    scan_1024(y, nb, ty, sh);
 }
 
 // (4c) global ids, the budget cut, and the appends to this rank's store.  A block's own
@@ -978,8 +984,7 @@ int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t ne
     a.nloc = S->nloc;
     const int nb = nblocks(S->P);
     sbfs_count_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
-    sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.bsum, nb, &a.ctl->total_new);
-    sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.lbsum, nb, &a.ctl->local_new);
+    sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.bsum, a.lbsum, nb, &a.ctl->total_new, &a.ctl->local_new);
     sbfs_commit_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
     const int r = sync_ctl(S, st, 1);  // and re-initialise the control block for the next chunk
     if (r != ACX_OK) return r;

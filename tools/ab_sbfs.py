@@ -3,7 +3,11 @@ library (a whole libacx.so, e.g. a build of an earlier revision) in its own proc
 the processes interleaved ROUNDS times; per process a warmup then REPS timed searches (wall clock
 around the call, after a synchronize), plus the device BFS in the same process for scale.
 
-    python tools/ab_sbfs.py abv/libacx_r03.so ac-solver-caltech_amd/acx/libacx.so [--nodes 1e7] [--rounds 3]
+    python tools/ab_sbfs.py abv/libacx_r03.so:abv/r03/ac-solver-caltech_amd ac-solver-caltech_amd/acx/libacx.so
+
+Each entry is LIB or LIB:PKGROOT -- the Python package (acx) the library is driven by, e.g. an
+earlier revision's (`git archive REV ac-solver-caltech_amd/acx | tar -x -C DIR`), whose C-ABI
+calls match that library's.  [--nodes 1e7] [--rounds 3] [--reps 5]
 """
 import argparse
 import json
@@ -47,20 +51,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
-    code = CHILD % {"pkg": os.path.join(REPO, "ac-solver-caltech_amd"), "nodes": a.nodes, "reps": a.reps}
     res = {lib: {"sharded": [], "device": []} for lib in a.libs}
     for _ in range(a.rounds):
-        for lib in a.libs:
+        for entry in a.libs:
+            lib, _, pkg = entry.partition(":")
+            code = CHILD % {"pkg": os.path.abspath(pkg or os.path.join(REPO, "ac-solver-caltech_amd")),
+                            "nodes": a.nodes, "reps": a.reps}
             env = dict(os.environ, ACX_LIB=os.path.abspath(lib))
             p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
             if p.returncode != 0:
-                sys.exit(f"{lib}: {p.stderr[-2000:]}")
+                sys.exit(f"{entry}: {p.stderr[-2000:]}")
             d = json.loads(p.stdout.strip().splitlines()[-1])
             for k in d:
-                res[lib][k] += d[k]
+                res[entry][k] += d[k]
     out = {"nodes": a.nodes, "rounds": a.rounds, "reps_per_process": a.reps}
     for lib, d in res.items():
-        out[os.path.basename(lib) if "abv" in lib else lib] = {
+        out[os.path.basename(lib.partition(":")[0]) if "abv" in lib else lib] = {
             k: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4), "all": [round(x, 4) for x in v]}
             for k, v in d.items()}
     print(json.dumps(out, indent=1))
