@@ -211,11 +211,17 @@ class VecACEnv:
       info_format "actions" (the gymnasium >= 1.0 key layout): info["actions"][i] = the move list
         of env i's solved episode, info["_actions"] its mask.
     Building it synchronises with the device once per step (the trainer reads it on the host).
+
+    autoreset_mode "same_step" (default; gymnasium < 1.0, what the reference trains with): the
+    step that ends an episode returns the env's starting state.  "next_step" (gymnasium >= 1.0):
+    it returns the terminal state, and the env's next step resets it instead of moving (action
+    ignored, reward 0, done = truncated = False) -- acx_step_next; its info layout is "actions"
+    (no final_observation).  Parity unpinned: gymnasium is an un-vendored dependency.
     """
 
     def __init__(self, initial_states, horizon_length: int = 1000, device=None, cyclical: bool = True,
                  track_final_obs: bool = True, check_errors: bool = False, record_actions: bool = False,
-                 info_format: str = "final_info"):
+                 info_format: str = "final_info", autoreset_mode: str = "same_step"):
         self.device = torch.device(device if device is not None else "cuda")
         init = torch.as_tensor(np.asarray(initial_states) if not torch.is_tensor(initial_states) else initial_states)
         if init.dim() != 2 or init.shape[1] % 2:
@@ -241,6 +247,14 @@ class VecACEnv:
         self.lengths = torch.empty((B, 2), dtype=torch.int32, device=dev)
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        if autoreset_mode not in ("same_step", "next_step"):
+            raise ValueError("autoreset_mode must be 'same_step' or 'next_step'")
+        self.autoreset_mode = autoreset_mode
+        if autoreset_mode == "next_step":
+            if record_actions and info_format != "actions":
+                raise ValueError("autoreset_mode='next_step' reports info in the 'actions' layout (gymnasium >= 1.0)")
+            track_final_obs = False  # the ending step's own observation is the terminal state
+            self.pending = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.final_obs = torch.zeros_like(self.state) if track_final_obs else None
         if info_format not in ("final_info", "actions"):
             raise ValueError("info_format must be 'final_info' or 'actions'")
@@ -260,6 +274,8 @@ class VecACEnv:
             self.reset_state.copy_(s.reshape(self.reset_state.shape))
         self.state.copy_(self.reset_state)
         self.step_count.zero_()
+        if self.autoreset_mode == "next_step":
+            self.pending.zero_()
         return self.state, {}
 
     def reset_env(self, i: int, starting_state) -> None:
@@ -273,6 +289,8 @@ class VecACEnv:
         self.reset_state[i].copy_(t)
         self.state[i].copy_(t)
         self.step_count[i] = 0
+        if self.autoreset_mode == "next_step":
+            self.pending[i] = 0
 
     def _step_args(self):
         """Pointers of the env's persistent buffers, computed once (the per-call Python
@@ -292,7 +310,15 @@ class VecACEnv:
             actions = actions.to(self.device, torch.int32).contiguous().reshape(self.num_envs)
         s_in, s_out, rs, cnt, rew, dn, tr, ln, fo, err, ec = self._step_args()
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        if self.record_actions:
+        if self.autoreset_mode == "next_step":
+            rec = self.record_actions
+            st = self._lib.acx_step_next(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln,
+                                         self.pending.data_ptr(), self.action_hist.data_ptr() if rec else None,
+                                         self.action_hist.shape[0] if rec else 0,
+                                         self.episode_len.data_ptr() if rec else None, err, ec, self.num_envs,
+                                         self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
+            _lib.check(st, "acx_step_next")
+        elif self.record_actions:
             st = self._lib.acx_step_record(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo,
                                            self.action_hist.data_ptr(), self.action_hist.shape[0],
                                            self.episode_len.data_ptr(), err, ec, self.num_envs,

@@ -1550,6 +1550,9 @@ struct StepArgs {
     int32_t* next_base;
     // state_out == state_in (set by the launcher): the state store writes changed relators only
     int in_place;
+    // next-step autoreset (acx_step_next; NULL: same-step): per env, its episode ended on the
+    // previous call -- this call resets it instead of stepping, and records whether it ends now
+    uint8_t* pending;
 };
 
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path)
@@ -1565,6 +1568,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 
     // the env's move id and step count: issued ahead of the tile so their latency hides under it
     int act_in = 0, cnt_in = 0;
+    const bool pend = w.active && a.pending && a.pending[env] != 0;  // next-step autoreset: reset now
 #if ACX_EARLY_SCALARS
     if (w.active) {
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
@@ -1601,10 +1605,12 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
         // at [k][i] -- envs at the same episode position write one coalesced row segment (an
         // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
-        if (LEARN && a.action_hist && cnt - 1 < a.hist_cap) a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
+        if (LEARN && a.action_hist && !pend && cnt - 1 < a.hist_cap)
+            a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
         const bool bad = tile.pack(w.lane, p);
         const bool cyc = a.cyclical != 0;
-        if (bad) e = ACX_ERR_DOMAIN;
+        if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
+        else if (bad) e = ACX_ERR_DOMAIN;
         else if (pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         else {
                 const pl::MoveOut<PW> mo = pl::ac_move_call<PW>(p, act, L, cyc);
@@ -1614,18 +1620,23 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
         if (!keep) dm = tile.unpack_dirty(w.lane, p);
-        const bool triv = !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
-        const bool trunc = !keep && a.step_count && cnt >= a.horizon;
-        if (a.reward) a.reward[env] = triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        const bool triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
+        const bool trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
+        // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does
+        const int32_t rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        if (a.reward) a.reward[env] = rwd;
         if (a.done) a.done[env] = triv;
         if (a.truncated) a.truncated[env] = trunc;
         fin = triv || trunc;
         if constexpr (LEARN) {
-            if (a.reward_f32) a.reward_f32[env] = (float)(triv ? a.horizon * L * 2 : -(p.n0 + p.n1));
+            if (a.reward_f32) a.reward_f32[env] = (float)rwd;
             if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
             if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
         }
-        reset = fin && a.reset_state && !keep;
+        // same-step autoreset: an env that ends resets now; next-step: a pending env resets now and
+        // an env that ends is reset by the next call
+        reset = a.pending ? pend : (fin && a.reset_state && !keep);
+        if (a.pending) a.pending[env] = fin ? 1 : 0;
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
     }
@@ -2688,6 +2699,24 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
                lengths_out, final_obs, err, err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                B, L, horizon, cyclical, 0};
     StepLaunch f{a, (hipStream_t)stream, false};
+    return dispatch(L, f);
+}
+
+int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
+                  int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
+                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                  int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state_in || !state_out || !action || !reset_state || !step_count || !pending) return ACX_E_ARG;
+    if ((action_hist != nullptr) != (hist_cap > 0) || (episode_len && !action_hist)) return ACX_E_ARG;
+    if (!aligned16(state_in) || !aligned16(state_out)) return ACX_E_ARG;
+    StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated, lengths_out, nullptr,
+               err, err_count, nullptr, nullptr, nullptr, nullptr, action_hist, episode_len, B, L, horizon, cyclical,
+               hist_cap};
+    a.pending = pending;
+    // with a move history: the learner instantiation (it compiles the history writes)
+    StepLaunch f{a, (hipStream_t)stream, action_hist != nullptr};
     return dispatch(L, f);
 }
 

@@ -136,6 +136,22 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
                     int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
 
 /*
+ * acx_step with gymnasium >= 1.0's NEXT_STEP autoreset instead of the same-step one (the
+ * reference trainer reads either info layout, training.py:273-280; gymnasium is an
+ * un-vendored dependency, so this timing is parity unpinned).  pending (B) uint8, in/out: an
+ * env whose flag is set is reset to its reset_state row on this call instead of stepping --
+ * its action is ignored, reward 0, done = truncated = 0, step count 0 -- and every env's flag
+ * becomes done | truncated of this call, so the step that ends an episode returns the terminal
+ * state itself.  action_hist / hist_cap / episode_len: as acx_step_record (NULL / 0 / NULL for
+ * none).  reset_state and step_count are required; other arguments as acx_step (no final_obs:
+ * the ending step's state is the observation).
+ */
+int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
+                  int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
+                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
+                  int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+
+/*
  * Start-state curriculum of the PPO trainer, round 1 (training.py:319-352): every env whose
  * episode ended this step (done | truncated), in env order, starts next from
  * curriculum_states[k], k = *next_index, *next_index + 1, ... (max(states_processed) + 1);

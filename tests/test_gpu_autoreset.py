@@ -1,0 +1,88 @@
+"""GPU: gymnasium >= 1.0's NEXT_STEP autoreset (VecACEnv(autoreset_mode="next_step") ->
+acx_step_next) against a host model built on the oracle's ACEnv.step without autoreset
+(oracle/acx_oracle.c): the step that ends an episode returns the terminal state; the env's next
+step resets it instead of moving (action ignored, reward 0, done = truncated = 0, count 0).
+Parity unpinned upstream (gymnasium is an un-vendored dependency); the per-step
+semantics are the oracle's, which is pinned to the reference's fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _starts(L, B):
+    from bench import ms_starts
+    st = ms_starts(L, B)
+    triv = np.zeros((8, 2 * L), np.int32)
+    for r, (a0, a1) in enumerate([(1, 2), (1, -2), (-1, 2), (-1, -2), (2, 1), (2, -1), (-2, 1), (-2, -1)]):
+        triv[r, 0], triv[r, L] = a0, a1
+    st[::3] = triv[np.arange(B)[::3] % 8]  # a third start trivial: episodes end often
+    return st
+
+
+@pytest.mark.parametrize("L,record", [(36, False), (36, True), (128, False), (18, True)])
+def test_next_step_autoreset_matches_oracle_model(L, record):
+    from acx.envs.ac_env import VecACEnv
+    from oracle import oracle as O
+    B, H, T = 3000, 7, 30
+    starts = _starts(L, B)
+    env = VecACEnv(starts, horizon_length=H, device=DEV, record_actions=record, info_format="actions",
+                   autoreset_mode="next_step")
+    rng = np.random.default_rng(L)
+    state = starts.copy()
+    count = np.zeros(B, np.int32)
+    pending = np.zeros(B, bool)
+    hist = [[] for _ in range(B)]
+    n_done = n_trunc = n_reset = 0
+    for t in range(T):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        obs, rew, dn, tr, info = env.step(torch.as_tensor(a, device=DEV))
+        # model: pending envs reset, the others take the oracle's step (no autoreset)
+        m_rew = np.zeros(B, np.int32)
+        m_dn = np.zeros(B, np.uint8)
+        m_tr = np.zeros(B, np.uint8)
+        go = ~pending
+        idx = np.nonzero(go)[0]
+        sub = np.ascontiguousarray(state[idx])
+        cnt = np.ascontiguousarray(count[idx])
+        r, d, tt, err, _, _ = O.env_step(sub, a[idx], L, H, cnt)
+        assert not err.any()
+        state[idx], count[idx] = sub, cnt
+        m_rew[idx], m_dn[idx], m_tr[idx] = r, d, tt
+        for k, i in enumerate(idx):
+            hist[i].append(int(a[i]))
+        rs = np.nonzero(pending)[0]
+        state[rs], count[rs] = starts[rs], 0
+        for i in rs:
+            hist[i] = []
+        n_reset += len(rs)
+        assert np.array_equal(obs.cpu().numpy(), state), t
+        assert np.array_equal(rew.cpu().numpy(), m_rew), t
+        assert np.array_equal(dn.cpu().numpy(), m_dn), t
+        assert np.array_equal(tr.cpu().numpy(), m_tr), t
+        assert np.array_equal(env.step_count.cpu().numpy(), count), t
+        if record:
+            solved = np.nonzero(m_dn)[0]
+            if len(solved):
+                assert info["_actions"].tolist() == m_dn.astype(bool).tolist()
+                for i in solved:
+                    assert list(info["actions"][i]) == hist[i], (t, i)
+        n_done += int(m_dn.sum())
+        n_trunc += int(m_tr.sum())
+        pending = (m_dn | m_tr).astype(bool)
+    assert n_done > 50 and n_trunc > 50 and n_reset > 100  # every path exercised
+    assert int(env.err_count.item()) == 0
+
+
+def test_next_step_mode_rejects_final_info_layout():
+    from acx.envs.ac_env import VecACEnv
+    with pytest.raises(ValueError):
+        VecACEnv(_starts(36, 64), device=DEV, record_actions=True, info_format="final_info",
+                 autoreset_mode="next_step")
+    with pytest.raises(ValueError):
+        VecACEnv(_starts(36, 64), device=DEV, autoreset_mode="bogus")
