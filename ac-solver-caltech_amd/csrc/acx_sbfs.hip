@@ -553,13 +553,13 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     uint32_t bs;
     block_excl_scan(stored, sh, bs);  // (its barrier: every read of the block's sslot / srf is done)
     if (threadIdx.x == 0 && bs) atomicAdd(&a.ctl->stored, bs);
-    // the block's seqs back to SEEN / not lost for the next chunk (no per-chunk memset)
-    if (p < a.P) {
-#pragma unroll
-        for (int act = 0; act < 12; ++act) {
-            a.sslot[(uint32_t)p * 12u + act] = SEEN;
-            a.lost[(uint32_t)p * 12u + act] = 0;
-        }
+    // the block's seqs back to SEEN / not lost for the next chunk (no per-chunk memset);
+    // consecutive threads on consecutive seqs
+    const uint32_t s0 = (uint32_t)blockIdx.x * TPB * 12u;
+    const uint32_t s1 = min((uint32_t)a.P * 12u, s0 + TPB * 12u);
+    for (uint32_t sq = s0 + threadIdx.x; sq < s1; sq += TPB) {
+        a.sslot[sq] = SEEN;
+        a.lost[sq] = 0;
     }
 }
 
