@@ -89,6 +89,7 @@ class LearnerEnv:
         if a32 is None and a64 is None:
             a64 = action.to(torch.int64)
         v = self.vec
+        v._lengths_ok = False  # the learner step does not write the vector env's lengths
         stream = torch.cuda.current_stream(dev).cuda_stream
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         if fused:
@@ -142,6 +143,7 @@ class LearnerEnv:
         s = self.initial_states[state_index]
         self.vec.reset_state[i].copy_(s)
         self.vec.state[i].copy_(s)
+        self.vec._lengths_ok = False
         self.vec.step_count[i] = 0
         self.curr_index[i] = state_index
         self.needs_host[i] = 0

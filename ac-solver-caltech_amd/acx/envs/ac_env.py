@@ -193,6 +193,15 @@ class ACEnv:
         return self
 
 
+def _row_extent(rows: torch.Tensor, L: int) -> torch.Tensor:
+    """(B, 2) int32: per relator, the position after its last non-zero letter -- its length for
+    a canonical row; for any other row (a gap, a letter out of domain) it still covers every
+    non-zero entry, so acx_step_lengths reads them and reports the row as acx_step would"""
+    nz = rows.reshape(-1, 2, L) != 0
+    pos = torch.arange(1, L + 1, dtype=torch.int32, device=rows.device)
+    return (nz * pos).amax(dim=2).to(torch.int32)
+
+
 class VecACEnv:
     """B Andrews-Curtis envs stepped by one kernel launch per step.
 
@@ -244,7 +253,11 @@ class VecACEnv:
         self.reward = torch.empty(B, dtype=torch.int32, device=dev)
         self.done = torch.empty(B, dtype=torch.uint8, device=dev)
         self.truncated = torch.empty(B, dtype=torch.uint8, device=dev)
-        self.lengths = torch.empty((B, 2), dtype=torch.int32, device=dev)
+        # the rows' relator lengths: kept current so that a plain step reads and writes only the
+        # letters (acx_step_lengths); _lengths_ok is False after anything that changed rows without
+        # them (rollout, direct writes by a learner), and the next step uses acx_step, which rewrites them
+        self.lengths = _row_extent(self.state, L).contiguous()
+        self._lengths_ok = True
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
         if autoreset_mode not in ("same_step", "next_step"):
@@ -270,9 +283,15 @@ class VecACEnv:
     def reset(self, *, seed=None, options=None):
         """Reset every env to its starting state (options["starting_states"] replaces them)."""
         if options and "starting_states" in options:
-            s = torch.as_tensor(np.asarray(options["starting_states"])).to(self.device, torch.int32)
-            self.reset_state.copy_(s.reshape(self.reset_state.shape))
+            rows = np.asarray(options["starting_states"]).reshape(tuple(self.reset_state.shape))
+            if _invalid_rows(rows).any():
+                raise ValueError("starting_states must be valid presentations")
+            _check_domain(rows)
+            self.reset_state.copy_(torch.as_tensor(rows.astype(np.int32)).to(self.device))
         self.state.copy_(self.reset_state)
+        # (reset_state may also have been rewritten on the device, e.g. by the learner's curriculum)
+        self.lengths.copy_(_row_extent(self.state, self.max_relator_length))
+        self._lengths_ok = True
         self.step_count.zero_()
         if self.autoreset_mode == "next_step":
             self.pending.zero_()
@@ -288,6 +307,7 @@ class VecACEnv:
         t = torch.as_tensor(s.astype(np.int32), device=self.device)
         self.reset_state[i].copy_(t)
         self.state[i].copy_(t)
+        self.lengths[i].copy_(_row_extent(t, self.max_relator_length)[0])
         self.step_count[i] = 0
         if self.autoreset_mode == "next_step":
             self.pending[i] = 0
@@ -318,6 +338,12 @@ class VecACEnv:
                                          self.episode_len.data_ptr() if rec else None, err, ec, self.num_envs,
                                          self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
             _lib.check(st, "acx_step_next")
+        elif self._lengths_ok and not self.record_actions:
+            # the rows' lengths are current: only their letters are read and written
+            st = self._lib.acx_step_lengths(s_in, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
+                                            self.num_envs, self.max_relator_length, self.horizon_length,
+                                            int(self.cyclical), stream)
+            _lib.check(st, "acx_step_lengths")
         elif self.record_actions:
             st = self._lib.acx_step_record(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo,
                                            self.action_hist.data_ptr(), self.action_hist.shape[0],
@@ -329,6 +355,7 @@ class VecACEnv:
                                     self.num_envs, self.max_relator_length, self.horizon_length, int(self.cyclical),
                                     stream)
             _lib.check(st, "acx_step")
+        self._lengths_ok = True  # every step kernel writes the rows' lengths
         if self.check_errors:
             self.raise_if_errors()
         info = {"final_observation": self.final_obs} if self.final_obs is not None else {}
@@ -369,6 +396,7 @@ class VecACEnv:
         ops.rollout(self.state, actions, self.reset_state, self.step_count, horizon=self.horizon_length,
                     cyclical=self.cyclical, obs_traj=obs_traj, reward_traj=reward_traj, done_traj=done_traj,
                     trunc_traj=trunc_traj, err=self.err, err_count=self.err_count)
+        self._lengths_ok = False  # the rollout does not write lengths
         if self.check_errors:
             self.raise_if_errors()
 

@@ -67,8 +67,12 @@ def step(
     final_obs: Optional[torch.Tensor] = None,
     err: Optional[torch.Tensor] = None,
     err_count: Optional[torch.Tensor] = None,
+    lengths_in: bool = False,
 ) -> torch.Tensor:
-    """acx_step: batched ACEnv.step / ACMove.  Returns state_out (in place if given as state_in)."""
+    """acx_step: batched ACEnv.step / ACMove.  Returns state_out (in place if given as state_in).
+    lengths_in: `lengths` already holds the rows' relator lengths (the previous call's output,
+    or (L, L) for "unknown") and the step is in place -> acx_step_lengths, which reads and writes
+    only the chunks inside the letters (ACMove's lengths in / lengths out, ac_moves.py:159,231)."""
     lib = _lib.load()
     _need_gpu(state_in, "state_in")
     L = _L_of(state_in)
@@ -88,6 +92,16 @@ def step(
     _check(final_obs, "final_obs", _INT32, (B, 2 * L), dev)
     _check(err, "err", _UINT8, (B,), dev)
     _check(err_count, "err_count", _INT32, (1,), dev)
+    if lengths_in:
+        if lengths is None or state_out.data_ptr() != state_in.data_ptr():
+            raise ValueError("lengths_in needs lengths and an in-place step (state_out is state_in)")
+        st = lib.acx_step_lengths(
+            _ptr(state_in), _ptr(action), _ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done),
+            _ptr(truncated), _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count),
+            B, L, int(horizon), int(bool(cyclical)), _stream(dev),
+        )
+        _lib.check(st, "acx_step_lengths")
+        return state_out
     st = lib.acx_step(
         _ptr(state_in), _ptr(state_out), _ptr(action), _ptr(reset_state), _ptr(step_count), _ptr(reward),
         _ptr(done), _ptr(truncated), _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count),

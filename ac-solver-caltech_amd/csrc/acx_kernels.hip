@@ -147,6 +147,24 @@ __device__ __forceinline__ void swar_pack4(uint32_t d, uint32_t& c8, uint32_t& n
     nz4 = (u & 3u) | ((u >> 14) & 0xcu);
 }
 
+// the step kernel's L = 128 tile load: chunks converted by chunk_i8 into a lane-fixed slot
+// address, rows flagged from one wave-wide bad mask at the end (A/B knob: 0 = the per-letter
+// to_i8 conversion and a per-chunk flag store)
+#ifndef ACX_FAST_CONVERT
+#define ACX_FAST_CONVERT 1
+#endif
+// 16 bytes of a row (4 int32 letters) -> the dword of their low bytes (2 v_perm_b32 + or);
+// bad = a letter outside {-2..2} (max / min of the four).  A bad chunk's bytes are arbitrary:
+// its row is flagged and never decoded from the tile.
+__device__ __forceinline__ uint32_t chunk_i8(const int4& v, bool& bad) {
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, 0x0c0c0400u);  // x.b0, y.b0
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, 0x04000c0cu);  // z.b0, w.b0
+    const int mx = max(max(v.x, v.y), max(v.z, v.w));
+    const int mn = min(min(v.x, v.y), min(v.z, v.w));
+    bad = mx > 2 || mn < -2;
+    return lo | hi;
+}
+
 // 8-bit code field -> 4 int8 letters, the first s/8 kept (s = 8m, m = 0..4), the rest zero.
 // The four 2-bit codes are spread to one per byte (two shift-or-mask rounds); a byte past m
 // gets selector bit 2 set, so one v_perm_b32 reads either the letter table {1,-1,2,-2}
@@ -183,9 +201,10 @@ struct FastTile {
     uint32_t* lds;
     uint8_t* flags;
     uint8_t* dirty;         // per row: bit h = relator h differs from the loaded row (store_dirty)
+    uint8_t* lim;           // per row and relator, lengths-carrying step: live 16-byte chunks (lim[2r + h])
     bool tile_bad = false;  // wave-uniform: some row of the last load was flagged
 
-    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     // per-row fallback codes (FB_* below) replacing whatever the loads left in flags[]; the
     // flagged rows of store<true> / store_dirty / store_rows_i8_fb copy their fallback row
     __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
@@ -204,6 +223,24 @@ struct FastTile {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
         dirty = flags + WAVE;
+        lim = flags + 2 * WAVE;
+    }
+    // lengths-carrying step: row `lane` has relators of n0 / n1 letters -> its live chunk counts
+    __device__ __forceinline__ void set_lim(int lane, int n0, int n1) const {
+        lim[2 * lane] = (uint8_t)live_chunks(n0);
+        lim[2 * lane + 1] = (uint8_t)live_chunks(n1);
+    }
+    __device__ __forceinline__ static int live_chunks(int n) { return n <= 0 ? 0 : n >= L ? HALF : (n + 3) >> 2; }
+    // before the store: the live chunks of the row's old (set_lim) or new letters n0 / n1
+    __device__ __forceinline__ void widen_lim(int lane, int n0, int n1) const {
+        const int a = live_chunks(n0), b = live_chunks(n1);
+        if (a > lim[2 * lane]) lim[2 * lane] = (uint8_t)a;
+        if (b > lim[2 * lane + 1]) lim[2 * lane + 1] = (uint8_t)b;
+    }
+    // chunk k (< CPR) of row r is live (inside its relator's letters)
+    __device__ __forceinline__ bool live(int r, int k) const {
+        const int h = k >= HALF ? 1 : 0;
+        return k - h * HALF < lim[2 * r + h];
     }
     __device__ __forceinline__ int Lr() const { return L; }
     __device__ __forceinline__ int8_t* row(int r) const { return reinterpret_cast<int8_t*>(lds + r * S); }
@@ -220,8 +257,10 @@ struct FastTile {
     }
 
     // global rows (contiguous, 2L int32 each) -> LDS (PIPE: see CodeTile::load; this full-tile
-    // loop is unrolled already)
-    template <bool PIPE = false>
+    // loop is unrolled already).  LIVE (the lengths-carrying step; lim[] set for every row): only
+    // the chunks inside each relator's letters are read, the rest of the image is zero (the rows
+    // are canonical: letters, then zero padding)
+    template <bool PIPE = false, bool LIVE = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));  // keep the address math here (no hoisting into the caller)
@@ -234,15 +273,26 @@ struct FastTile {
 #pragma unroll
             for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
                 int4 v[LOAD_BATCH];
+                bool lv[LOAD_BATCH];
 #pragma unroll
-                for (int u = 0; u < LOAD_BATCH; ++u)
-                    if (u0 + u < CPR) v[u] = src[(u0 + u) * WAVE];
+                for (int u = 0; u < LOAD_BATCH; ++u) {
+                    if (u0 + u >= CPR) continue;
+                    const int c = ln + (u0 + u) * WAVE;
+                    lv[u] = !LIVE || live(c / CPR, c % CPR);
+                    if (lv[u]) v[u] = src[(u0 + u) * WAVE];
+                }
 #pragma unroll
                 for (int u = 0; u < LOAD_BATCH; ++u) {
                     if (u0 + u >= CPR) continue;
                     bool bad = false;
-                    const uint32_t p = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
-                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                    uint32_t p = 0;
+#if ACX_FAST_CONVERT
+                    if (lv[u]) p = chunk_i8(v[u], bad);
+#else
+                    if (lv[u])
+                        p = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) | (to_i8(v[u].z, bad) << 16) |
+                            (to_i8(v[u].w, bad) << 24);
+#endif
                     lds[lds_index(ln, u0 + u)] = p;
                     if (bad) flags[(ln + (u0 + u) * WAVE) / CPR] = 1;
                     any_bad |= bad;
@@ -252,11 +302,13 @@ struct FastTile {
             for (int u = 0; u < CPR; ++u) {
                 const int c = ln + u * WAVE;
                 if (c < nc) {
-                    const int4 v = src[u * WAVE];
-                    bool bad = false;
-                    const uint32_t p = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
-                                       (to_i8(v.w, bad) << 24);
                     const int r = c / CPR;
+                    bool bad = false;
+                    uint32_t p = 0;
+                    if (!LIVE || live(r, c - r * CPR)) {
+                        const int4 v = src[u * WAVE];
+                        p = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) | (to_i8(v.w, bad) << 24);
+                    }
                     lds[r * S + (c - r * CPR)] = p;
                     if (bad) flags[r] = 1;
                     any_bad |= bad;
@@ -649,7 +701,9 @@ struct FastTile {
     // value in HBM (a gated move, an unchanged relator, a failed env).  Needs set_dirty for every
     // row of the tile and a wave_sync after it.  Dirty rows flagged FB_RESET (an autoreset to an
     // out-of-domain starting row) are copied from fallback2 (same row pitch).
-    template <bool NT>
+    // LIVE: a dirty relator's chunks past lim[] (the live chunks of its old and new letters, set
+    // by the caller) already hold zero padding in HBM and are not written
+    template <bool NT, bool LIVE = false>
     __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -661,7 +715,7 @@ struct FastTile {
                 const int k = c - r * CPR;
                 if (!((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u)) continue;
                 if (flags[r] == FB_RESET) dst[c] = reinterpret_cast<const int4*>(fallback2)[c];
-                else dst[c] = widen4(lds[r * S + k]);
+                else if (!LIVE || live(r, k)) dst[c] = widen4(lds[r * S + k]);
             }
             return;
         }
@@ -676,7 +730,7 @@ struct FastTile {
                 if (u0 + u < CPR && c < nc) {
                     const int r = c / CPR;
                     const int k = c - r * CPR;
-                    wr[u] = (dirty[r] >> (k >= HALF ? 1 : 0)) & 1u;
+                    wr[u] = ((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u) && (!LIVE || live(r, k));
                     if (wr[u]) p[u] = lds[r * S + k];
                 }
             }
@@ -720,9 +774,12 @@ struct CodeTile {
     uint32_t* lds;
     uint8_t* flags;
     uint8_t* dirty;  // see FastTile
+    uint8_t* lim;    // see FastTile
+    uint32_t limv = 0;  // this lane's row's live chunk counts, lim0 | lim1 << 8 (set_lim)
+    uint32_t dirtyv = 0;  // this lane's row's dirty bits (set_dirty)
     bool tile_bad = false;
 
-    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 2 * WAVE; }
+    static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
     __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
         flags[lane] = (uint8_t)code;
@@ -742,6 +799,32 @@ struct CodeTile {
         lds = reinterpret_cast<uint32_t*>(base);
         flags = reinterpret_cast<uint8_t*>(base + WAVE * S * 4);
         dirty = flags + WAVE;
+        lim = flags + 2 * WAVE;
+    }
+    // see FastTile::set_lim / live (chunks of 4 letters; HALF chunks per relator)
+    __device__ __forceinline__ void set_lim(int lane, int n0, int n1) {
+        lim[2 * lane] = (uint8_t)live_chunks(n0);
+        lim[2 * lane + 1] = (uint8_t)live_chunks(n1);
+        limv = (uint32_t)live_chunks(n0) | ((uint32_t)live_chunks(n1) << 8);
+    }
+    // see FastTile::widen_lim
+    __device__ __forceinline__ void widen_lim(int lane, int n0, int n1) {
+        const int a = max((int)(limv & 0xffu), live_chunks(n0)), b = max((int)(limv >> 8), live_chunks(n1));
+        lim[2 * lane] = (uint8_t)a;
+        lim[2 * lane + 1] = (uint8_t)b;
+        limv = (uint32_t)a | ((uint32_t)b << 8);
+    }
+    // CPR == WAVE (one row per wave-instruction): chunk ln of row u is live, row u's counts read
+    // from lane u's register (a scalar per compile-time u; no LDS read, no per-u VGPR)
+    __device__ __forceinline__ bool live_lane(int u, int ln) const {
+        const int lu = __builtin_amdgcn_readlane((int)limv, u);
+        const int l0 = lu & 0xff, l1 = (lu >> 8) & 0xff;  // scalars
+        return ln < l0 || (ln >= HALF && ln < HALF + l1);  // l0 <= HALF
+    }
+    __device__ __forceinline__ static int live_chunks(int n) { return n <= 0 ? 0 : n >= L ? HALF : (n + 3) >> 2; }
+    __device__ __forceinline__ bool live(int r, int k) const {
+        const int h = k >= HALF ? 1 : 0;
+        return k - h * HALF < lim[2 * r + h];
     }
     __device__ __forceinline__ int Lr() const { return L; }
     __device__ __forceinline__ uint16_t* slots(int r) const { return reinterpret_cast<uint16_t*>(lds + r * S); }
@@ -757,7 +840,7 @@ struct CodeTile {
 
     // PIPE (the step kernel; the rollout keeps the plain loop, whose register budget the
     // in-flight batch pair would exceed): full tiles software-pipelined, see below
-    template <bool PIPE = false>
+    template <bool PIPE = false, bool LIVE = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -766,25 +849,98 @@ struct CodeTile {
         const int nc = R * CPR;
         const int4* src = reinterpret_cast<const int4*>(g) + ln;
         bool any_bad = false;
+#if ACX_FAST_CONVERT
+        if constexpr (CPR == WAVE) {
+            if (PIPE && R == WAVE) {
+                // full tile, one row per wave-instruction (row u, lane ln = its chunk ln):
+                // software-pipelined as below; each chunk is converted by chunk_i8 and stored at
+                // the lane's fixed slot address (row u at a compile-time offset).  Rows with a
+                // letter outside {-2..2} (error inputs only) are found afterwards, when some
+                // chunk was bad: each lane rescans its own row's loaded chunks
+                int4 va[LOAD_BATCH], vb[LOAD_BATCH];
+                uint16_t* mine = reinterpret_cast<uint16_t*>(lds) + ln;
+                auto lv = [&](int u) {
+                    if constexpr (!LIVE) return true;
+                    else return live_lane(u, ln);
+                };
+                auto issue = [&](int4* v, int u0) {
+#pragma unroll
+                    for (int u = 0; u < LOAD_BATCH; ++u)
+                        if (lv(u0 + u)) v[u] = src[(u0 + u) * WAVE];
+                };
+                auto convert = [&](const int4* v, int u0) {
+#pragma unroll
+                    for (int u = 0; u < LOAD_BATCH; ++u) {
+                        bool bad = false;
+                        uint32_t slot = 0;
+                        if (lv(u0 + u)) {
+                            uint32_t c8, nz4;
+                            swar_pack4(chunk_i8(v[u], bad), c8, nz4);
+                            slot = c8 | (nz4 << 8);
+                        }
+                        mine[(u0 + u) * 2 * S] = (uint16_t)slot;
+                        any_bad |= bad;
+                    }
+                };
+                static_assert(CPR % (2 * LOAD_BATCH) == 0, "pipelined tile load: whole batch pairs");
+                issue(va, 0);
+#pragma unroll
+                for (int u0 = 0; u0 < CPR; u0 += 2 * LOAD_BATCH) {
+                    issue(vb, u0 + LOAD_BATCH);
+                    convert(va, u0);
+                    if (u0 + 2 * LOAD_BATCH < CPR) issue(va, u0 + 2 * LOAD_BATCH);
+                    convert(vb, u0 + LOAD_BATCH);
+                }
+                tile_bad = __any(any_bad);
+                if (tile_bad) {  // rare (wave-uniform)
+                    bool rb = false;
+                    const int32_t* row = g + (int64_t)ln * twoL;
+                    for (int k = 0; k < CPR; ++k) {
+                        bool in = true;
+                        if constexpr (LIVE) in = live(ln, k);
+                        if (!in) continue;
+                        const int4 v = reinterpret_cast<const int4*>(row)[k];
+                        bool b = false;
+                        chunk_i8(v, b);
+                        rb |= b;
+                    }
+                    flags[ln] = rb ? 1 : 0;
+                }
+                wave_sync();
+                return;
+            }
+        }
+#endif
         if (PIPE && R == WAVE) {
             // full tile (wave-uniform): software-pipelined, batch b + 1's loads are issued before
             // batch b is converted, so LOAD_BATCH..2*LOAD_BATCH loads stay in flight through the
             // whole 64 KB tile (L = 128) instead of draining to zero between batches
+            // LIVE: a wave-instruction u covers row u (CPR == WAVE), lane ln its chunk ln
             int4 va[LOAD_BATCH], vb[LOAD_BATCH];
+            auto lv = [&](int u) {
+                if constexpr (!LIVE) return true;
+                else if constexpr (CPR == WAVE) return live_lane(u, ln);
+                else return live((ln + u * WAVE) / CPR, (ln + u * WAVE) % CPR);
+            };
             auto issue = [&](int4* v, int u0) {
 #pragma unroll
-                for (int u = 0; u < LOAD_BATCH; ++u) v[u] = src[(u0 + u) * WAVE];
+                for (int u = 0; u < LOAD_BATCH; ++u)
+                    if (lv(u0 + u)) v[u] = src[(u0 + u) * WAVE];
             };
             auto convert = [&](const int4* v, int u0) {
 #pragma unroll
                 for (int u = 0; u < LOAD_BATCH; ++u) {
                     const int c = ln + (u0 + u) * WAVE;
                     bool bad = false;
-                    const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
-                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
-                    uint32_t c8, nz4;
-                    swar_pack4(d, c8, nz4);
-                    put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+                    uint32_t slot = 0;
+                    if (lv(u0 + u)) {
+                        const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
+                                           (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                        uint32_t c8, nz4;
+                        swar_pack4(d, c8, nz4);
+                        slot = c8 | (nz4 << 8) | ((uint32_t)bad << 12);
+                    }
+                    put(c, slot);
                     if (bad) flags[c / CPR] = 1;
                     any_bad |= bad;
                 }
@@ -804,19 +960,27 @@ struct CodeTile {
         }
         for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
             int4 v[LOAD_BATCH];
+            bool lv[LOAD_BATCH];
 #pragma unroll
-            for (int u = 0; u < LOAD_BATCH; ++u)
-                if (ln + (u0 + u) * WAVE < nc) v[u] = src[(u0 + u) * WAVE];
+            for (int u = 0; u < LOAD_BATCH; ++u) {
+                const int c = ln + (u0 + u) * WAVE;
+                lv[u] = c < nc && (!LIVE || live(c / CPR, c % CPR));
+                if (lv[u]) v[u] = src[(u0 + u) * WAVE];
+            }
 #pragma unroll
             for (int u = 0; u < LOAD_BATCH; ++u) {
                 const int c = ln + (u0 + u) * WAVE;
                 if (c < nc) {
                     bool bad = false;
-                    const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
-                                       (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
-                    uint32_t c8, nz4;
-                    swar_pack4(d, c8, nz4);
-                    put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
+                    uint32_t slot = 0;
+                    if (lv[u]) {
+                        const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
+                                           (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
+                        uint32_t c8, nz4;
+                        swar_pack4(d, c8, nz4);
+                        slot = c8 | (nz4 << 8) | ((uint32_t)bad << 12);
+                    }
+                    put(c, slot);
                     if (bad) flags[c / CPR] = 1;
                     any_bad |= bad;
                 }
@@ -1112,10 +1276,13 @@ struct CodeTile {
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PresRegs<NW>& p) const {
         return unpack_impl<true>(lane, p);
     }
-    __device__ __forceinline__ void set_dirty(int lane, uint32_t m) const { dirty[lane] = (uint8_t)m; }
+    __device__ __forceinline__ void set_dirty(int lane, uint32_t m) {
+        dirty[lane] = (uint8_t)m;
+        dirtyv = m;
+    }
 
     // see FastTile::store_dirty
-    template <bool NT>
+    template <bool NT, bool LIVE = false>
     __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -1128,13 +1295,42 @@ struct CodeTile {
                 if (!((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u)) continue;
                 if (flags[r] == FB_RESET) {
                     dst[c] = reinterpret_cast<const int4*>(fallback2)[c];
-                } else {
+                } else if (!LIVE || live(r, k)) {
                     const uint32_t sl = slots(r)[k];
                     dst[c] = widen4(codes_to_i8x4(sl & 0xffu, 8u * __builtin_popcount((sl >> 8) & 0xfu)));
                 }
             }
             return;
         }
+#if ACX_FAST_CONVERT
+        if constexpr (CPR == WAVE) {
+            // one row per wave-instruction (row r, lane ln = its chunk ln): the lane's fixed slot
+            // address, row r's dirty bits and live counts read from lane r's registers (scalars)
+            const uint16_t* mine = reinterpret_cast<const uint16_t*>(lds) + ln;
+            const int hs = ln >= HALF ? 1 : 0;
+            for (int r0 = 0; r0 < R; r0 += STAGE_UNROLL) {
+                uint32_t p[STAGE_UNROLL];
+                bool wr[STAGE_UNROLL];
+#pragma unroll
+                for (int u = 0; u < STAGE_UNROLL; ++u) {
+                    const int r = r0 + u;
+                    const uint32_t dr = (uint32_t)__builtin_amdgcn_readlane((int)dirtyv, r);
+                    bool lv = true;
+                    if constexpr (LIVE) lv = live_lane(r, ln);
+                    wr[u] = r < R && ((dr >> hs) & 1u) && lv;
+                    if (wr[u]) p[u] = mine[r * 2 * S];
+                }
+#pragma unroll
+                for (int u = 0; u < STAGE_UNROLL; ++u) {
+                    if (!wr[u]) continue;
+                    const uint32_t nz4 = (p[u] >> 8) & 0xfu;
+                    out16<NT, false>(dst + ln + (r0 + u) * WAVE,
+                                     widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
+                }
+            }
+            return;
+        }
+#endif
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
             bool wr[STAGE_UNROLL];
@@ -1145,7 +1341,9 @@ struct CodeTile {
                 if (c < nc) {
                     const int r = c / CPR;
                     const int k = c - r * CPR;
-                    wr[u] = (dirty[r] >> (k >= HALF ? 1 : 0)) & 1u;
+                    bool lv = true;
+                    if constexpr (LIVE) lv = (CPR == WAVE) ? live_lane(u0 + u, ln) : live(r, k);
+                    wr[u] = ((dirty[r] >> (k >= HALF ? 1 : 0)) & 1u) && lv;
                     if (wr[u]) p[u] = slots(r)[k];
                 }
             }
@@ -1267,7 +1465,8 @@ struct GenericTile {
         }
     };
 
-    template <bool PIPE = false>  // see CodeTile::load (not used by the runtime-L path)
+    // PIPE, LIVE: see CodeTile::load (the runtime-L path reads and writes whole rows)
+    template <bool PIPE = false, bool LIVE = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         flags[lane] = 0;
         wave_sync();
@@ -1442,7 +1641,9 @@ struct GenericTile {
         return 3u;
     }
     __device__ __forceinline__ void set_dirty(int, uint32_t) const {}
-    template <bool NT>
+    __device__ __forceinline__ void set_lim(int, int, int) const {}  // whole rows (see FastTile)
+    __device__ __forceinline__ void widen_lim(int, int, int) const {}
+    template <bool NT, bool LIVE = false>
     __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
         store<true>(g, twoL, R, g, twoL, lane, fallback2);
     }
@@ -1553,11 +1754,15 @@ struct StepArgs {
     // next-step autoreset (acx_step_next; NULL: same-step): per env, its episode ended on the
     // previous call -- this call resets it instead of stepping, and records whether it ends now
     uint8_t* pending;
+    // lengths-carrying step (acx_step_lengths): lengths_out holds the rows' relator lengths on
+    // entry (canonical rows), so only their letters are read and written
+    int live;
 };
 
-// LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path)
-template <int NW, int LC, int VEC, bool LEARN>
-__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
+// LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
+// LIVE: the lengths-carrying step (its own kernel, so the plain step's registers stay its own)
+template <int NW, int LC, int VEC, bool LEARN, bool LIVE>
+__device__ __forceinline__ void step_body(const StepArgs& a) {
     using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
@@ -1580,7 +1785,18 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
         cnt_in = a.step_count ? a.step_count[env] : 0;
     }
 #endif
-    tile.template load<ACX_PIPE_LOAD != 0>(a.state_in + w.r0 * twoL, w.R, w.lane);
+    if constexpr (LIVE) {
+        int n_in0 = 0, n_in1 = 0;  // the rows' relator lengths on entry
+        if (w.active) {
+            n_in0 = a.lengths_out[2 * env];
+            n_in1 = a.lengths_out[2 * env + 1];
+        }
+        tile.set_lim(w.lane, n_in0, n_in1);
+        wave_sync();
+        tile.template load<ACX_PIPE_LOAD != 0, true>(a.state_in + w.r0 * twoL, w.R, w.lane);
+    } else {
+        tile.template load<ACX_PIPE_LOAD != 0>(a.state_in + w.r0 * twoL, w.R, w.lane);
+    }
 
     bool fin = false;    // done | truncated (the curriculum's "finished")
     bool reset = false;  // same-step autoreset of this env
@@ -1677,8 +1893,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     if (w.active) {
         if (a.step_count) a.step_count[env] = cnt;
         if (a.lengths_out) {
-            a.lengths_out[2 * env] = p.n0;
-            a.lengths_out[2 * env + 1] = p.n1;
+            // lengths-carrying step: an out-of-domain row is read whole on the next call (L, L)
+            const bool whole = LIVE && e == ACX_ERR_DOMAIN;
+            a.lengths_out[2 * env] = whole ? L : p.n0;
+            a.lengths_out[2 * env + 1] = whole ? L : p.n1;
         }
         if (a.err) a.err[env] = (uint8_t)e;
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
@@ -1692,11 +1910,18 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     }
     if (a.in_place) {
         // state_out == state_in: write only the relators that changed (a gated move, a
-        // cyclic conjugation that is a no-op and a failed env leave their row as it is in HBM)
+        // cyclic conjugation that is a no-op and a failed env leave their row as it is in HBM);
+        // lengths-carrying: of those, only the chunks inside the old or the new letters
         tile.set_dirty(w.lane, dm);
+        if constexpr (LIVE) tile.widen_lim(w.lane, p.n0, p.n1);
         wave_sync();
-        if (__ballot(dm != 0u))
-            tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
+        if (__ballot(dm != 0u)) {
+            if constexpr (LIVE)
+                tile.template store_dirty<false, true>(a.state_out + w.r0 * twoL, w.R, w.lane,
+                                                       a.reset_state + w.r0 * twoL);
+            else
+                tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
+        }
     } else {
         wave_sync();
         tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane,
@@ -1705,6 +1930,18 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
+}
+
+template <int NW, int LC, int VEC, bool LEARN>
+__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
+    step_body<NW, LC, VEC, LEARN, false>(a);
+}
+// acx_step_lengths (in place, lengths in and out).  At L = 128 the tile's LDS allows 4 waves per
+// SIMD; the live-chunk predicates took the register count just past 128 VGPRs (3 waves), so
+// the allocator is held to 4
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK, LC == 128 ? 4 : Occupancy<LC>::waves_per_simd) void step_lengths_kernel(StepArgs a) {
+    step_body<NW, LC, VEC, false, true>(a);
 }
 
 // the first half of a FastTile row's chunk slots, rounded to whole store batches
@@ -2522,7 +2759,10 @@ static inline unsigned grid_for(int64_t rows) {
 template <int NW, int LC, int VEC, bool LEARN>
 int launch_step(StepArgs a, hipStream_t s) {
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-    step_kernel<NW, LC, VEC, LEARN><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+    if (!LEARN && a.live)
+        step_lengths_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+    else
+        step_kernel<NW, LC, VEC, LEARN><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }
 template <int NW, int LC, int VEC, int OBS>
@@ -2698,6 +2938,22 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
     StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated,
                lengths_out, final_obs, err, err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                B, L, horizon, cyclical, 0};
+    StepLaunch f{a, (hipStream_t)stream, false};
+    return dispatch(L, f);
+}
+
+int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset_state, int32_t* step_count,
+                     int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths, int32_t* final_obs,
+                     uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical,
+                     void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state || !action || !lengths) return ACX_E_ARG;
+    if (!aligned16(state)) return ACX_E_ARG;
+    if (reset_state && !step_count) return ACX_E_ARG;
+    StepArgs a{state, state, action, reset_state, step_count, reward, done, truncated, lengths, final_obs, err,
+               err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, B, L, horizon, cyclical, 0};
+    a.live = 1;
     StepLaunch f{a, (hipStream_t)stream, false};
     return dispatch(L, f);
 }

@@ -614,16 +614,67 @@ def run_rank(args):
                                        "(in place: unchanged relators are not written)"},
             "env_errors": n_err_api,
         }
+        # the same walk through the lengths-carrying step (acx_step_lengths, VecACEnv.step's
+        # path): lengths in and out, so only the chunks inside each relator's letters are read
+        # and only those inside the old or new letters of a changed relator written
+        st2 = starts.clone()
+        cnt2 = torch.zeros(B, dtype=torch.int32, device=dev)
+        lens2 = torch.full((B, 2), L, dtype=torch.int32, device=dev)  # (L, L): read whole, once
+
+        def step2(a):
+            ops.step(st2, a, state_out=st2, reset_state=starts, step_count=cnt2, horizon=H, cyclical=True,
+                     reward=rew1, done=dn1, truncated=tr1, lengths=lens2, err=err, err_count=err_count,
+                     lengths_in=True)
+
+        err_count.zero_()
+        for t in range(W):
+            step2(actions[t])
+
+        def go_steps2():
+            for t in range(K):
+                step2(actions[W + t])
+
+        wall_len, s_len, wall_len_local = timed(go_steps2)
+        n_err_len = int(err_count.item())
+        # algorithmic bytes of this path, measured off the clock over the next 8 steps of the
+        # walk: per relator, its live 16-byte chunks read (ceil(n/4)), and for a changed relator
+        # the chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars
+        rd = wr = 0.0
+        for t in range(8):
+            before, n_before = st2.clone(), lens2.clone()
+            step2(actions[(W + K + t) % actions.shape[0]])
+            ch = (before.view(B, 2, L) != st2.view(B, 2, L)).any(2)
+            c_old = (n_before.clamp(0, L) + 3) // 4
+            c_new = (lens2.clamp(0, L) + 3) // 4
+            rd += float(c_old.sum().item()) * 16 / B
+            wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16 / B
+            del before, n_before
+        rd, wr = rd / 8, wr / 8
+        sb_len = rd + wr + 16 + 27
+        same = bool(torch.equal(st1, st2))  # both walks took the same 8 + K + W steps
+        len_kernel = f"acx::step_lengths_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>"
+        a_len = B * sb_len / (s_len / K) / 1e9
+        variants["step_api_lengths"] = {
+            "value": seen * B * K / wall_len, "unit": "env-steps/s", "ms_per_step": wall_len / K * 1e3,
+            "kernel_ms": s_len * 1e3, "env_errors": n_err_len, "same_states_as_step_api": same,
+            "roofline": {"bound": "hbm", "achieved": a_len, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
+                         "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
+                         "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
+                                       "chunks inside old or new letters written, lengths 16 B + 27 B of scalars"},
+            "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
+        }
         if not rollout_head:
-            a_api = B * sb / (s_api / K) / 1e9
             head = {
-                "elapsed": wall_api, "kernel_s": s_api, "wall_local": wall_api_local, "frac": a_api / HBM_PEAK_GBS,
-                "roofline": dict(variants["step_api"]["roofline"], kernel_ms=s_api * 1e3, launches=K,
-                                 launch_bytes=B * sb),
-                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step, {B} envs/GPU, L={L}, "
-                             f"horizon {H}, cyclical=True, in-place state, same-step autoreset; {K} launches"),
-                "env_errors": n_err_api,
+                "elapsed": wall_len, "kernel_s": s_len, "wall_local": wall_len_local, "frac": a_len / HBM_PEAK_GBS,
+                "roofline": dict(variants["step_api_lengths"]["roofline"], kernel_ms=s_len * 1e3, launches=K,
+                                 launch_bytes=B * sb_len),
+                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step_lengths (the env's "
+                             f"step, ACMove's lengths in/out), {B} envs/GPU, L={L}, horizon {H}, cyclical=True, "
+                             f"in-place state, same-step autoreset; {K} launches"),
+                "env_errors": n_err_len,
             }
+        del st2, cnt2, lens2
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
         # the ctypes launches on the capture stream) and replayed: no per-launch host cost

@@ -100,6 +100,21 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
              void* stream);
 
 /*
+ * acx_step in place, carrying the rows' relator lengths (ACMove takes and returns them,
+ * ac_moves.py:159,184,231): lengths (B,2) int32, in/out, holds each row's relator lengths on
+ * entry and its new lengths on exit, so the kernel reads only the 16-byte chunks inside each
+ * relator's letters and writes only those inside its old or new letters (the padding past both
+ * already holds zeros).  Rows must be canonical (letters, then zero padding) with exact lengths;
+ * (L, L) is always safe and means "read the whole row" (the next call writes the exact lengths).
+ * An out-of-domain row (ACX_ERR_DOMAIN) gets (L, L).  Other arguments as acx_step; lengths is
+ * required.
+ */
+int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset_state, int32_t* step_count,
+                     int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths, int32_t* final_obs,
+                     uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical,
+                     void* stream);
+
+/*
  * acx_step for the PPO learner (ac_solver/agents/training.py:221-356), state updated in place
  * with same-step autoreset to reset_state, plus the learner-side writes fused in:
  *   action / action_i64 : exactly one non-NULL; action_i64 = the policy's int64 samples

@@ -74,6 +74,19 @@ def test_host_utils_match_reference_cases():
     assert q.tolist() == [1, 2, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0]
 
 
+def test_row_extent_covers_every_letter():
+    """VecACEnv's lengths for acx_step_lengths: the relator lengths of canonical rows, and for a
+    row with a gap or an out-of-domain letter an extent reaching its last non-zero entry (so
+    the lengths-carrying step reads it and flags it as acx_step does)."""
+    from acx.envs.ac_env import _row_extent
+    L = 6
+    rows = torch.tensor([[1, 2, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0],
+                         [0, 0, 0, 0, 0, 0, 2, -1, 2, -1, 2, -1],
+                         [1, 0, 0, 0, 3, 0, 1, 0, 2, 0, 0, 0]], dtype=torch.int32)
+    assert _row_extent(rows, L).tolist() == [[2, 1], [0, 6], [5, 3]]
+    assert _row_extent(rows, L).dtype == torch.int32
+
+
 def test_acenvconfig_validation():
     from acx import ACEnvConfig
     c = ACEnvConfig()

@@ -49,10 +49,14 @@ def test_bench_line_short_launch_reads_int32_ids():
 
 def test_bench_step_workload_headline():
     # config 5's shape (--workload step) at a small batch: the per-call step API is the headline
+    # (the lengths-carrying acx_step_lengths; acx_step on the same walk is a variant)
     d = _bench("--workload", "step", "--L", "128", "--batch", "8192", "--steps", "12", "--warmup", "2", "--no-cpu",
                "--no-bfs", "--no-learner", "--no-search")
     assert d["n_gpus"] == 1 and d["world_size_seen"] == 1 and d["env_errors"] == 0
-    assert d["roofline"]["kernel"] == "acx::step_kernel<8,128,4,false>" and d["roofline"]["launches"] == 12
+    assert d["roofline"]["kernel"] == "acx::step_lengths_kernel<8,128,4>" and d["roofline"]["launches"] == 12
+    v = d["variants"]
+    assert v["step_api"]["roofline"]["kernel"] == "acx::step_kernel<8,128,4,false>"
+    assert v["step_api_lengths"]["same_states_as_step_api"] and v["step_api_lengths"]["env_errors"] == 0
     assert "random-action stepping" in d["config"]["workload"]
     assert "rollout_obs_int8" not in d["variants"] and "step_api_hipgraph" in d["variants"]
 

@@ -1,0 +1,140 @@
+"""GPU: the lengths-carrying step (acx_step_lengths: in place, the rows' relator lengths in and
+out, only the chunks inside the letters read and written) against acx_step on the same rows,
+actions and starting states, many steps: states, rewards, flags, step counts, final
+observations, errors and lengths bit-exact.  acx_step is itself pinned to the reference's
+fixtures (test_gpu_parity.py); VecACEnv's plain step goes through acx_step_lengths, so the
+env-level golden replays (test_gpu_parity.py::test_vec_env_matches_golden_episodes and the
+oracle-model tests) cover it too."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _rows(L, B, rng):
+    """canonical rows of mixed lengths (0 .. L letters per relator), a tenth trivial"""
+    s = np.zeros((B, 2 * L), np.int32)
+    letters = np.array([1, -1, 2, -2], np.int32)
+    for b in range(B):
+        for h in range(2):
+            n = int(rng.integers(1, L + 1)) if b % 10 else 1
+            w = []
+            while len(w) < n:  # freely reduced
+                x = int(letters[rng.integers(0, 4)])
+                if w and w[-1] == -x:
+                    continue
+                w.append(x)
+            if b % 10 == 0:
+                w = [1 + h]
+            s[b, h * L:h * L + n] = w
+    return s
+
+
+def _t(x):
+    return torch.as_tensor(np.ascontiguousarray(x)).to(DEV)
+
+
+@pytest.mark.parametrize("L", [36, 128, 18, 64])
+@pytest.mark.parametrize("cyc", [0, 1])
+def test_step_lengths_matches_acx_step(L, cyc):
+    from acx import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(L * 7 + cyc)
+    B, T, H = 64 * 37 + 11, 40, 9
+    start = _rows(L, B, rng)
+    reset = _rows(L, B, rng)
+    reset[5::97, 3] = 3  # out-of-domain starting rows: envs that reset onto them become ACX_ERR_DOMAIN
+    n_ood = len(range(5, B, 97))
+    st = {k: _t(start) for k in "ab"}
+    rs = _t(reset)
+    cnt = {k: torch.zeros(B, dtype=torch.int32, device=DEV) for k in "ab"}
+    rew = {k: torch.zeros(B, dtype=torch.int32, device=DEV) for k in "ab"}
+    dn = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    tr = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    fo = {k: torch.zeros((B, 2 * L), dtype=torch.int32, device=DEV) for k in "ab"}
+    err = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    ec = {k: torch.zeros(1, dtype=torch.int32, device=DEV) for k in "ab"}
+    lens_a = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
+    lens_b = _t(np.stack([np.count_nonzero(start[:, :L], 1), np.count_nonzero(start[:, L:], 1)], 1).astype(np.int32))
+    lens_b[::13] = L  # (L, L): "read the whole row", always safe
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    n_reset = n_err = 0
+    for t in range(T):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        if t % 7 == 3:
+            a[::211] = 12  # ACX_ERR_ACTION: the row is left as it is
+        at = _t(a)
+        for k in "ab":
+            P = lambda x: x[k].data_ptr()  # noqa: E731
+            if k == "a":
+                rc = lib.acx_step(P(st), P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
+                                  lens_a.data_ptr(), P(fo), P(err), P(ec), B, L, H, cyc, stream)
+            else:
+                rc = lib.acx_step_lengths(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
+                                          lens_b.data_ptr(), P(fo), P(err), P(ec), B, L, H, cyc, stream)
+            assert rc == 0, (k, rc)
+        for name, d in (("state", st), ("reward", rew), ("done", dn), ("trunc", tr), ("count", cnt),
+                        ("final_obs", fo), ("err", err), ("err_count", ec)):
+            assert torch.equal(d["a"], d["b"]), (t, name)
+        e = err["a"].cpu().numpy()
+        dom = e == 3
+        la, lb = lens_a.cpu().numpy(), lens_b.cpu().numpy()
+        assert np.array_equal(la[~dom], lb[~dom]), t
+        assert (lb[dom] == L).all(), t  # out-of-domain rows are read whole on the next call
+        # the lengths are the rows' own (canonical rows: letters, then zero padding)
+        s = st["b"].cpu().numpy()
+        ok = ~dom
+        assert np.array_equal(lb[ok, 0], np.count_nonzero(s[ok, :L], 1)), t
+        assert np.array_equal(lb[ok, 1], np.count_nonzero(s[ok, L:], 1)), t
+        n_reset += int((dn["a"] | tr["a"]).sum())
+        n_err += int((e != 0).sum())
+    assert n_reset > B and n_err > n_ood  # resets, out-of-domain resets and failed moves exercised
+
+
+def test_step_lengths_rejects_missing_lengths():
+    from acx import _lib
+    lib = _lib.load()
+    L, B = 36, 64
+    s = _t(_rows(L, B, np.random.default_rng(0)))
+    a = torch.zeros(B, dtype=torch.int32, device=DEV)
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    rc = lib.acx_step_lengths(s.data_ptr(), a.data_ptr(), None, None, None, None, None, None, None, None, None,
+                              B, L, 5, 1, stream)
+    assert rc == _lib.E_ARG
+
+
+def test_vec_env_lengths_after_rollout_and_direct_writes():
+    """VecACEnv keeps lengths current across steps; a rollout (no lengths out) and reset_env
+    hand over correctly: the env matches a twin stepped one move at a time with acx_step."""
+    from acx import VecACEnv, _lib
+    L, B, H = 36, 64 * 5 + 3, 8
+    rng = np.random.default_rng(3)
+    start = _rows(L, B, rng)
+    env = VecACEnv(start, horizon_length=H, device=DEV)
+    twin = VecACEnv(start, horizon_length=H, device=DEV)
+    twin._lengths_ok = False  # the twin always takes acx_step (it rewrites its lengths each call)
+    T = 6
+    acts = rng.integers(0, 12, size=(T + 4, B)).astype(np.int32)
+    env.rollout(_t(acts[:T]))
+    assert not env._lengths_ok
+    for t in range(T):
+        twin.step(_t(acts[t]))
+        twin._lengths_ok = False
+    assert torch.equal(env.state, twin.state)
+    new = _rows(L, 1, rng)[0]
+    env.reset_env(7, new)
+    twin.reset_env(7, new)
+    for t in range(T, T + 4):
+        o1, r1, d1, t1, _ = env.step(_t(acts[t]))
+        assert env._lengths_ok
+        o2, r2, d2, t2, _ = twin.step(_t(acts[t]))
+        twin._lengths_ok = False
+        for x, y in ((o1, o2), (r1, r2), (d1, d2), (t1, t2), (env.step_count, twin.step_count)):
+            assert torch.equal(x, y), t
+        assert torch.equal(env.lengths, twin.lengths), t
+    assert _lib.E_ARG < 0

@@ -8,6 +8,11 @@ leave the same state / counts / rewards (checksums).  Bytes per env-step as benc
 step_api (state read 8L + changed relators x 4L + 27 B), with the changed-relator rate measured.
 
     python tools/ab_step.py abv/libacx_a.so abv/libacx_b.so ... [--L 128] [--K 20] [--reps 5] [--ceiling]
+
+An entry LIB@lengths steps through acx_step_lengths (the rows' lengths carried from call to call,
+set from the rows before the warmup), LIB@LL through acx_step_lengths with every row's lengths
+reset to (L, L) -- "read the whole row" -- before each call (the refill is a separate timed
+launch, reported apart): the cost of the lengths dependency without the byte saving.
 """
 import argparse
 import ctypes
@@ -32,6 +37,8 @@ PEAK = 8000.0
 def load(path):
     lib = ctypes.CDLL(os.path.abspath(path))
     lib.acx_step.argtypes = [P] * 12 + [I64, I32, I32, I32, P]
+    if hasattr(lib, "acx_step_lengths"):
+        lib.acx_step_lengths.argtypes = [P] * 11 + [I64, I32, I32, I32, P]
     return lib
 
 
@@ -94,7 +101,10 @@ def main():
     out = {"L": L, "B": B, "K": K}
     if a.ceiling:
         out["ceilings"] = ceilings(L, B, a.reps, dev)
-    libs = [(os.path.basename(p), load(p)) for p in a.libs]
+    libs = []
+    for p in a.libs:
+        path, _, mode = p.partition("@")
+        libs.append((os.path.basename(path) + (f"@{mode}" if mode else ""), (load(path), mode or "full")))
     if libs:
         starts = torch.as_tensor(ms_starts(L, B)).to(dev)
         g = torch.Generator(device=dev)
@@ -110,10 +120,18 @@ def main():
         ec = torch.zeros(1, dtype=torch.int32, device=dev)
         s = torch.cuda.current_stream().cuda_stream
 
-        def step(lib, t):
-            rc = lib.acx_step(st.data_ptr(), st.data_ptr(), acts[t].data_ptr(), starts.data_ptr(), cnt.data_ptr(),
-                              rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), lens.data_ptr(), None, err.data_ptr(),
-                              ec.data_ptr(), B, L, H, 1, s)
+        def step(lm, t):
+            lib, mode = lm
+            if mode == "full":
+                rc = lib.acx_step(st.data_ptr(), st.data_ptr(), acts[t].data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                  rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), lens.data_ptr(), None, err.data_ptr(),
+                                  ec.data_ptr(), B, L, H, 1, s)
+            else:
+                if mode == "LL":
+                    lens.fill_(L)
+                rc = lib.acx_step_lengths(st.data_ptr(), acts[t].data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                          rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), lens.data_ptr(), None,
+                                          err.data_ptr(), ec.data_ptr(), B, L, H, 1, s)
             assert rc == 0, rc
 
         ms = {n: [] for n, _ in libs}
@@ -124,6 +142,8 @@ def main():
                 st.copy_(starts)
                 cnt.zero_()
                 ec.zero_()
+                nz = st.view(B, 2, L) != 0
+                lens.copy_((nz * torch.arange(1, L + 1, device=dev, dtype=torch.int32)).amax(2))
                 for t in range(W):
                     step(lib, t)
                 torch.cuda.synchronize()
@@ -146,6 +166,15 @@ def main():
                         step(lib, t)
                         c += float((before.view(B, 2, L) != st.view(B, 2, L)).any(2).sum().item()) / B
                     chg = c / 8
+        # the (L, L) refill alone (the LL entries' per-call extra launch)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(K):
+            lens.fill_(L)
+        e1.record()
+        torch.cuda.synchronize()
+        out["LL_refill_ms"] = round(e0.elapsed_time(e1) / K, 4)
         sb = 8 * L + 27 + 4 * L * chg
         out["changed_relators_per_env_step"] = chg
         out["bytes_per_env_step"] = sb

@@ -118,10 +118,13 @@ if bench:
         })
         summary["rollout_timed_dispatch"] = rec
 if bench and "random-action stepping" in bench["config"]["workload"]:
-    # bench.py --workload step: the headline is K per-call acx_step launches after W warmup
-    # calls (then 8 off-the-clock calls for the changed-relator rate, then the hipGraph ones)
+    # bench.py --workload step: the headline is K per-call acx_step_lengths launches after W
+    # warmup calls (then 8 off-the-clock calls for the live-byte rate); before round 4's
+    # lengths-carrying step it was acx_step's (step_kernel<.., false>)
     import re
-    steps = [(n, v) for n, v in summary["kernels"].items() if re.search(r"step_kernel<\d+, \d+, \d+, false>", n)]
+    pat = (r"step_lengths_kernel<\d+, \d+, \d+>" if "step_lengths_kernel" in bench["roofline"].get("kernel", "")
+           else r"step_kernel<\d+, \d+, \d+, false>")
+    steps = [(n, v) for n, v in summary["kernels"].items() if re.search(pat, n)]
     if steps:
         kname, k = max(steps, key=lambda nv: nv[1]["dispatches"])
         W, K = bench["warmup"], bench["steps"]
