@@ -258,6 +258,9 @@ class VecACEnv:
         # them (rollout, direct writes by a learner), and the next step uses acx_step, which rewrites them
         self.lengths = _row_extent(self.state, L).contiguous()
         self._lengths_ok = True
+        # the compile-time tiles (L = 36, 128) read only the live chunks; at any other L the
+        # kernel reads whole rows either way, so the plain step is taken
+        self._live_tile = L in ops.LIVE_TILE_L
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
         if autoreset_mode not in ("same_step", "next_step"):
@@ -338,7 +341,7 @@ class VecACEnv:
                                          self.episode_len.data_ptr() if rec else None, err, ec, self.num_envs,
                                          self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
             _lib.check(st, "acx_step_next")
-        elif self._lengths_ok and not self.record_actions:
+        elif self._lengths_ok and self._live_tile and not self.record_actions:
             # the rows' lengths are current: only their letters are read and written
             st = self._lib.acx_step_lengths(s_in, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
                                             self.num_envs, self.max_relator_length, self.horizon_length,

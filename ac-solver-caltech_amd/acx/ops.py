@@ -51,6 +51,11 @@ def _L_of(states: torch.Tensor) -> int:
     return L
 
 
+# relator lengths for which acx_step_lengths reads and writes only the live chunks (the kernels'
+# compile-time tiles); at any other L it reads whole rows like acx_step
+LIVE_TILE_L = (36, 128)
+
+
 def step(
     state_in: torch.Tensor,
     action: torch.Tensor,

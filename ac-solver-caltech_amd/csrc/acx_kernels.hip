@@ -270,6 +270,13 @@ struct FastTile {
         const int4* src = reinterpret_cast<const int4*>(g) + ln;
         bool any_bad = false;
         if (R == WAVE) {  // full tile (wave-uniform): unguarded, LOAD_BATCH loads in flight
+            // LIVE: loads through a buffer descriptor over the tile's rows, a dead chunk at an
+            // out-of-range offset (zeros, nothing read): no load under a branch (see CodeTile::load)
+            const uint64_t gb = reinterpret_cast<uint64_t>(g);
+            const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
+            const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
+            const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
 #pragma unroll
             for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
                 int4 v[LOAD_BATCH];
@@ -278,8 +285,14 @@ struct FastTile {
                 for (int u = 0; u < LOAD_BATCH; ++u) {
                     if (u0 + u >= CPR) continue;
                     const int c = ln + (u0 + u) * WAVE;
-                    lv[u] = !LIVE || live(c / CPR, c % CPR);
-                    if (lv[u]) v[u] = src[(u0 + u) * WAVE];
+                    lv[u] = true;
+                    if constexpr (LIVE) {
+                        const uint32_t off = live(c / CPR, c % CPR) ? (uint32_t)c * 16u : 0x80000000u;
+                        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, 0, 0);
+                        v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
+                    } else {
+                        v[u] = src[(u0 + u) * WAVE];
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < LOAD_BATCH; ++u) {
@@ -317,6 +330,23 @@ struct FastTile {
         }
         tile_bad = __any(any_bad);
         wave_sync();
+#if ACX_FAST_CONVERT
+        if (tile_bad) {
+            // rare (wave-uniform): chunk_i8 left arbitrary bytes in the flagged rows; their image
+            // is rebuilt with to_i8 (an out-of-domain letter -> 0x7f), so the letter counts the
+            // contract reports for them (reward, lengths) are those of the input row
+            if (ln < R && flags[ln]) {
+                const int4* row = reinterpret_cast<const int4*>(g) + (int64_t)ln * CPR;
+                for (int k = 0; k < CPR; ++k) {
+                    if (LIVE && !live(ln, k)) continue;
+                    const int4 v = row[k];
+                    bool b = false;
+                    lds[ln * S + k] = to_i8(v.x, b) | (to_i8(v.y, b) << 8) | (to_i8(v.z, b) << 16) | (to_i8(v.w, b) << 24);
+                }
+            }
+            wave_sync();
+        }
+#endif
     }
 
     // all BLOCK threads load R rows into this tile (the block's one): consecutive threads on
@@ -857,28 +887,37 @@ struct CodeTile {
                 // the lane's fixed slot address (row u at a compile-time offset).  Rows with a
                 // letter outside {-2..2} (error inputs only) are found afterwards, when some
                 // chunk was bad: each lane rescans its own row's loaded chunks
+                // LIVE: every chunk is loaded through a buffer descriptor over the tile's rows, a
+                // dead chunk at an out-of-range offset -- the hardware returns zeros and reads
+                // nothing -- so no load sits under a branch (a conditional load made the
+                // compiler wait for all of them, vmcnt(0), before each conversion) and a dead
+                // chunk converts to an empty slot like any zero padding
                 int4 va[LOAD_BATCH], vb[LOAD_BATCH];
                 uint16_t* mine = reinterpret_cast<uint16_t*>(lds) + ln;
-                auto lv = [&](int u) {
-                    if constexpr (!LIVE) return true;
-                    else return live_lane(u, ln);
-                };
+                const uint64_t gb = reinterpret_cast<uint64_t>(g);
+                const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
+                const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
+                const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
                 auto issue = [&](int4* v, int u0) {
 #pragma unroll
-                    for (int u = 0; u < LOAD_BATCH; ++u)
-                        if (lv(u0 + u)) v[u] = src[(u0 + u) * WAVE];
+                    for (int u = 0; u < LOAD_BATCH; ++u) {
+                        if constexpr (LIVE) {
+                            const uint32_t off = live_lane(u0 + u, ln) ? (uint32_t)((u0 + u) * WAVE + ln) * 16u : 0x80000000u;
+                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, 0, 0);
+                            v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
+                        } else {
+                            v[u] = src[(u0 + u) * WAVE];
+                        }
+                    }
                 };
                 auto convert = [&](const int4* v, int u0) {
 #pragma unroll
                     for (int u = 0; u < LOAD_BATCH; ++u) {
                         bool bad = false;
-                        uint32_t slot = 0;
-                        if (lv(u0 + u)) {
-                            uint32_t c8, nz4;
-                            swar_pack4(chunk_i8(v[u], bad), c8, nz4);
-                            slot = c8 | (nz4 << 8);
-                        }
-                        mine[(u0 + u) * 2 * S] = (uint16_t)slot;
+                        uint32_t c8, nz4;
+                        swar_pack4(chunk_i8(v[u], bad), c8, nz4);
+                        mine[(u0 + u) * 2 * S] = (uint16_t)(c8 | (nz4 << 8));
                         any_bad |= bad;
                     }
                 };
@@ -905,6 +944,22 @@ struct CodeTile {
                         rb |= b;
                     }
                     flags[ln] = rb ? 1 : 0;
+                    // a flagged row's slots are rebuilt with to_i8 (an out-of-domain letter ->
+                    // 0x7f, non-zero), so the letter counts reported for it are the input row's
+                    if (rb) {
+                        for (int k = 0; k < CPR; ++k) {
+                            bool in = true;
+                            if constexpr (LIVE) in = live(ln, k);
+                            if (!in) continue;
+                            const int4 v = reinterpret_cast<const int4*>(row)[k];
+                            bool b = false;
+                            const uint32_t d = to_i8(v.x, b) | (to_i8(v.y, b) << 8) | (to_i8(v.z, b) << 16) |
+                                               (to_i8(v.w, b) << 24);
+                            uint32_t c8, nz4;
+                            swar_pack4(d, c8, nz4);
+                            slots(ln)[k] = (uint16_t)(c8 | (nz4 << 8) | ((uint32_t)b << 12));
+                        }
+                    }
                 }
                 wave_sync();
                 return;

@@ -10,9 +10,11 @@ default K = 200; a larger K reuses the same buffers, as a PPO loop does) that wr
 (K, B, 2L) int32 observation trajectory plus reward/done/truncated per step.  Inputs are
 resident in HBM before the timed region.
 
-`--workload step` makes the per-call acx_step API (one launch per env step, random actions,
-in-place state, autoreset) the headline instead: BASELINE configs[4] ("random-action stepping",
-L = 128, 2^20 envs per GPU over 8 GPUs) is
+`--workload step` makes the per-call step API (one launch per env step, random actions,
+in-place state, autoreset) the headline instead -- the call VecACEnv.step makes: at L = 36 and
+128 acx_step_lengths (the rows' relator lengths in and out, only the chunks inside the letters
+read and written), otherwise acx_step; the other call on the same walk is a variant.  BASELINE
+configs[4] ("random-action stepping", L = 128, 2^20 envs per GPU over 8 GPUs) is
 
     python bench.py --gpus 8 --workload step --L 128 --batch 1048576
 
@@ -664,7 +666,18 @@ def run_rank(args):
                                        "chunks inside old or new letters written, lengths 16 B + 27 B of scalars"},
             "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
         }
-        if not rollout_head:
+        if not rollout_head and L not in ops.LIVE_TILE_L:
+            # whole-row tiles: the env's step is acx_step (the step_api variant)
+            a_api = B * sb / (s_api / K) / 1e9
+            head = {
+                "elapsed": wall_api, "kernel_s": s_api, "wall_local": wall_api_local, "frac": a_api / HBM_PEAK_GBS,
+                "roofline": dict(variants["step_api"]["roofline"], kernel_ms=s_api * 1e3, launches=K,
+                                 launch_bytes=B * sb),
+                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step, {B} envs/GPU, L={L}, "
+                             f"horizon {H}, cyclical=True, in-place state, same-step autoreset; {K} launches"),
+                "env_errors": n_err_api,
+            }
+        elif not rollout_head:
             head = {
                 "elapsed": wall_len, "kernel_s": s_len, "wall_local": wall_len_local, "frac": a_len / HBM_PEAK_GBS,
                 "roofline": dict(variants["step_api_lengths"]["roofline"], kernel_ms=s_len * 1e3, launches=K,
