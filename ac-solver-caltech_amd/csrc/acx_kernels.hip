@@ -562,6 +562,7 @@ struct FastTile {
     // lane's row -> bit planes; returns true if the row is outside the domain.  Streams the row
     // 8 letters (two dwords) at a time through one gather per plane (pl::i8x8_to_bytes), so few
     // values are live at once: this pack sets the env-step kernels' register peak
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -604,6 +605,7 @@ struct FastTile {
 #pragma unroll
         for (int k = 0; k < CPR; k += 2) *reinterpret_cast<uint2*>(dst + k) = make_uint2(d[k], d[k + 1]);
     }
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -899,12 +901,22 @@ struct CodeTile {
                 const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
                 const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
                     reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
+                const uint32_t lane_off = (uint32_t)ln * 16u;
+                const uint32_t oob = 0x80000000u;
                 auto issue = [&](int4* v, int u0) {
 #pragma unroll
                     for (int u = 0; u < LOAD_BATCH; ++u) {
                         if constexpr (LIVE) {
-                            const uint32_t off = live_lane(u0 + u, ln) ? (uint32_t)((u0 + u) * WAVE + ln) * 16u : 0x80000000u;
-                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, 0, 0);
+                            // row u's live lanes as a 64-bit scalar mask (its counts read from lane
+                            // u: one readlane, the rest scalar), then one v_cndmask on it picks the
+                            // lane's offset or the out-of-range one; the row's base is the scalar
+                            // offset (in range on either reading of the bounds check)
+                            const uint32_t lu = (uint32_t)__builtin_amdgcn_readlane((int)limv, u0 + u);
+                            const uint32_t l0 = lu & 0xffu, l1 = (lu >> 8) & 0xffu;
+                            const uint64_t m = ((1ull << l0) - 1ull) | (((1ull << l1) - 1ull) << 32);
+                            uint32_t off;
+                            asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(off) : "v"(oob), "v"(lane_off), "s"(m));
+                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, (u0 + u) * WAVE * 16, 0);
                             v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
                         } else {
                             v[u] = src[(u0 + u) * WAVE];
@@ -1193,6 +1205,7 @@ struct CodeTile {
         x = (x | (x << 2)) & 0x33333333u;
         return (x | (x << 1)) & 0x55555555u;
     }
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
         static_assert(HALF % 4 == 0, "16-letter groups per relator");
         int ln = lane;
@@ -1205,8 +1218,12 @@ struct CodeTile {
             uint64_t nz[PW];
 #pragma unroll
             for (int j = 0; j < PW; ++j) w.s[j] = w.y[j] = nz[j] = 0ull;
+            const int lim_h = (int)((limv >> (8 * h)) & 0xffu);
 #pragma unroll
             for (int g = 0; g < HALF / 4; ++g) {  // 16 letters
+                // LIVE (the first pack after a live load): a group past every row's live chunks
+                // holds zero slots -- skipped when no lane of the wave has one (wave-uniform)
+                if (LIVE && !__any(lim_h > 4 * g)) continue;
                 const uint2 x = *reinterpret_cast<const uint2*>(src + (h * HALF + 4 * g) / 2);
                 const uint32_t codes = __builtin_amdgcn_perm(x.y, x.x, 0x06040200u);
                 uint32_t nzb = __builtin_amdgcn_perm(x.y, x.x, 0x07050301u) & 0x0F0F0F0Fu;
@@ -1229,11 +1246,16 @@ struct CodeTile {
         return bad;
     }
     // relator h of the lane's row from planes (canonical slots: codes and nz of absent letters 0)
-    __device__ __forceinline__ uint32_t put_relator(uint32_t* dst, const Planes<PW>& w, int n, bool cmp) const {
+    // glim >= 0: the slots past chunk glim are zero both in the tile and in the new image (a
+    // live-loaded relator: max of its old and new live chunks); groups past every lane's glim
+    // are neither compared nor written
+    __device__ __forceinline__ uint32_t put_relator(uint32_t* dst, const Planes<PW>& w, int n, bool cmp,
+                                                    int glim = -1) const {
         const pl::Bits<PW> m = pl::bmask<PW>(n);
         uint32_t x = 0;
 #pragma unroll
         for (int g = 0; g < HALF / 4; ++g) {
+            if (glim >= 0 && !__any(glim > 4 * g)) continue;
             const int sh = 16 * (g & 3);
             const uint32_t s16 = (uint32_t)(w.s[g >> 2] >> sh) & 0xffffu;
             const uint32_t y16 = (uint32_t)(w.y[g >> 2] >> sh) & 0xffffu;
@@ -1259,12 +1281,18 @@ struct CodeTile {
         put_relator(dst, p.w0, p.n0, false);
         put_relator(dst + HALF / 2, p.w1, p.n1, false);
     }
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         uint32_t* dst = lds + ln * S;
-        const uint32_t x0 = put_relator(dst, p.w0, p.n0, true);
-        const uint32_t x1 = put_relator(dst + HALF / 2, p.w1, p.n1, true);
+        int g0 = -1, g1 = -1;
+        if constexpr (LIVE) {
+            g0 = max((int)(limv & 0xffu), live_chunks(p.n0));
+            g1 = max((int)((limv >> 8) & 0xffu), live_chunks(p.n1));
+        }
+        const uint32_t x0 = put_relator(dst, p.w0, p.n0, true, g0);
+        const uint32_t x1 = put_relator(dst + HALF / 2, p.w1, p.n1, true, g1);
         return (x0 != 0u ? 1u : 0u) | (x1 != 0u ? 2u : 0u);
     }
     __device__ __forceinline__ void unpack_half(int lane, const PlaneRegs<PW>& p, bool h1) const {
@@ -1622,6 +1650,7 @@ struct GenericTile {
             zero_seen |= !nz;
         }
     }
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ bool pack(int lane, PlaneRegs<PW>& p) const {
         const int8_t* r = row(lane);
         bool bad = flags[lane] != 0;
@@ -1645,6 +1674,7 @@ struct GenericTile {
     __device__ __forceinline__ void unpack_half(int lane, const PlaneRegs<PW>& p, bool h1) const {
         unpack_relator(row(lane) + (h1 ? L : 0), pl::psel<PW>(h1, p.w1, p.w0), h1 ? p.n1 : p.n0);
     }
+    template <bool LIVE = false>  // LIVE: CodeTile only (see there)
     __device__ __forceinline__ uint32_t unpack_dirty(int lane, const PlaneRegs<PW>& p) const {
         unpack(lane, p);
         return 3u;
@@ -1878,7 +1908,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
         if (LEARN && a.action_hist && !pend && cnt - 1 < a.hist_cap)
             a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
-        const bool bad = tile.pack(w.lane, p);
+        const bool bad = tile.template pack<LIVE>(w.lane, p);
         const bool cyc = a.cyclical != 0;
         if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
         else if (bad) e = ACX_ERR_DOMAIN;
@@ -1890,7 +1920,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             }
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
-        if (!keep) dm = tile.unpack_dirty(w.lane, p);
+        if (!keep) dm = tile.template unpack_dirty<LIVE>(w.lane, p);
         const bool triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
         const bool trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
         // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does

@@ -100,8 +100,8 @@ int acx_step(const int32_t* state_in, int32_t* state_out, const int32_t* action,
              void* stream);
 
 /*
- * acx_step in place, carrying the rows' relator lengths (ACMove takes and returns them,
- * ac_moves.py:159,184,231): lengths (B,2) int32, in/out, holds each row's relator lengths on
+ * acx_step in place, carrying the rows' relator lengths as ACEnv does (self.lengths, set at reset
+ * and passed through ACMove every step, ac_env.py:81-95,119; ac_moves.py:159,184,231): lengths (B,2) int32, in/out, holds each row's relator lengths on
  * entry and its new lengths on exit, so the kernel reads only the 16-byte chunks inside each
  * relator's letters and writes only those inside its old or new letters (the padding past both
  * already holds zeros).  Rows must be canonical (letters, then zero padding) with exact lengths;

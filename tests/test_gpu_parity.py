@@ -465,7 +465,8 @@ def test_full_size_step_api_in_place(L, B):
     batch) and L = 128 (config 5's per-GPU shard), and config 2's exact batch (65,536 envs, L =
     36).  24 in-place acx_step calls with autoreset (horizon 10) -- the dirty-relator write-back
     (unchanged relators skipped, partial 64-B lines) -- against, on every env and every step:
-    the same steps out of place (every row written), the fused rollout's observations, rewards,
+    the same steps out of place (every row written), the lengths-carrying in-place steps
+    (acx_step_lengths: only live chunks read and written), the fused rollout's observations, rewards,
     done and truncated flags; size-independent invariants (valid, reduced, lengths = letter
     counts); and a 512-env sampled oracle replay of states, counts, rewards and lengths."""
     from acx import ops
@@ -485,11 +486,14 @@ def test_full_size_step_api_in_place(L, B):
                 trunc_traj=tr_r)
     st, cnt = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)  # in place
     st_o, cnt_o = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)  # out of place
+    st_l, cnt_l = starts.clone(), torch.zeros(B, dtype=torch.int32, device=DEV)  # lengths-carrying
     outs = [{k: torch.empty(B, dtype=dt, device=DEV) for k, dt in
-             (("rew", torch.int32), ("dn", torch.uint8), ("tr", torch.uint8), ("err", torch.uint8))} for _ in range(2)]
+             (("rew", torch.int32), ("dn", torch.uint8), ("tr", torch.uint8), ("err", torch.uint8))} for _ in range(3)]
     for o in outs:
         o["len"] = torch.empty((B, 2), dtype=torch.int32, device=DEV)
         o["ec"] = torch.zeros(1, dtype=torch.int32, device=DEV)
+    nz0 = starts.view(B, 2, L) != 0
+    outs[2]["len"].copy_(nz0.sum(2).to(torch.int32))  # acx_step_lengths: the rows' lengths carried
     rng = np.random.default_rng(L + B)
     sample = rng.choice(B, size=512, replace=False)
     si = torch.as_tensor(sample, device=DEV)
@@ -506,9 +510,15 @@ def test_full_size_step_api_in_place(L, B):
         ops.step(st_o, a, state_out=nxt, reset_state=starts, step_count=cnt_o, horizon=H, cyclical=True,
                  reward=p["rew"], done=p["dn"], truncated=p["tr"], lengths=p["len"], err=p["err"], err_count=p["ec"])
         st_o = nxt
+        q = outs[2]
+        ops.step(st_l, a, state_out=st_l, reset_state=starts, step_count=cnt_l, horizon=H, cyclical=True,
+                 reward=q["rew"], done=q["dn"], truncated=q["tr"], lengths=q["len"], err=q["err"], err_count=q["ec"],
+                 lengths_in=True)
         assert torch.equal(st, st_o) and torch.equal(cnt, cnt_o), t
+        assert torch.equal(st, st_l) and torch.equal(cnt, cnt_l), t
         for k in ("rew", "dn", "tr", "err", "len"):
             assert torch.equal(o[k], p[k]), (t, k)
+            assert torch.equal(o[k], q[k]), (t, k)
         assert torch.equal(st, obs[t]), t
         assert torch.equal(o["rew"], rew_r[t]) and torch.equal(o["dn"], dn_r[t]) and torch.equal(o["tr"], tr_r[t]), t
         # invariants on every env
