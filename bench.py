@@ -636,24 +636,34 @@ def run_rank(args):
             for t in range(K):
                 step2(actions[W + t])
 
-        wall_len, s_len, wall_len_local = timed(go_steps2)
-        n_err_len = int(err_count.item())
-        # algorithmic bytes of this path, measured off the clock over the next 8 steps of the
-        # walk: per relator, its live 16-byte chunks read (ceil(n/4)), and for a changed relator
-        # the chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars
+        # algorithmic bytes of exactly the timed steps: the same K steps are first run off the
+        # clock from a snapshot (the kernel is deterministic, so the timed pass replays this
+        # walk): per relator its live 16-byte chunks read (ceil(n/4)), for a changed relator the
+        # chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.
+        # The live bytes follow the walk's lengths, which grow through a horizon and drop at the
+        # synchronised resets, so a sample of other steps would not do.
+        snap = (st2.clone(), cnt2.clone(), lens2.clone(), err_count.clone())
         rd = wr = 0.0
-        for t in range(8):
+        for t in range(K):
             before, n_before = st2.clone(), lens2.clone()
-            step2(actions[(W + K + t) % actions.shape[0]])
+            step2(actions[W + t])
             ch = (before.view(B, 2, L) != st2.view(B, 2, L)).any(2)
             c_old = (n_before.clamp(0, L) + 3) // 4
             c_new = (lens2.clamp(0, L) + 3) // 4
             rd += float(c_old.sum().item()) * 16 / B
             wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16 / B
             del before, n_before
-        rd, wr = rd / 8, wr / 8
+        rd, wr = rd / K, wr / K
         sb_len = rd + wr + 16 + 27
-        same = bool(torch.equal(st1, st2))  # both walks took the same 8 + K + W steps
+        for x, y in zip((st2, cnt2, lens2, err_count), snap):
+            x.copy_(y)
+        del snap
+
+        wall_len, s_len, wall_len_local = timed(go_steps2)
+        n_err_len = int(err_count.item())
+        for t in range(8):  # the step_api walk took 8 more steps (its changed-relator sample)
+            step2(actions[(W + K + t) % actions.shape[0]])
+        same = bool(torch.equal(st1, st2))  # both walks took the same W + K + 8 steps
         len_kernel = f"acx::step_lengths_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>"
         a_len = B * sb_len / (s_len / K) / 1e9
         variants["step_api_lengths"] = {
@@ -756,7 +766,8 @@ def run_rank(args):
     if rollout_head:
         traffic, traffic_src = committed_traffic(B, L, K, head["roofline"]["launch_bytes"])
     else:
-        traffic, traffic_src = committed_step_traffic(B, L, head["roofline"]["launch_bytes"])
+        traffic, traffic_src = committed_step_traffic(B, L, head["roofline"]["launch_bytes"],
+                                                      head["roofline"].get("kernel", ""))
     head["roofline"].update(traffic=traffic, traffic_source=traffic_src)
 
     rows = gather_rows([B * K / head["wall_local"], head["kernel_s"] * 1e3, head["frac"], head["wall_local"] * 1e3],
@@ -828,12 +839,13 @@ def committed_traffic(B, L, K, launch_bytes):
             f"{where} at K={kp}: measured/algorithmic = {ratio:.4f}, applied to this launch's algorithmic bytes")
 
 
-def committed_step_traffic(B, L, launch_bytes):
+def committed_step_traffic(B, L, launch_bytes, kernel):
     """(HBM bytes per step launch, where from) for --workload step: the newest committed
-    rocprofv3 PMC profile of the step workload at this (B, L), as its measured/algorithmic ratio
-    applied to this launch's algorithmic bytes (the changed-relator rate, hence the bytes, vary
-    slightly with the walk); or (None, None)"""
-    for tag in ("r04_step128", "r04_step36"):
+    rocprofv3 PMC profile of the step workload at this (B, L) and of this kernel, as its
+    measured/algorithmic ratio applied to this launch's algorithmic bytes (the changed-relator
+    rate, hence the bytes, vary slightly with the walk); or (None, None)"""
+    want = kernel.replace(" ", "")
+    for tag in ("r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
         prof = os.path.join(REPO, "profiles", "r04", f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
@@ -841,7 +853,9 @@ def committed_step_traffic(B, L, launch_bytes):
             ps = json.load(f)
         pc = ps.get("bench_line", {}).get("config", {})
         rec = ps.get("step_timed_dispatches") or {}
-        if pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and rec.get("pmc_over_algorithmic"):
+        got = rec.get("kernel", "").split("(")[0].replace("void ", "", 1).replace(" ", "")
+        if (pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and rec.get("pmc_over_algorithmic")
+                and got == want):
             r = rec["pmc_over_algorithmic"]
             return (launch_bytes * r, f"profiles/r04/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc "
                                       f"WRITE_SIZE per step launch, measured/algorithmic = {r:.4f}")

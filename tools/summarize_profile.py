@@ -119,7 +119,7 @@ if bench:
         summary["rollout_timed_dispatch"] = rec
 if bench and "random-action stepping" in bench["config"]["workload"]:
     # bench.py --workload step: the headline is K per-call acx_step_lengths launches after W
-    # warmup calls (then 8 off-the-clock calls for the live-byte rate); before round 4's
+    # warmup calls and K off-the-clock ones (the live-byte accounting); before round 4's
     # lengths-carrying step it was acx_step's (step_kernel<.., false>)
     import re
     pat = (r"step_lengths_kernel<\d+, \d+, \d+>" if "step_lengths_kernel" in bench["roofline"].get("kernel", "")
@@ -128,7 +128,10 @@ if bench and "random-action stepping" in bench["config"]["workload"]:
     if steps:
         kname, k = max(steps, key=lambda nv: nv[1]["dispatches"])
         W, K = bench["warmup"], bench["steps"]
-        idx = list(range(W, W + K))
+        # the lengths-carrying headline runs its K steps once off the clock (byte accounting)
+        # before the timed K; a profile from before that change has W + K + 8 dispatches
+        acct = K if "step_lengths_kernel" in kname and k["dispatches"] >= W + 2 * K else 0
+        idx = list(range(W + acct, W + acct + K))
         ms = [k["durations_ms"][i] for i in idx]
         tb = [(k.get("fetch_bytes_corrected") or [None] * (W + K))[i] for i in idx]
         wb = [(k.get("write_bytes") or [None] * (W + K))[i] for i in idx]
