@@ -673,7 +673,14 @@ def run_rank(args):
                          "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
                          "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
                          "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
-                                       "chunks inside old or new letters written, lengths 16 B + 27 B of scalars"},
+                                       "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
+                                       "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
+                                       "relator's last live chunk brings its sector's dead ones (PMC 1.30x these "
+                                       "bytes, profiles/r04/r04n_step128_summary.json)",
+                         "compute_note": "the tile conversion spends VALU on every chunk slot of a row, live or "
+                                         "not: early in a horizon (short relators) the kernel is VALU-issue-bound "
+                                         "(SQ_INSTS_VALU / (256 CUs x 2.4 GHz) = 0.111 ms of a 0.134 ms launch, "
+                                         "profiles/r04/r04o_step_sq_counters.json), later HBM-bound"},
             "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
         }
         if not rollout_head and L not in ops.LIVE_TILE_L:
