@@ -565,6 +565,52 @@ def run_rank(args):
                              "and resets fire on a large share of env-steps")
         del tstarts, desync
 
+    if not rollout_head and not args.no_obs8:
+        # config 5's random-action stepping through the fused rollout instead of one call per
+        # step: every step's observation is still materialised, as the (K, B, 2L) int8
+        # trajectory of VecACEnv.rollout (the reference's observation dtype, ac_env.py:64-70,
+        # and what SyncVectorEnv returns), in launches of <= T8 steps reusing the buffers
+        T8 = max(1, min(K, 50, (64 << 30) // max(1, B * (2 * L + 6))))
+        obs8 = torch.zeros((T8, B, 2 * L), dtype=torch.int8, device=dev)
+        rew8 = torch.zeros((T8, B), dtype=torch.int32, device=dev)
+        dn8 = torch.zeros((T8, B), dtype=torch.uint8, device=dev)
+        tr8 = torch.zeros((T8, B), dtype=torch.uint8, device=dev)
+        st8, cnt8 = starts.clone(), torch.zeros(B, dtype=torch.int32, device=dev)
+        err_count.zero_()
+        n_res8 = [0]
+
+        def go8(a, T, count=False):
+            for t0 in range(0, T, T8):
+                t1 = min(T, t0 + T8)
+                ops.rollout(st8, a[t0:t1], starts, cnt8, horizon=H, cyclical=True, obs_traj=obs8[: t1 - t0],
+                            reward_traj=rew8[: t1 - t0], done_traj=dn8[: t1 - t0], trunc_traj=tr8[: t1 - t0],
+                            err=err, err_count=err_count)
+                if count:
+                    n_res8[0] += int((dn8[: t1 - t0] | tr8[: t1 - t0]).sum().item())
+
+        if W > 0:
+            go8(actions[:W], W)
+        snap8 = (st8.clone(), cnt8.clone())
+        go8(actions[W: W + K], K, count=True)  # off the clock: the resets of the timed steps (bytes)
+        st8.copy_(snap8[0]), cnt8.copy_(snap8[1])
+        del snap8
+        err_count.zero_()
+        wall8, s8, _ = timed(lambda: go8(actions[W: W + K], K))
+        n8 = -(-K // T8)
+        # per env-step: action 4 + obs 2L + reward 4 + done 1 + truncated 1; per env per launch
+        # state in/out 16L + count in/out 8 + err 1; the starting row (8L) of every reset
+        nb8 = K * B * (2 * L + 10) + n8 * B * (16 * L + 9) + n_res8[0] * 8 * L
+        variants["stepping_rollout_obs_int8"] = {
+            "value": seen * B * K / wall8, "unit": "env-steps/s", "kernel_ms": s8 * 1e3, "ms_per_step": wall8 / K * 1e3,
+            "env_errors": int(err_count.item()), "launches": n8,
+            "workload": (f"the same random-action walk ({B} envs/GPU, L={L}, horizon {H}, autoreset) through the "
+                         f"fused rollout (VecACEnv.rollout), every step's observation written to an int8 (K,B,2L) "
+                         f"trajectory, launches of <= {T8} steps"),
+            "roofline": {"bound": "hbm", "achieved": nb8 / s8 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": nb8 / s8 / 1e9 / HBM_PEAK_GBS, "launch_bytes": nb8,
+                         "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,2>"}}
+        del obs8, rew8, dn8, tr8, st8, cnt8
+
     chg_rate = None  # changed relators per env-step of the in-place step (step_api)
     if not args.no_step_api or not rollout_head:
         # per-call acx_step API: one launch per env step, state in place in HBM, autoreset

@@ -59,6 +59,8 @@ def test_bench_step_workload_headline():
     assert v["step_api_lengths"]["same_states_as_step_api"] and v["step_api_lengths"]["env_errors"] == 0
     assert "random-action stepping" in d["config"]["workload"]
     assert "rollout_obs_int8" not in d["variants"] and "step_api_hipgraph" in d["variants"]
+    r8 = d["variants"]["stepping_rollout_obs_int8"]
+    assert r8["env_errors"] == 0 and r8["value"] > 0 and r8["roofline"]["kernel"] == "acx::rollout_kernel<8,128,4,2>"
 
 
 def test_bench_launcher_two_ranks_gloo_one_gpu():
