@@ -258,9 +258,8 @@ class VecACEnv:
         # them (rollout, direct writes by a learner), and the next step uses acx_step, which rewrites them
         self.lengths = _row_extent(self.state, L).contiguous()
         self._lengths_ok = True
-        # the compile-time tiles (L = 36, 128) read only the live chunks; at any other L the
-        # kernel reads whole rows either way, so the plain step is taken
-        self._live_tile = L in ops.LIVE_TILE_L
+        # the lengths-carrying step where it measured faster (ops.LENGTHS_STEP_L, L = 128)
+        self._live_tile = L in ops.LENGTHS_STEP_L
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
         if autoreset_mode not in ("same_step", "next_step"):

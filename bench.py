@@ -11,9 +11,9 @@ default K = 200; a larger K reuses the same buffers, as a PPO loop does) that wr
 resident in HBM before the timed region.
 
 `--workload step` makes the per-call step API (one launch per env step, random actions,
-in-place state, autoreset) the headline instead -- the call VecACEnv.step makes: at L = 36 and
-128 acx_step_lengths (the rows' relator lengths in and out, only the chunks inside the letters
-read and written), otherwise acx_step; the other call on the same walk is a variant.  BASELINE
+in-place state, autoreset) the headline instead -- the call VecACEnv.step makes: at L = 128
+acx_step_lengths (the rows' relator lengths in and out, only the chunks inside the letters read
+and written), otherwise acx_step; the other call on the same walk is a variant.  BASELINE
 configs[4] ("random-action stepping", L = 128, 2^20 envs per GPU over 8 GPUs) is
 
     python bench.py --gpus 8 --workload step --L 128 --batch 1048576
@@ -729,7 +729,7 @@ def run_rank(args):
                                          "profiles/r04/r04o_step_sq_counters.json), later HBM-bound"},
             "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
         }
-        if not rollout_head and L not in ops.LIVE_TILE_L:
+        if not rollout_head and L not in ops.LENGTHS_STEP_L:
             # whole-row tiles: the env's step is acx_step (the step_api variant)
             a_api = B * sb / (s_api / K) / 1e9
             head = {

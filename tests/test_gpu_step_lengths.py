@@ -2,9 +2,9 @@
 out, only the chunks inside the letters read and written) against acx_step on the same rows,
 actions and starting states, many steps: states, rewards, flags, step counts, final
 observations, errors and lengths bit-exact.  acx_step is itself pinned to the reference's
-fixtures (test_gpu_parity.py); VecACEnv's plain step goes through acx_step_lengths, so the
-env-level golden replays (test_gpu_parity.py::test_vec_env_matches_golden_episodes and the
-oracle-model tests) cover it too."""
+fixtures (test_gpu_parity.py), and the full-size in-place test there runs the lengths-carrying
+stream beside it at 2^20 envs.  VecACEnv's plain step takes acx_step_lengths at L = 128
+(ops.LENGTHS_STEP_L)."""
 import numpy as np
 import pytest
 import torch
@@ -108,14 +108,17 @@ def test_step_lengths_rejects_missing_lengths():
     assert rc == _lib.E_ARG
 
 
-def test_vec_env_lengths_after_rollout_and_direct_writes():
+@pytest.mark.parametrize("L", [128, 36])
+def test_vec_env_lengths_after_rollout_and_direct_writes(L):
     """VecACEnv keeps lengths current across steps; a rollout (no lengths out) and reset_env
-    hand over correctly: the env matches a twin stepped one move at a time with acx_step."""
-    from acx import VecACEnv, _lib
-    L, B, H = 36, 64 * 5 + 3, 8
+    hand over correctly: the env matches a twin stepped one move at a time with acx_step.  At
+    L = 128 the env's steps go through acx_step_lengths (ops.LENGTHS_STEP_L)."""
+    from acx import VecACEnv, _lib, ops
+    B, H = 64 * 5 + 3, 8
     rng = np.random.default_rng(3)
     start = _rows(L, B, rng)
     env = VecACEnv(start, horizon_length=H, device=DEV)
+    assert env._live_tile == (L in ops.LENGTHS_STEP_L)
     twin = VecACEnv(start, horizon_length=H, device=DEV)
     twin._lengths_ok = False  # the twin always takes acx_step (it rewrites its lengths each call)
     T = 6
