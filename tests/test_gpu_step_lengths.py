@@ -96,6 +96,54 @@ def test_step_lengths_matches_acx_step(L, cyc):
     assert n_reset > B and n_err > n_ood  # resets, out-of-domain resets and failed moves exercised
 
 
+@pytest.mark.parametrize("L", [36, 128, 17])
+def test_step_lengths_error_stream_matches_acx_step(L):
+    """The error-contract stream of test_gpu_rollout_errors (moves that empty a relator from
+    r0 == r1 rows, an unreduced relator whose conjugation raises, out-of-domain INPUT rows -- a
+    letter 3, a zero inside r1, a letter 300 -- and out-of-domain starting rows, bad move ids,
+    desynchronised and whole-wave resets) through acx_step_lengths with the lengths VecACEnv
+    computes (_row_extent: far enough to see every bad entry), against acx_step."""
+    from test_gpu_rollout_errors import _error_stream
+    from acx import _lib
+    from acx.envs.ac_env import _row_extent
+    lib = _lib.load()
+    B, T, H = 64 * 11 + 21, 26, 6
+    st0, resets, count0, acts, eq, bad_in, bad_rs = _error_stream(L, B, T, H, seed=L + 7)
+    st = {k: _t(st0) for k in "ab"}
+    rs = _t(resets)
+    cnt = {k: _t(count0) for k in "ab"}
+    rew = {k: torch.zeros(B, dtype=torch.int32, device=DEV) for k in "ab"}
+    dn = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    tr = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    err = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    ec = {k: torch.zeros(1, dtype=torch.int32, device=DEV) for k in "ab"}
+    lens_a = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
+    lens_b = _row_extent(st["b"], L).contiguous()
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    seen = set()
+    for t in range(T):
+        at = _t(acts[t])
+        for k in "ab":
+            P = lambda x: x[k].data_ptr()  # noqa: E731
+            if k == "a":
+                rc = lib.acx_step(P(st), P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
+                                  lens_a.data_ptr(), None, P(err), P(ec), B, L, H, 1, stream)
+            else:
+                rc = lib.acx_step_lengths(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
+                                          lens_b.data_ptr(), None, P(err), P(ec), B, L, H, 1, stream)
+            assert rc == 0, (k, rc)
+        for name, d in (("state", st), ("reward", rew), ("done", dn), ("trunc", tr), ("count", cnt),
+                        ("err", err), ("err_count", ec)):
+            assert torch.equal(d["a"], d["b"]), (t, name)
+        e = err["a"].cpu().numpy()
+        dom = e == 3
+        la, lb = lens_a.cpu().numpy(), lens_b.cpu().numpy()
+        assert np.array_equal(la[~dom], lb[~dom]), t
+        assert (lb[dom] == L).all(), t
+        seen |= set(np.unique(e).tolist())
+    assert {1, 2, 3, 4} <= seen  # every error kind went through both calls
+
+
 def test_step_lengths_rejects_missing_lengths():
     from acx import _lib
     lib = _lib.load()
