@@ -662,73 +662,76 @@ def run_rank(args):
                                        "(in place: unchanged relators are not written)"},
             "env_errors": n_err_api,
         }
-        # the same walk through the lengths-carrying step (acx_step_lengths, VecACEnv.step's
-        # path): lengths in and out, so only the chunks inside each relator's letters are read
-        # and only those inside the old or new letters of a changed relator written
-        st2 = starts.clone()
-        cnt2 = torch.zeros(B, dtype=torch.int32, device=dev)
-        lens2 = torch.full((B, 2), L, dtype=torch.int32, device=dev)  # (L, L): read whole, once
+        # the same walk through the lengths-carrying step (acx_step_lengths), where VecACEnv.step
+        # takes it (ops.LENGTHS_STEP_L) or with --workload step; at L = 36 it ties with acx_step
+        # (DESIGN.md "The lengths-carrying step") and the default line leaves it out
+        run_len = not rollout_head or L in ops.LENGTHS_STEP_L
+        if run_len:
+            st2 = starts.clone()
+            cnt2 = torch.zeros(B, dtype=torch.int32, device=dev)
+            lens2 = torch.full((B, 2), L, dtype=torch.int32, device=dev)  # (L, L): read whole, once
 
-        def step2(a):
-            ops.step(st2, a, state_out=st2, reset_state=starts, step_count=cnt2, horizon=H, cyclical=True,
-                     reward=rew1, done=dn1, truncated=tr1, lengths=lens2, err=err, err_count=err_count,
-                     lengths_in=True)
+            def step2(a):
+                ops.step(st2, a, state_out=st2, reset_state=starts, step_count=cnt2, horizon=H, cyclical=True,
+                         reward=rew1, done=dn1, truncated=tr1, lengths=lens2, err=err, err_count=err_count,
+                         lengths_in=True)
 
-        err_count.zero_()
-        for t in range(W):
-            step2(actions[t])
+            err_count.zero_()
+            for t in range(W):
+                step2(actions[t])
 
-        def go_steps2():
+            def go_steps2():
+                for t in range(K):
+                    step2(actions[W + t])
+
+            # algorithmic bytes of exactly the timed steps: the same K steps are first run off the
+            # clock from a snapshot (the kernel is deterministic, so the timed pass replays this
+            # walk): per relator its live 16-byte chunks read (ceil(n/4)), for a changed relator the
+            # chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.
+            # The live bytes follow the walk's lengths, which grow through a horizon and drop at the
+            # synchronised resets, so a sample of other steps would not do.
+            snap = (st2.clone(), cnt2.clone(), lens2.clone(), err_count.clone())
+            rd = wr = 0.0
             for t in range(K):
+                before, n_before = st2.clone(), lens2.clone()
                 step2(actions[W + t])
+                ch = (before.view(B, 2, L) != st2.view(B, 2, L)).any(2)
+                c_old = (n_before.clamp(0, L) + 3) // 4
+                c_new = (lens2.clamp(0, L) + 3) // 4
+                rd += float(c_old.sum().item()) * 16 / B
+                wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16 / B
+                del before, n_before
+            rd, wr = rd / K, wr / K
+            sb_len = rd + wr + 16 + 27
+            for x, y in zip((st2, cnt2, lens2, err_count), snap):
+                x.copy_(y)
+            del snap
 
-        # algorithmic bytes of exactly the timed steps: the same K steps are first run off the
-        # clock from a snapshot (the kernel is deterministic, so the timed pass replays this
-        # walk): per relator its live 16-byte chunks read (ceil(n/4)), for a changed relator the
-        # chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.
-        # The live bytes follow the walk's lengths, which grow through a horizon and drop at the
-        # synchronised resets, so a sample of other steps would not do.
-        snap = (st2.clone(), cnt2.clone(), lens2.clone(), err_count.clone())
-        rd = wr = 0.0
-        for t in range(K):
-            before, n_before = st2.clone(), lens2.clone()
-            step2(actions[W + t])
-            ch = (before.view(B, 2, L) != st2.view(B, 2, L)).any(2)
-            c_old = (n_before.clamp(0, L) + 3) // 4
-            c_new = (lens2.clamp(0, L) + 3) // 4
-            rd += float(c_old.sum().item()) * 16 / B
-            wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16 / B
-            del before, n_before
-        rd, wr = rd / K, wr / K
-        sb_len = rd + wr + 16 + 27
-        for x, y in zip((st2, cnt2, lens2, err_count), snap):
-            x.copy_(y)
-        del snap
-
-        wall_len, s_len, wall_len_local = timed(go_steps2)
-        n_err_len = int(err_count.item())
-        for t in range(8):  # the step_api walk took 8 more steps (its changed-relator sample)
-            step2(actions[(W + K + t) % actions.shape[0]])
-        same = bool(torch.equal(st1, st2))  # both walks took the same W + K + 8 steps
-        len_kernel = f"acx::step_lengths_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>"
-        a_len = B * sb_len / (s_len / K) / 1e9
-        variants["step_api_lengths"] = {
-            "value": seen * B * K / wall_len, "unit": "env-steps/s", "ms_per_step": wall_len / K * 1e3,
-            "kernel_ms": s_len * 1e3, "env_errors": n_err_len, "same_states_as_step_api": same,
-            "roofline": {"bound": "hbm", "achieved": a_len, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
-                         "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
-                         "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
-                                       "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
-                                       "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
-                                       "relator's last live chunk brings its sector's dead ones (PMC 1.30x these "
-                                       "bytes, profiles/r04/r04n_step128_summary.json)",
-                         "compute_note": "the tile conversion spends VALU on every chunk slot of a row, live or "
-                                         "not: early in a horizon (short relators) the kernel is VALU-issue-bound "
-                                         "(SQ_INSTS_VALU / (256 CUs x 2.4 GHz) = 0.111 ms of a 0.134 ms launch, "
-                                         "profiles/r04/r04o_step_sq_counters.json), later HBM-bound"},
-            "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
-        }
+            wall_len, s_len, wall_len_local = timed(go_steps2)
+            n_err_len = int(err_count.item())
+            for t in range(8):  # the step_api walk took 8 more steps (its changed-relator sample)
+                step2(actions[(W + K + t) % actions.shape[0]])
+            same = bool(torch.equal(st1, st2))  # both walks took the same W + K + 8 steps
+            len_kernel = f"acx::step_lengths_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>"
+            a_len = B * sb_len / (s_len / K) / 1e9
+            variants["step_api_lengths"] = {
+                "value": seen * B * K / wall_len, "unit": "env-steps/s", "ms_per_step": wall_len / K * 1e3,
+                "kernel_ms": s_len * 1e3, "env_errors": n_err_len, "same_states_as_step_api": same,
+                "roofline": {"bound": "hbm", "achieved": a_len, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
+                             "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
+                             "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
+                                           "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
+                                           "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
+                                           "relator's last live chunk brings its sector's dead ones (PMC 1.30x these "
+                                           "bytes, profiles/r04/r04n_step128_summary.json)",
+                             "compute_note": "the tile conversion spends VALU on every chunk slot of a row, live or "
+                                             "not: early in a horizon (short relators) the kernel is VALU-issue-bound "
+                                             "(SQ_INSTS_VALU / (256 CUs x 2.4 GHz) = 0.111 ms of a 0.134 ms launch, "
+                                             "profiles/r04/r04o_step_sq_counters.json), later HBM-bound"},
+                "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
+            }
+            del st2, cnt2, lens2
         if not rollout_head and L not in ops.LENGTHS_STEP_L:
             # whole-row tiles: the env's step is acx_step (the step_api variant)
             a_api = B * sb / (s_api / K) / 1e9
@@ -750,7 +753,6 @@ def run_rank(args):
                              f"in-place state, same-step autoreset; {K} launches"),
                 "env_errors": n_err_len,
             }
-        del st2, cnt2, lens2
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
         # the ctypes launches on the capture stream) and replayed: no per-launch host cost
