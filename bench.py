@@ -1002,60 +1002,105 @@ def search_variants(dev) -> dict:
     return out
 
 
+class LineGuard:
+    """World > 1, around the sharded-BFS variant: the measured line reaches stdout even if that
+    variant never returns.  Two triggers make rank 0 print the line (the variant marked with what
+    happened) and end the process with EXIT_BFS_STALL:
+      * a deadline of `timeout_s` (a stalled exchange);
+      * a signal -- SIGTERM is what torchrun sends the surviving ranks when another rank dies (a
+        fault inside its collective, say).  It arrives through signal.set_wakeup_fd, so a helper
+        thread sees it while the main thread is blocked inside a C call (an RCCL wait, a ctypes
+        call), where a Python-level handler would not run until that call returned.
+    Leaving the block normally disarms both.  Main thread only (signal handlers)."""
+
+    def __init__(self, line: dict, variants: dict, key: str, rank: int, timeout_s: float):
+        self.line, self.variants, self.key, self.rank, self.timeout_s = line, variants, key, rank, timeout_s
+
+    def __enter__(self):
+        import signal
+        import threading
+
+        self._r, self._w = os.pipe()
+        self._cr, self._cw = os.pipe()  # disarm
+        os.set_blocking(self._w, False)
+        self._old_fd = signal.set_wakeup_fd(self._w)
+        self._old_h = signal.signal(signal.SIGTERM, lambda *_: None)  # no-op: the helper thread acts
+        self._t = threading.Thread(target=self._watch, daemon=True)
+        self._t.start()
+        return self
+
+    def _fire(self, why: str) -> None:
+        if self.rank == 0:  # the variant may be inside redirect_stdout: write to the real stdout
+            self.variants[self.key] = {"error": why}
+            sys.__stdout__.write(json.dumps(self.line) + "\n")
+            sys.__stdout__.flush()
+        os._exit(EXIT_BFS_STALL)
+
+    def _watch(self) -> None:
+        import select
+        import signal
+
+        ready, _, _ = select.select([self._r, self._cr], [], [], self.timeout_s)
+        if self._cr in ready:
+            return
+        if self._r in ready:
+            sig = os.read(self._r, 1)
+            name = signal.Signals(sig[0]).name if sig and sig[0] in signal.Signals._value2member_map_ else "a signal"
+            self._fire(f"aborted by {name} (torchrun stops the surviving ranks when one exits)")
+        self._fire(f"timeout after {self.timeout_s:.0f} s")
+
+    def __exit__(self, *exc):
+        import signal
+
+        os.write(self._cw, b"x")
+        self._t.join()
+        signal.signal(signal.SIGTERM, self._old_h)
+        signal.set_wakeup_fd(self._old_fd)
+        for fd in (self._r, self._w, self._cr, self._cw):
+            os.close(fd)
+        return False
+
+
 def run_sharded_bfs_variant(args, line, variants, dev, rank, world, backend) -> None:
     """BASELINE configs[3] on the owner-partitioned BFS (csrc/acx_sbfs.hip): AK(3), L = 36, to 10^7
     nodes; node store + visited set sharded over the ranks by key owner, per-chunk RCCL
     all_gather / all_to_all / all_reduce (world 1: the exchanges are local copies).  Last, behind
-    a watchdog: the one variant with collectives on its data path.  If its exchanges at world > 1
-    stall, every rank's watchdog prints the line (rank 0) with the variant marked and exits with
-    EXIT_BFS_STALL: a hang costs neither the headline line nor a visible failure status."""
-    import threading
-
+    a guard: the one variant with collectives on its data path.  At world > 1 (LineGuard) a stalled
+    exchange, or the SIGTERM torchrun sends when another rank dies, makes rank 0 print the line with
+    the variant marked and every rank exit with EXIT_BFS_STALL: a failure there costs neither the
+    headline line nor a visible failure status."""
     import torch
 
     from acx.envs.utils import convert_relators_to_presentation
     from acx.search import _sharded_bfs as SB
 
-    variants["sharded_bfs"] = {"error": f"timeout after {args.bfs_timeout:.0f} s"}
-    timed_out_line = json.dumps(line)
-
-    def on_timeout():
-        if rank == 0:  # the variant may be inside redirect_stdout: write to the real stdout
-            sys.__stdout__.write(timed_out_line + "\n")
-            sys.__stdout__.flush()
-        os._exit(EXIT_BFS_STALL)
-
-    dog = threading.Timer(args.bfs_timeout, on_timeout) if world > 1 else None
-    if dog is not None:
-        dog.daemon = True
-        dog.start()
-    try:
-        ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
-        nb = 10 ** 7
-        with contextlib.redirect_stdout(io.StringIO()):
-            SB.sharded_bfs(ak3, nb, device=dev)  # warmup: workspace allocation
-        best = None
-        for _ in range(3):
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
+    guard = LineGuard(line, variants, "sharded_bfs", rank, args.bfs_timeout) if world > 1 else contextlib.nullcontext()
+    with guard:
+        try:
+            ak3 = convert_relators_to_presentation([1, 1, 1, -2, -2, -2, -2], [1, 2, 1, -2, -1, -2], 36)
+            nb = 10 ** 7
             with contextlib.redirect_stdout(io.StringIO()):
-                res = SB.sharded_bfs(ak3, nb, device=dev)
-            torch.cuda.synchronize()
-            el = synced_max(time.perf_counter() - t0, dev)
-            best = el if best is None else min(best, el)
-        st = SB.LAST_STATS
-        variants["sharded_bfs"] = {
-            "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],
-            "parents_expanded": st["parents"], "chunks": st["chunks"], "result": list(res) if res[0] else [False, None],
-            "workload": "BASELINE configs[3]: bfs from AK(3), L=36, cyclical=False, to 10^7 nodes; node store and "
-                        f"visited set partitioned by key owner over {world} rank(s), "
-                        f"{'RCCL' if backend == 'nccl' else backend} exchanges per chunk",
-        }
-    except Exception as e:  # noqa: BLE001 -- a variant (failing the same on every rank)
-        variants["sharded_bfs"] = {"error": repr(e)[:300]}
-    if dog is not None:
-        dog.cancel()
+                SB.sharded_bfs(ak3, nb, device=dev)  # warmup: workspace allocation
+            best = None
+            for _ in range(3):
+                barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    res = SB.sharded_bfs(ak3, nb, device=dev)
+                torch.cuda.synchronize()
+                el = synced_max(time.perf_counter() - t0, dev)
+                best = el if best is None else min(best, el)
+            st = SB.LAST_STATS
+            variants["sharded_bfs"] = {
+                "value": st["nodes"] / best, "unit": "BFS nodes/s", "wall_ms": best * 1e3, "nodes": st["nodes"],
+                "parents_expanded": st["parents"], "chunks": st["chunks"], "result": list(res) if res[0] else [False, None],
+                "workload": "BASELINE configs[3]: bfs from AK(3), L=36, cyclical=False, to 10^7 nodes; node store and "
+                            f"visited set partitioned by key owner over {world} rank(s), "
+                            f"{'RCCL' if backend == 'nccl' else backend} exchanges per chunk",
+            }
+        except Exception as e:  # noqa: BLE001 -- a variant (failing the same on every rank)
+            variants["sharded_bfs"] = {"error": repr(e)[:300]}
     SB.release_workspaces()
 
 

@@ -75,3 +75,45 @@ def test_failing_rank_fails_the_launcher():
     # every rank rejects the argument list (argparse exits 2); the launcher returns that status
     rc = bench.spawn_ranks(2, ["--dry-run", "--workload", "no-such-workload"])
     assert rc == 2
+
+
+_GUARD = """
+import os, signal, sys, time
+sys.path.insert(0, {repo!r})
+import bench
+line = {{"metric": "m", "value": 1.0, "variants": {{}}}}
+with bench.LineGuard(line, line["variants"], "sharded_bfs", 0, {timeout}):
+    if {kill}:
+        os.kill(os.getpid(), signal.SIGTERM)
+    time.sleep({sleep})  # the main thread inside a C call, as in an RCCL wait
+print("left the guard")
+"""
+
+
+def _guard(timeout, kill, sleep):
+    code = _GUARD.format(repo=REPO, timeout=timeout, kill=kill, sleep=sleep)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+
+
+def test_line_guard_prints_the_line_when_torchrun_stops_the_rank():
+    """SIGTERM (torchrun's stop of the surviving ranks) while the main thread is blocked: the line
+    is printed with the variant marked and the process exits EXIT_BFS_STALL, long before the sleep
+    or the deadline would end."""
+    p = _guard(30.0, True, 20)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    lines = _lines(p.stdout)
+    assert len(lines) == 1 and "left the guard" not in p.stdout
+    assert lines[0]["value"] == 1.0 and "SIGTERM" in lines[0]["variants"]["sharded_bfs"]["error"]
+
+
+def test_line_guard_deadline():
+    p = _guard(0.5, False, 20)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    lines = _lines(p.stdout)
+    assert len(lines) == 1 and "timeout" in lines[0]["variants"]["sharded_bfs"]["error"]
+
+
+def test_line_guard_disarms_on_exit():
+    p = _guard(30.0, False, 0.2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert _lines(p.stdout) == [] and "left the guard" in p.stdout

@@ -1,0 +1,96 @@
+// Store-stream probe for the headline rollout's observation trajectory (K, B, 2L) int32 at
+// L = 36, B = 2^20 (302 MB per step, 6 GB at K = 20), no compute.  Question: does the number of
+// stores a wave keeps in flight set the write rate of the rollout's store pattern (a wave per 64
+// envs writing its 18 KB slice of every step row), as against a one-shot linear fill?
+//   fill_oneshot     each thread one 16-B store, blocks in address order (torch fill_'s shape)
+//   fill_stride<N>   grid sized to resident capacity, grid-stride 16-B stores; N > 0: at most N
+//                    stores in flight per wave (s_waitcnt vmcnt(N) after each)
+//   tile<N>          the rollout's shape: wave w owns rows [64w, 64w + 64) of every step row and
+//                    writes its 18 x 1 KB slice per step, K steps, spin VALU cycles between steps;
+//                    N > 0 as above
+//   tile_oneshot     the same slices, one wave per (step, tile), step-major (each wave one slice)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+constexpr int WAVE = 64, BLOCK = 256;
+
+template <int N>
+__device__ __forceinline__ void throttle() {
+    // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt_hi[15:14]
+    if constexpr (N > 0) __builtin_amdgcn_s_waitcnt((N & 0xf) | (0x7 << 4) | (0xf << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void st_nt(int4* p, int4 v) {
+    typedef int v4i_t __attribute__((ext_vector_type(4)));
+    const v4i_t x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(p));
+}
+
+__global__ __launch_bounds__(256) void fill_oneshot(int4* __restrict__ dst, int64_t n16, int v) {
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n16) st_nt(dst + i, make_int4(v, v, v, (int)i));
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void fill_stride(int4* __restrict__ dst, int64_t n16, int v) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n16; i += (int64_t)gridDim.x * BLOCK) {
+        st_nt(dst + i, make_int4(v, v, v, (int)i));
+        throttle<N>();
+    }
+}
+
+// cpr 16-B chunks per row; a wave's slice of one step row = 64 * cpr chunks, contiguous
+template <int N>
+__global__ __launch_bounds__(256) void tile(int4* __restrict__ dst, int64_t rows, int cpr, int K, int spin, int v) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WAVE;
+    if (r0 >= rows) return;
+    const int nch = WAVE * cpr;
+    int acc = v + lane;
+    for (int t = 0; t < K; ++t) {
+        int4* row = dst + ((int64_t)t * rows + r0) * cpr;
+        for (int c = lane; c < nch; c += WAVE) {
+            st_nt(row + c, make_int4(acc, t, c, lane));
+            throttle<N>();
+        }
+        for (int i = 0; i < spin; ++i) acc = acc * 1664525 + 1013904223;  // the step's compute
+    }
+    if (acc == 0x7fffffff && lane == 64) dst[0].x = acc;  // keeps the spin
+}
+
+__global__ __launch_bounds__(256) void tile_oneshot(int4* __restrict__ dst, int64_t rows, int cpr, int v) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tiles = rows / WAVE;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // step-major (t, tile)
+    const int64_t t = g / tiles, r0 = (g - t * tiles) * WAVE;
+    int4* row = dst + (t * rows + r0) * cpr;
+    for (int c = lane; c < WAVE * cpr; c += WAVE) st_nt(row + c, make_int4(v, (int)t, c, lane));
+}
+
+extern "C" {
+// kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot; n: stores in flight per wave
+// (0 = unthrottled; 1, 2, 4, 8, 16); returns a hip error code
+int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin, int resident_blocks, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int cpr = 2 * L / 4;
+    int4* d = (int4*)buf;
+    const int64_t n16 = (int64_t)K * rows * cpr;
+    const unsigned tiles = (unsigned)((rows + 255) / 256);
+    if (kind == 0) {
+        fill_oneshot<<<dim3((unsigned)((n16 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s>>>(d, n16, 7);
+    } else if (kind == 1) {
+#define F(NN) fill_stride<NN><<<dim3(resident_blocks), dim3(BLOCK), 0, s>>>(d, n16, 7)
+        switch (n) { case 0: F(0); break; case 1: F(1); break; case 2: F(2); break; case 4: F(4); break;
+                     case 8: F(8); break; default: F(16); }
+#undef F
+    } else if (kind == 2) {
+#define T(NN) tile<NN><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, spin, 7)
+        switch (n) { case 0: T(0); break; case 1: T(1); break; case 2: T(2); break; case 4: T(4); break;
+                     case 8: T(8); break; default: T(16); }
+#undef T
+    } else {
+        tile_oneshot<<<dim3((unsigned)((int64_t)K * rows / 256)), dim3(BLOCK), 0, s>>>(d, rows, cpr, 7);
+    }
+    return (int)hipGetLastError();
+}
+}
