@@ -23,6 +23,7 @@ from acx import _lib, ops  # noqa: E402
 from acx.envs.utils import convert_relators_to_presentation  # noqa: E402
 from acx.search import _device_bfs as D  # noqa: E402
 
+JSON_OUT, sys.stdout = sys.stdout, sys.stderr  # stdout: the JSON line only
 budgets = [int(float(x)) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [10 ** 7]
 L = 36
 dev = torch.device("cuda:0")
@@ -105,4 +106,4 @@ best = min(times)
 bpp = 8 * L + 12 * (8 * L + 9)
 res["expand12_children"] = {"parents": M, "kernel_ms": best * 1e3, "children_per_s": 12 * M / best,
                             "bytes_per_parent": bpp, "GBps": M * bpp / best / 1e9, "frac": M * bpp / best / 8e12}
-print(json.dumps(res))
+print(json.dumps(res), file=JSON_OUT)

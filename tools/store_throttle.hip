@@ -58,6 +58,25 @@ __global__ __launch_bounds__(256) void tile(int4* __restrict__ dst, int64_t rows
     if (acc == 0x7fffffff && lane == 64) dst[0].x = acc;  // keeps the spin
 }
 
+// the same, but wave w owns its 64 envs in groups of GE consecutive envs, group g at envs
+// (g * waves + w) * GE: the resident waves writing their g-th group cover one contiguous
+// (resident waves x GE x 2L x 4 B) window instead of the whole step row
+template <int GE>
+__global__ __launch_bounds__(256) void tile_grouped(int4* __restrict__ dst, int64_t rows, int cpr, int K, int v) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t waves = rows / WAVE;
+    if (w >= waves) return;
+    const int gch = GE * cpr;  // chunks per group
+    for (int t = 0; t < K; ++t) {
+        int4* row = dst + (int64_t)t * rows * cpr;
+        for (int c = lane; c < WAVE * cpr; c += WAVE) {
+            const int g = c / gch, o = c - g * gch;
+            st_nt(row + ((int64_t)g * waves + w) * gch + o, make_int4(v, t, c, lane));
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void tile_oneshot(int4* __restrict__ dst, int64_t rows, int cpr, int v) {
     const int lane = threadIdx.x & 63;
     const int64_t tiles = rows / WAVE;
@@ -68,7 +87,7 @@ __global__ __launch_bounds__(256) void tile_oneshot(int4* __restrict__ dst, int6
 }
 
 extern "C" {
-// kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot; n: stores in flight per wave
+// kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot, 4 tile_grouped (n = GE: 8, 16, 32); n: stores in flight per wave
 // (0 = unthrottled; 1, 2, 4, 8, 16); returns a hip error code
 int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin, int resident_blocks, void* stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -88,6 +107,10 @@ int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin
         switch (n) { case 0: T(0); break; case 1: T(1); break; case 2: T(2); break; case 4: T(4); break;
                      case 8: T(8); break; default: T(16); }
 #undef T
+    } else if (kind == 4) {
+#define G(NN) tile_grouped<NN><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7)
+        switch (n) { case 8: G(8); break; case 16: G(16); break; default: G(32); }
+#undef G
     } else {
         tile_oneshot<<<dim3((unsigned)((int64_t)K * rows / 256)), dim3(BLOCK), 0, s>>>(d, rows, cpr, 7);
     }

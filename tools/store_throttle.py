@@ -39,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--spin", default="0,200")
+    ap.add_argument("--throttle", default="0,1,2,4,8,16", type=lambda x: [int(v) for v in x.split(",")])
     a = ap.parse_args()
     K, B, L, H = 20, 1 << 20, 36, 200
     dev = torch.device("cuda:0")
@@ -64,8 +65,9 @@ def main():
     spins = [int(x) for x in a.spin.split(",")]
     cases = [("rollout_k20", None)]
     cases += [("fill_oneshot", (0, 0, 0)), ("tile_oneshot", (3, 0, 0))]
-    cases += [(f"fill_stride_n{n}", (1, n, 0)) for n in (0, 1, 2, 4, 8, 16)]
-    cases += [(f"tile_n{n}_spin{s}", (2, n, s)) for s in spins for n in (0, 1, 2, 4, 8, 16)]
+    cases += [(f"fill_stride_n{n}", (1, n, 0)) for n in a.throttle]
+    cases += [(f"tile_n{n}_spin{s}", (2, n, s)) for s in spins for n in a.throttle]
+    cases += [(f"tile_grouped{ge}", (4, ge, 0)) for ge in (8, 16, 32)]
     ms = {c: [] for c, _ in cases}
     for rep in range(a.reps + 1):
         for name, c in cases:
