@@ -288,7 +288,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-search", action="store_true", help="skip config 4's single-GPU search variants")
     ap.add_argument("--no-desync", action="store_true")
     ap.add_argument("--no-obs8", action="store_true")
-    ap.add_argument("--bfs-timeout", type=float, default=180.0,
+    ap.add_argument("--bfs-timeout", type=float, default=60.0,
                     help="world > 1: seconds the sharded-BFS variant may take before the line is printed "
                          "without it (exit status 3)")
     ap.add_argument("--dry-run", action="store_true",
@@ -1081,6 +1081,8 @@ def run_sharded_bfs_variant(args, line, variants, dev, rank, world, backend) -> 
             nb = 10 ** 7
             with contextlib.redirect_stdout(io.StringIO()):
                 SB.sharded_bfs(ak3, nb, device=dev)  # warmup: workspace allocation
+            if os.environ.get("ACX_BENCH_KILL_RANK") == str(rank):  # rehearsal hook (tools/gpu_n2_rehearsal.sh)
+                os._exit(7)  # a rank dying mid-variant: the others must still produce the line
             best = None
             for _ in range(3):
                 barrier()

@@ -128,7 +128,7 @@ def _worker(rank, world, port, jobs, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_bfs_multi_rank(world):
     import torch.multiprocessing as mp
 
