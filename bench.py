@@ -22,7 +22,8 @@ Also measured (reported under "variants"): the rollout with an int8 trajectory a
 resets, the per-call step API (+ hipGraph), the PPO learner step, config 4's searches (device BFS,
 expansion kernel, host-dedup BFS, owner-partitioned BFS).
 
-Multi-GPU: one process per GPU, envs sharded by index (weak scaling: B envs per rank); no
+Multi-GPU: one process per GPU, envs sharded by index (weak scaling: B envs per rank, or with
+`--global-batch G` strong scaling: G / N envs per rank, "scaling": "strong"); no
 collective on the data path, a barrier + max-over-ranks of every timed region only.  Either
 torchrun starts the ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the environment), or
 `--gpus N > 1` without them makes this process a launcher that starts N rank processes of this
@@ -273,7 +274,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many envs in total, split evenly over the ranks (overrides --batch)")
     ap.add_argument("--L", type=int, default=36)
     ap.add_argument("--horizon", type=int, default=200)
     ap.add_argument("--workload", choices=("rollout", "step"), default="rollout",
@@ -314,6 +317,16 @@ def _check_world(args, rank: int) -> int:
     return seen
 
 
+def per_rank_batch(args, world: int) -> tuple:
+    """(envs per rank, "weak" | "strong"): --batch per rank, or --global-batch split over the ranks
+    (weak scaling at 2^20 envs per GPU, strong scaling at a fixed total of 2^20)"""
+    if not args.global_batch:
+        return args.batch, "weak"
+    if args.global_batch % (64 * world):
+        sys.exit(f"--global-batch {args.global_batch} must be a multiple of 64 x {world} ranks")
+    return args.global_batch // world, "strong"
+
+
 def _per_rank_rows(rows):
     return [{"rank": i, "value": r[0], "kernel_ms": r[1], "frac": r[2], "wall_ms": r[3]} for i, r in enumerate(rows)]
 
@@ -325,7 +338,7 @@ def dry_run(args, rank: int, local_rank: int, world: int) -> None:
 
     dev = dist_setup(local_rank, world, "gloo", cpu=True)
     seen = _check_world(args, rank)
-    L, B, K, W = args.L, args.batch, args.steps, args.warmup
+    (B, scaling), L, K, W = per_rank_batch(args, seen), args.L, args.steps, args.warmup
     shard = ms_starts(L, B, offset=rank * B)
     acc = np.zeros(B, np.int64)
 
@@ -344,7 +357,7 @@ def dry_run(args, rank: int, local_rank: int, world: int) -> None:
     rows = gather_rows([B * K / el, el * 1e3, 0.0, el * 1e3], dev)
     line = {
         "metric": METRIC, "value": seen * B * K / elapsed, "unit": "env-steps/s", "n_gpus": seen, "steps": K,
-        "warmup": W, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
+        "warmup": W, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "dtype": "int32", "data": "dry run: no GPU work (launcher / process-group check)",
         "dry_run": True, "world_size_seen": seen, "per_rank": _per_rank_rows(rows),
         "config": {"workload": f"dry run ({args.workload})", "global_batch": seen * B, "envs_per_gpu": B,
@@ -362,7 +375,7 @@ def run_rank(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.dry_run:
         return dry_run(args, rank, local_rank, world)
-    L, B, K, W, H = args.L, args.batch, args.steps, args.warmup, args.horizon
+    (B, scaling), L, K, W, H = per_rank_batch(args, world), args.L, args.steps, args.warmup, args.horizon
 
     cpu = None
     cpu_c = None
@@ -837,7 +850,7 @@ def run_rank(args):
         "warmup": W,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic: Miller-Schupp starting states (all_presentations.txt, env i -> i mod 1190), "

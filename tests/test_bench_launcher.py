@@ -117,3 +117,16 @@ def test_line_guard_disarms_on_exit():
     p = _guard(30.0, False, 0.2)
     assert p.returncode == 0, p.stderr[-2000:]
     assert _lines(p.stdout) == [] and "left the guard" in p.stdout
+
+
+def test_strong_scaling_splits_the_global_batch():
+    """--global-batch: the total is fixed and split over the ranks (SURVEY 8(d) strong scaling)."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1",
+                        "--global-batch", "1024"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    (d,) = _lines(p.stdout)
+    assert d["scaling"] == "strong" and d["n_gpus"] == 2
+    assert d["config"]["global_batch"] == 1024 and d["config"]["envs_per_gpu"] == 512
+    bad = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--global-batch", "1000"], cwd=REPO,
+                         capture_output=True, text=True, timeout=180, env=_env())
+    assert bad.returncode != 0 and "multiple of 64" in bad.stderr
