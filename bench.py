@@ -937,7 +937,8 @@ def search_variants(dev) -> dict:
                          (576 B per parent: row in 8L + 12 packed child keys);
       host_dedup_bfs  -- BASELINE's wording, "dedup on host": GPU expansion + the host engine
                          (csrc/acx_search.cpp) replaying the reference's FIFO / dedup / budget;
-                         kernel time, kernel + copies, and the host's share reported apart."""
+                         kernel time, kernel + copies, and the host's share reported apart;
+      device_greedy   -- greedy_search from AK(3) to 10^6 nodes, visited set in HBM."""
     import torch
 
     from acx import _lib, ops
@@ -1010,6 +1011,29 @@ def search_variants(dev) -> dict:
             "workload": work + "; dedup on host (engine='host'): kernel_ms = unpack + expand12 on the GPU, "
                                "kernel_d2h_ms = + H2D parents / D2H child keys per batch, host_dedup_ms = the host "
                                "engine's pop / store / replay"}
+        # the other half of configs[3]: greedy_search from AK(3) (greedy.py:15-121) to 10^6 nodes,
+        # the visited set in HBM (csrc/acx_greedy.hip), pops replayed on the host in the reference's
+        # order; best of 2 wall times after a warm-up
+        from acx.search import greedy_search
+
+        ng = 10 ** 6
+        with contextlib.redirect_stdout(io.StringIO()):
+            greedy_search(ak3, ng, device=dev)
+        gw = []
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(io.StringIO()):
+                gres = greedy_search(ak3, ng, device=dev)
+            gw.append(time.perf_counter() - t0)
+        gs = dict(E.LAST_STATS)
+        out["device_greedy"] = {
+            "value": gs["nodes"] / min(gw), "unit": "search nodes/s", "wall_ms": min(gw) * 1e3,
+            "walls_ms": [w * 1e3 for w in gw], "nodes": gs["nodes"], "pops": gs["pops"], "rounds": gs["rounds"],
+            "expanded": gs["expanded"], "gpu_roundtrip_ms": gs["gpu_roundtrip_s"] * 1e3,
+            "host_replay_ms": gs["host_replay_s"] * 1e3, "result": [bool(gres[0]), len(gres[1]) if gres[1] else None],
+            "workload": "greedy_search from AK(3), L=36, cyclical=False, to 10^6 nodes (BASELINE configs[3], "
+                        "greedy half); visited set in HBM (csrc/acx_greedy.hip), host replays the pop order"}
     except Exception as e:  # noqa: BLE001 -- a variant: its failure must not cost the headline line
         out["search_error"] = repr(e)[:300]
     return out
