@@ -291,6 +291,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-search", action="store_true", help="skip config 4's single-GPU search variants")
     ap.add_argument("--no-desync", action="store_true")
     ap.add_argument("--no-obs8", action="store_true")
+    ap.add_argument("--no-config2", action="store_true", help="skip the configs[1] (65,536 envs) step variant")
     ap.add_argument("--bfs-timeout", type=float, default=60.0,
                     help="world > 1: seconds the sharded-BFS variant may take before the line is printed "
                          "without it (exit status 3)")
@@ -822,6 +823,9 @@ def run_rank(args):
         }
         del lobs, lrew, ldone, lenv
 
+    if not args.no_config2 and world == 1 and rollout_head:
+        variants["config2_step"] = config2_variant(dev, H, timed)
+
     if not args.no_search and world == 1:
         variants.update(search_variants(dev))
 
@@ -928,6 +932,73 @@ def committed_step_traffic(B, L, launch_bytes, kernel):
             return (launch_bytes * r, f"profiles/r04/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc "
                                       f"WRITE_SIZE per step launch, measured/algorithmic = {r:.4f}")
     return None, None
+
+
+def config2_variant(dev, H: int, timed) -> dict:
+    """BASELINE configs[1]: 65,536 envs, L = 36, Miller-Schupp starts, uniform random move ids
+    (device generator, seed 0), per-call step API in place with same-step autoreset (SURVEY 8(d)
+    config 2), 200 timed steps after 10 warm-up steps; eager launches and the same 200 launches
+    replayed from one hipGraph.  At this batch a launch moves ~24 MB, so launch latency, not HBM,
+    bounds it ("bound": "launch"; frac is against HBM anyway)."""
+    import torch
+
+    from acx import ops
+
+    B2, L2, K2, W2 = 65536, 36, 200, 10
+    starts = torch.as_tensor(ms_starts(L2, B2)).to(dev)
+    st = starts.clone()
+    cnt = torch.zeros(B2, dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    acts = torch.randint(0, 12, (W2 + K2 + 8, B2), dtype=torch.int32, device=dev, generator=g)
+    rew = torch.empty(B2, dtype=torch.int32, device=dev)
+    dn = torch.empty(B2, dtype=torch.uint8, device=dev)
+    tr = torch.empty(B2, dtype=torch.uint8, device=dev)
+    lens = torch.empty((B2, 2), dtype=torch.int32, device=dev)
+    err = torch.zeros(B2, dtype=torch.uint8, device=dev)
+    ec = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step(a):
+        ops.step(st, a, state_out=st, reset_state=starts, step_count=cnt, horizon=H, cyclical=True, reward=rew,
+                 done=dn, truncated=tr, lengths=lens, err=err, err_count=ec)
+
+    for t in range(W2):
+        step(acts[t])
+    snap = (st.clone(), cnt.clone())
+
+    def go():
+        for t in range(K2):
+            step(acts[W2 + t])
+
+    wall, s_k, _ = timed(go)
+    n_err = int(ec.item())
+    chg = 0.0  # changed relators per env-step (the in-place write-back), off the clock
+    for t in range(8):
+        before = st.clone()
+        step(acts[W2 + K2 + t])
+        chg += float(((before.view(B2, 2, L2) != st.view(B2, 2, L2)).any(2)).sum().item()) / B2 / 8
+    sb = 8 * L2 + 27 + 4 * L2 * chg
+    out = {"value": B2 * K2 / wall, "unit": "env-steps/s", "ms_per_step": wall / K2 * 1e3, "kernel_ms": s_k * 1e3,
+           "env_errors": n_err, "envs": B2, "steps": K2,
+           "roofline": {"bound": "launch", "achieved": B2 * sb / (s_k / K2) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": B2 * sb / (s_k / K2) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": sb},
+           "workload": "BASELINE configs[1]: 65536 envs, L=36, Miller-Schupp starts, uniform random actions, per-call "
+                       "acx_step in place, horizon 200, same-step autoreset; 200 launches"}
+    st.copy_(snap[0]), cnt.copy_(snap[1])
+    gs = torch.cuda.Stream(device=dev)
+    gs.wait_stream(torch.cuda.current_stream(dev))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(gs):
+        with torch.cuda.graph(graph, stream=gs):
+            go()
+    torch.cuda.synchronize()
+    st.copy_(snap[0]), cnt.copy_(snap[1])
+    graph.replay()  # warm
+    st.copy_(snap[0]), cnt.copy_(snap[1])
+    wall_g, s_g, _ = timed(graph.replay)
+    out["hipgraph"] = {"value": B2 * K2 / wall_g, "ms_per_step": wall_g / K2 * 1e3, "kernel_ms": s_g * 1e3}
+    del graph
+    return out
 
 
 def search_variants(dev) -> dict:
