@@ -234,7 +234,8 @@ struct Engine {
         L = L_;
         kw = acx_key_words(L);
         pk = (HDR + 6 * L + 63) / 64;
-        frontier.pk = unexpanded.pk = pk;
+        frontier.init(pk);
+        unexpanded.init(pk);
         cyc = cyc_;
         max_nodes = max_nodes_;
         cap = max_nodes + 12;
@@ -420,12 +421,45 @@ struct Engine {
         }
         const uint64_t* top_key() const { return k.data(); }
     };
-    Heap frontier;    // every node not popped yet: the reference's to_explore (pop order)
+    // one heap per total (the priority key's top 9 bits): a pop sifts through the nodes of the
+    // smallest total only, not the whole frontier (10^6 nodes: ~10 cold levels per pop); the order
+    // is the single heap's, since the total is the key's most significant field
+    struct BucketHeap {
+        static constexpr int NB = 512;
+        int pk = 0;
+        int minb = NB;  // the smallest non-empty bucket (NB: none)
+        size_t n = 0;
+        std::vector<Heap> b;
+        void init(int pk_) {
+            pk = pk_;
+            b.assign(NB, Heap{});
+            for (Heap& h : b) h.pk = pk;
+            minb = NB;
+            n = 0;
+        }
+        static int bucket_of(const uint64_t* key) { return (int)(key[0] >> 55); }
+        bool empty() const { return n == 0; }
+        size_t size() const { return n; }
+        void push(const uint64_t* key, int64_t v) {
+            const int i = bucket_of(key);
+            b[(size_t)i].push(key, v);
+            if (i < minb) minb = i;
+            ++n;
+        }
+        int64_t top() const { return b[(size_t)minb].top(); }
+        const uint64_t* top_key() const { return b[(size_t)minb].top_key(); }
+        void pop() {
+            b[(size_t)minb].pop();
+            --n;
+            while (minb < NB && b[(size_t)minb].empty()) ++minb;
+        }
+    };
+    BucketHeap frontier;  // every node not popped yet: the reference's to_explore (pop order)
     // cached expansions in round order, to retire the ones that aged (their node then counts as
     // unexpanded again and is picked up by select() with the other smallest unexpanded nodes)
     std::vector<std::pair<int32_t, int64_t>> cache_fifo;
     size_t fifo_head = 0;
-    Heap unexpanded;  // the frontier nodes without usable cached children (expansion order)
+    BucketHeap unexpanded;  // the frontier nodes without usable cached children (expansion order)
 
     // ---------------------------------------------------------------- in-flight table
     static uint64_t tag_of(uint64_t h) { return (h >> 48) & 0xffffu; }
@@ -593,8 +627,6 @@ struct Engine {
         total.reserve(nres);
         depth.reserve(nres);
         cache_slot.reserve(nres);
-        frontier.reserve(nres);
-        unexpanded.reserve(nres);
         for (auto& g : gen) g.assign((size_t)2 * age, 0ull);
         gmask = 2 * age - 1;
         cur = 0;
