@@ -134,17 +134,19 @@ __device__ __forceinline__ void st_scalar(T* p, T v) {
     else *p = v;
 }
 
-// SWAR: 4 int8 letters (one dword) -> 8-bit code field (2 bits per letter, x=0 X=1 y=2 Y=3,
-// zero letters -> 0) and a 4-bit non-zero mask
-__device__ __forceinline__ void swar_pack4(uint32_t d, uint32_t& c8, uint32_t& nz4) {
-    const uint32_t nz = (d | (d >> 1)) & 0x01010101u;            // letter != 0
-    const uint32_t c1 = ~d & nz;                                  // code bit 1: |letter| == 2
-    const uint32_t c0 = (d >> 7) & 0x01010101u;                   // code bit 0: letter < 0
-    const uint32_t cb = (c1 << 1) | c0;                           // one code per byte
-    const uint32_t t = cb | (cb >> 6);
-    c8 = (t & 0xfu) | ((t >> 12) & 0xf0u);
-    const uint32_t u = nz | (nz >> 7);
-    nz4 = (u & 3u) | ((u >> 14) & 0xcu);
+// 4 int8 letters (one dword) -> 8-bit code field (2 bits per letter, x=0 X=1 y=2 Y=3, zero
+// letters -> 0) and a 4-bit non-zero mask.  A letter's low 3 bits index an 8-entry byte table
+// (v_perm_b32: 0 -> 0, 1 (x), 2 (y), 6 (Y = -2), 7 (X = -1)), and v_dot4_u32_u8 folds the four
+// per-byte results into their fields (weights 1, 4, 16, 64 for the codes, 1, 2, 4, 8 for the
+// mask): 6 VALU where a shift-and-mask SWAR took ~16.  Bytes outside {0, +-1, +-2} give
+// arbitrary codes (their rows are flagged and never decoded from the tile); 0x7F, to_i8's
+// out-of-domain byte, counts as non-zero.
+__device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& nz4) {
+    const uint32_t m = d & 0x07070707u;
+    const uint32_t codes = __builtin_amdgcn_perm(0x01030000u, 0x00020000u, m);
+    const uint32_t nz = __builtin_amdgcn_perm(0x01010101u, 0x01010100u, m);
+    c8 = __builtin_amdgcn_udot4(codes, 0x40100401u, 0u, false);
+    nz4 = __builtin_amdgcn_udot4(nz, 0x08040201u, 0u, false);
 }
 
 // the step kernel's L = 128 tile load: chunks converted by chunk_i8 into a lane-fixed slot
@@ -162,6 +164,18 @@ __device__ __forceinline__ uint32_t chunk_i8(const int4& v, bool& bad) {
     const int mx = max(max(v.x, v.y), max(v.z, v.w));
     const int mn = min(min(v.x, v.y), min(v.z, v.w));
     bad = mx > 2 || mn < -2;
+    return lo | hi;
+}
+
+// chunk_i8 with the range test folded into a running max / min of the letters (two v_max3 and
+// two v_min3 per chunk, no compare): some letter is outside {-2..2} <=> mx > 2 or mn < -2
+__device__ __forceinline__ uint32_t chunk_i8_acc(const int4& v, int& mx, int& mn) {
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, 0x04000c0cu);
+    mx = max(max(mx, v.x), v.y);
+    mx = max(max(mx, v.z), v.w);
+    mn = min(min(mn, v.x), v.y);
+    mn = min(min(mn, v.z), v.w);
     return lo | hi;
 }
 
@@ -664,7 +678,7 @@ struct FastTile {
 #pragma unroll
             for (int k = 0; k < HALF; ++k) {
                 uint32_t c8, nz4;
-                swar_pack4(d[h * HALF + k], c8, nz4);
+                pack4_codes(d[h * HALF + k], c8, nz4);
                 w.w[k >> 2] |= c8 << (8 * (k & 3));
                 if (k < 16) mlo |= (uint64_t)nz4 << (4 * k);
                 else mhi |= (uint64_t)nz4 << (4 * (k - 16));
@@ -923,14 +937,13 @@ struct CodeTile {
                         }
                     }
                 };
+                int mx = 0, mn = 0;  // running max / min of every loaded letter (dead chunks load 0)
                 auto convert = [&](const int4* v, int u0) {
 #pragma unroll
                     for (int u = 0; u < LOAD_BATCH; ++u) {
-                        bool bad = false;
                         uint32_t c8, nz4;
-                        swar_pack4(chunk_i8(v[u], bad), c8, nz4);
+                        pack4_codes(chunk_i8_acc(v[u], mx, mn), c8, nz4);
                         mine[(u0 + u) * 2 * S] = (uint16_t)(c8 | (nz4 << 8));
-                        any_bad |= bad;
                     }
                 };
                 static_assert(CPR % (2 * LOAD_BATCH) == 0, "pipelined tile load: whole batch pairs");
@@ -942,6 +955,7 @@ struct CodeTile {
                     if (u0 + 2 * LOAD_BATCH < CPR) issue(va, u0 + 2 * LOAD_BATCH);
                     convert(vb, u0 + LOAD_BATCH);
                 }
+                any_bad = mx > 2 || mn < -2;
                 tile_bad = __any(any_bad);
                 if (tile_bad) {  // rare (wave-uniform)
                     bool rb = false;
@@ -968,7 +982,7 @@ struct CodeTile {
                             const uint32_t d = to_i8(v.x, b) | (to_i8(v.y, b) << 8) | (to_i8(v.z, b) << 16) |
                                                (to_i8(v.w, b) << 24);
                             uint32_t c8, nz4;
-                            swar_pack4(d, c8, nz4);
+                            pack4_codes(d, c8, nz4);
                             slots(ln)[k] = (uint16_t)(c8 | (nz4 << 8) | ((uint32_t)b << 12));
                         }
                     }
@@ -1004,7 +1018,7 @@ struct CodeTile {
                         const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
                                            (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
                         uint32_t c8, nz4;
-                        swar_pack4(d, c8, nz4);
+                        pack4_codes(d, c8, nz4);
                         slot = c8 | (nz4 << 8) | ((uint32_t)bad << 12);
                     }
                     put(c, slot);
@@ -1044,7 +1058,7 @@ struct CodeTile {
                         const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) |
                                            (to_i8(v[u].z, bad) << 16) | (to_i8(v[u].w, bad) << 24);
                         uint32_t c8, nz4;
-                        swar_pack4(d, c8, nz4);
+                        pack4_codes(d, c8, nz4);
                         slot = c8 | (nz4 << 8) | ((uint32_t)bad << 12);
                     }
                     put(c, slot);
@@ -1078,7 +1092,7 @@ struct CodeTile {
             const uint32_t d = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) | (to_i8(v[u].z, bad) << 16) |
                                (to_i8(v[u].w, bad) << 24);
             uint32_t c8, nz4;
-            swar_pack4(d, c8, nz4);
+            pack4_codes(d, c8, nz4);
             put(c, c8 | (nz4 << 8) | ((uint32_t)bad << 12));
             if (bad) flags[c / CPR] = 1;
         }
@@ -1099,7 +1113,7 @@ struct CodeTile {
                 const uint32_t d = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
                                    (to_i8(v.w, bad) << 24);
                 uint32_t c8, nz4;
-                swar_pack4(d, c8, nz4);
+                pack4_codes(d, c8, nz4);
                 slots(r)[c] = (uint16_t)(c8 | (nz4 << 8) | ((uint32_t)bad << 12));
                 if (bad) flags[r] = 1;
                 any_bad |= bad;
