@@ -152,6 +152,10 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 // the step kernel's L = 128 tile load: chunks converted by chunk_i8 into a lane-fixed slot
 // address, rows flagged from one wave-wide bad mask at the end (A/B knob: 0 = the per-letter
 // to_i8 conversion and a per-chunk flag store)
+// A/B knob: extra LDS bytes per step-kernel block (occupancy probes; 0 in the product)
+#ifndef ACX_STEP_LDS_PAD
+#define ACX_STEP_LDS_PAD 0
+#endif
 #ifndef ACX_FAST_CONVERT
 #define ACX_FAST_CONVERT 1
 #endif
@@ -2857,7 +2861,7 @@ static inline unsigned grid_for(int64_t rows) {
 // while the main object declares them `extern template` below.
 template <int NW, int LC, int VEC, bool LEARN>
 int launch_step(StepArgs a, hipStream_t s) {
-    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L) + ACX_STEP_LDS_PAD;
     if (!LEARN && a.live)
         step_lengths_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     else

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--steps", type=int, default=210)
     ap.add_argument("--L", type=int, default=128)
     ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--ceiling-at", type=int, default=0,
+                    help="after the timed walk, replay to this step and run the bare live-chunk read "
+                         "shape (tools/stream_ceiling.hip live_tile) on that state and its lengths")
     a = ap.parse_args()
     from acx import ops
 
@@ -78,11 +81,49 @@ def main():
              "live_TBps": round(lb / m / 1e9, 3), "sector_TBps": round(sb / m / 1e9, 3)}
             for t, m, lb, sb in zip(range(1, K), ms, live, sect)]
     tot_ms = sum(ms)
+    ceil = None
+    if a.ceiling_at:
+        import ctypes
+        import subprocess
+        so = os.path.join(REPO, "tools", "libstream_ceiling.so")
+        src = os.path.join(REPO, "tools", "stream_ceiling.hip")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared",
+                                   "-fPIC", src, "-o", so])
+        cl = ctypes.CDLL(so)
+        cl.probe_live.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p]
+        for x, y in zip((st, cnt, lens), snap):
+            x.copy_(y)
+        for t in range(1, a.ceiling_at):
+            step(acts[t])
+        lb = float(((lens.clamp(0, L) + 3) // 4).sum().item()) * 16
+        sbytes = float(((lens.clamp(0, L) + 15) // 16).sum().item()) * 64
+        scratch = st.clone()
+        outb = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+        ceil = {"at_step": a.ceiling_at, "live_read_MB": round(lb / 1e6, 1), "sector_read_MB": round(sbytes / 1e6, 1)}
+        for wr in (0, 1):
+            for lds, occ in ((40 * 1024, 4), (20 * 1024, 8)):
+                ts = []
+                for r in range(6):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    assert cl.probe_live(wr, scratch.data_ptr(), lens.data_ptr(), B, lds, outb.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream) == 0
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if r:
+                        ts.append(e0.elapsed_time(e1))
+                m = statistics.median(ts)
+                ceil[f"{'rw' if wr else 'read'}_occ{occ}"] = {"ms": round(m, 4), "live_read_TBps": round(lb / m / 1e9, 3),
+                                                             "sector_read_TBps": round(sbytes / m / 1e9, 3)}
+        del scratch
     out = {"what": "tools/step_horizon.py: acx_step_lengths launch by launch on the bench's config-5 walk "
                    f"(L={L}, B={B}, horizon {H}, steps 1..{K - 1}; step 0 read whole rows)",
            "total_ms": round(tot_ms, 3), "live_TBps_overall": round(sum(live) / tot_ms / 1e9, 3),
            "sector_TBps_overall": round(sum(sect) / tot_ms / 1e9, 3),
-           "median_ms": round(statistics.median(ms), 4), "err_count": int(ec.item()), "launches": rows}
+           "median_ms": round(statistics.median(ms), 4), "err_count": int(ec.item()), "ceiling": ceil,
+           "launches": rows}
     print(json.dumps(out))
 
 

@@ -7,6 +7,11 @@
 //                 (>= NB loads always in flight)
 //   rw_tile       read_tile + a write of the first WQ/4 of every row in place (1 : WQ/4)
 //   rw_tile_pipe  read_tile_pipe + the same write
+//   live_tile<WR> (L = 128) the lengths-carrying step's read shape: a wave per 64 rows, row u per
+//                 wave-instruction, lane = chunk, only the chunks inside each relator's letters
+//                 loaded (a buffer descriptor, dead chunks at an out-of-range offset), 8..16 loads
+//                 in flight; WR: then the first relator's live chunks of every third row written
+//                 back (~the step's changed-relator writes)
 // One block = 4 waves (256 threads) as the step kernel; LDS per block sized for the occupancy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -77,7 +82,65 @@ __global__ __launch_bounds__(256) void tile_kernel(int4* __restrict__ st, int cp
     if (acc == 0x7fffffff) out[blockIdx.x] = acc;
 }
 
+template <bool WR>
+__global__ __launch_bounds__(256) void live_tile(int4* __restrict__ st, const int* __restrict__ lens, int64_t rows,
+                                                 int* out) {
+    extern __shared__ int smem[];
+    constexpr int CPR = 64, HALF = 32, NB = 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WAVE;
+    if (r0 >= rows) return;
+    const int l0 = (min(lens[2 * (r0 + lane)], 128) + 3) >> 2, l1 = (min(lens[2 * (r0 + lane) + 1], 128) + 3) >> 2;
+    const uint32_t limv = (uint32_t)l0 | ((uint32_t)l1 << 8);
+    const uint64_t gb = reinterpret_cast<uint64_t>(st + r0 * CPR);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(gb), (short)0,
+                                                                        WAVE * CPR * 16, 0x00020000);
+    const uint32_t lane_off = (uint32_t)lane * 16u, oob = 0x80000000u;
+    int acc = 0;
+    int4 a[NB], b[NB];
+    auto issue = [&](int4* v, int u0) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const uint32_t lu = (uint32_t)__builtin_amdgcn_readlane((int)limv, u0 + u);
+            const uint32_t c0 = lu & 0xffu, c1 = (lu >> 8) & 0xffu;
+            const uint64_t m = ((1ull << c0) - 1ull) | (((1ull << c1) - 1ull) << HALF);
+            uint32_t off;
+            asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(off) : "v"(oob), "v"(lane_off), "s"(m));
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, (u0 + u) * WAVE * 16, 0);
+            v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
+        }
+    };
+    auto use = [&](const int4* v) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        smem[threadIdx.x] = acc;
+    };
+    issue(a, 0);
+    for (int u0 = 0; u0 < CPR; u0 += 2 * NB) {
+        issue(b, u0 + NB);
+        use(a);
+        if (u0 + 2 * NB < CPR) issue(a, u0 + 2 * NB);
+        use(b);
+    }
+    if constexpr (WR) {
+        for (int r = 0; r < WAVE; r += 3) {
+            const int lr = __builtin_amdgcn_readlane(l0, r);
+            if (lane < lr) st[(r0 + r) * CPR + lane] = make_int4(acc, r, lane, 0);  // the probe's state is scratch
+        }
+    }
+    if (acc == 0x7fffffff) out[blockIdx.x] = acc;
+}
+
 extern "C" {
+// the live-chunk read shape at L = 128 over rows with the given relator lengths (B, 2) int32
+int probe_live(int wr, void* state, const void* lengths, int64_t rows, int lds_per_block, void* out, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned tiles = (unsigned)((rows + 255) / 256);
+    if (wr) live_tile<true><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
+    else live_tile<false><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
+    return (int)hipGetLastError();
+}
+
 // kind: 0 read_grid, 1 read_tile, 2 read_tile_pipe, 3 rw_tile, 4 rw_tile_pipe; nb in {8, 16};
 // lds_per_block bytes of dynamic LDS (occupancy control); returns 0 or a hip error code
 int probe_run(int kind, int nb, void* state, int64_t rows, int L, int lds_per_block, void* out, void* stream) {
