@@ -102,7 +102,7 @@ def main():
         scratch = st.clone()
         outb = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
         ceil = {"at_step": a.ceiling_at, "live_read_MB": round(lb / 1e6, 1), "sector_read_MB": round(sbytes / 1e6, 1)}
-        for wr in (0, 1):
+        for wr in (0, 1, 2):
             for lds, occ in ((40 * 1024, 4), (20 * 1024, 8)):
                 ts = []
                 for r in range(6):
@@ -115,7 +115,7 @@ def main():
                     if r:
                         ts.append(e0.elapsed_time(e1))
                 m = statistics.median(ts)
-                ceil[f"{'rw' if wr else 'read'}_occ{occ}"] = {"ms": round(m, 4), "live_read_TBps": round(lb / m / 1e9, 3),
+                ceil[f"{('read', 'rw', 'rw_sectors')[wr]}_occ{occ}"] = {"ms": round(m, 4), "live_read_TBps": round(lb / m / 1e9, 3),
                                                              "sector_read_TBps": round(sbytes / m / 1e9, 3)}
         del scratch
     out = {"what": "tools/step_horizon.py: acx_step_lengths launch by launch on the bench's config-5 walk "

@@ -11,7 +11,7 @@
 //                 wave-instruction, lane = chunk, only the chunks inside each relator's letters
 //                 loaded (a buffer descriptor, dead chunks at an out-of-range offset), 8..16 loads
 //                 in flight; WR: then the first relator's live chunks of every third row written
-//                 back (~the step's changed-relator writes)
+//                 back (~the step's changed-relator writes); WR = 2: rounded up to whole 64-B sectors
 // One block = 4 waves (256 threads) as the step kernel; LDS per block sized for the occupancy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void tile_kernel(int4* __restrict__ st, int cp
     if (acc == 0x7fffffff) out[blockIdx.x] = acc;
 }
 
-template <bool WR>
+template <int WR>
 __global__ __launch_bounds__(256) void live_tile(int4* __restrict__ st, const int* __restrict__ lens, int64_t rows,
                                                  int* out) {
     extern __shared__ int smem[];
@@ -122,9 +122,10 @@ __global__ __launch_bounds__(256) void live_tile(int4* __restrict__ st, const in
         if (u0 + 2 * NB < CPR) issue(a, u0 + 2 * NB);
         use(b);
     }
-    if constexpr (WR) {
+    if constexpr (WR > 0) {
         for (int r = 0; r < WAVE; r += 3) {
-            const int lr = __builtin_amdgcn_readlane(l0, r);
+            int lr = __builtin_amdgcn_readlane(l0, r);
+            if (WR == 2) lr = min((lr + 3) & ~3, HALF);  // whole 64-B sectors
             if (lane < lr) st[(r0 + r) * CPR + lane] = make_int4(acc, r, lane, 0);  // the probe's state is scratch
         }
     }
@@ -136,8 +137,9 @@ extern "C" {
 int probe_live(int wr, void* state, const void* lengths, int64_t rows, int lds_per_block, void* out, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const unsigned tiles = (unsigned)((rows + 255) / 256);
-    if (wr) live_tile<true><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
-    else live_tile<false><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
+    if (wr == 2) live_tile<2><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
+    else if (wr) live_tile<1><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
+    else live_tile<0><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>((int4*)state, (const int*)lengths, rows, (int*)out);
     return (int)hipGetLastError();
 }
 
