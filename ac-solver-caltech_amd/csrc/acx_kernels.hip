@@ -152,6 +152,19 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 // the step kernel's L = 128 tile load: chunks converted by chunk_i8 into a lane-fixed slot
 // address, rows flagged from one wave-wide bad mask at the end (A/B knob: 0 = the per-letter
 // to_i8 conversion and a per-chunk flag store)
+// Non-temporal stores for the in-place step's write-back of changed relators (`ACX_NT_WRITEBACK`):
+// nothing reads those lines again inside the launch, and plain stores kept them in L2 beside the
+// tile loads (same buffers: L = 128 0.2727 -> 0.2581 ms, lengths-carrying 0.2302 -> 0.2102, L = 36
+// 0.0742 -> 0.0697; profiles/r04/r04z_ab_nt*.json).  Whole output rows (`ACX_NT_STATE`: the
+// out-of-place step, the rollout's final state, canonicalized rows, expanded children) stay plain:
+// non-temporal made the rollout slower (K = 20 int32 1.332 -> 1.351 ms, int8 0.447 -> 0.477; its
+// next launch reads that state) and expand12's children no faster (0.778 -> 0.772 ms).
+#ifndef ACX_NT_WRITEBACK
+#define ACX_NT_WRITEBACK 1
+#endif
+#ifndef ACX_NT_STATE
+#define ACX_NT_STATE 0
+#endif
 // A/B knob: extra LDS bytes per step-kernel block (occupancy probes; 0 in the product)
 #ifndef ACX_STEP_LDS_PAD
 #define ACX_STEP_LDS_PAD 0
@@ -1748,7 +1761,7 @@ struct GenericTile {
     __device__ __forceinline__ void widen_lim(int, int, int) const {}
     template <bool NT, bool LIVE = false>
     __device__ __forceinline__ void store_dirty(int32_t* g, int R, int lane, const int32_t* fallback2 = nullptr) const {
-        store<true>(g, twoL, R, g, twoL, lane, fallback2);
+        store<true, NT>(g, twoL, R, g, twoL, lane, fallback2);
     }
 };
 
@@ -2020,14 +2033,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         wave_sync();
         if (__ballot(dm != 0u)) {
             if constexpr (LIVE)
-                tile.template store_dirty<false, true>(a.state_out + w.r0 * twoL, w.R, w.lane,
+                tile.template store_dirty<ACX_NT_WRITEBACK != 0, true>(a.state_out + w.r0 * twoL, w.R, w.lane,
                                                        a.reset_state + w.r0 * twoL);
             else
-                tile.template store_dirty<false>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
+                tile.template store_dirty<ACX_NT_WRITEBACK != 0>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
         }
     } else {
         wave_sync();
-        tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane,
+        tile.template store<true, ACX_NT_STATE != 0>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL,
+                                                     twoL, w.lane,
                                   a.reset_state + w.r0 * twoL);
     }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
@@ -2280,8 +2294,8 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     }
     // out-of-domain rows: their input row (untouched in HBM), or the starting row they reset to
     tile.restore_flags(w.lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
-    tile.template store<true>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL, w.lane,
-                              a.reset_state + w.r0 * twoL);
+    tile.template store<true, ACX_NT_STATE != 0>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
+                                                 w.lane, a.reset_state + w.r0 * twoL);
 }
 
 // Move ids (T, B) int32 -> (ceil(T/8), B) uint32, 8 consecutive steps of one env per word,
@@ -2403,7 +2417,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
         }
         if (a.children) {
             wave_sync();
-            tile.template store<true>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
+            tile.template store<true, ACX_NT_STATE != 0>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
                                       a.parents + w.r0 * twoL, twoL, w.lane);
             wave_sync();
         }
@@ -2597,7 +2611,7 @@ __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) 
             if (!bad) tile.unpack(lane, q);
         }
         wave_sync();
-        tile.template store<true>(a.children + (r0 * 12 + act) * twoL, (int64_t)12 * twoL, R,
+        tile.template store<true, ACX_NT_STATE != 0>(a.children + (r0 * 12 + act) * twoL, (int64_t)12 * twoL, R,
                                   a.parents + r0 * twoL, twoL, lane);
         wave_sync();
     }
@@ -2777,7 +2791,8 @@ __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
     }
     tile.flag_rows(w.lane, bad ? FB_IN : 0u);  // incl. a zero inside a relator (not flagged by the load)
     wave_sync();
-    tile.template store<true>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL, w.lane);
+    tile.template store<true, ACX_NT_STATE != 0>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL,
+                                                 w.lane);
 }
 
 struct UnpackArgs {
