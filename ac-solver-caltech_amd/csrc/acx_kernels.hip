@@ -165,6 +165,26 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_NT_STATE
 #define ACX_NT_STATE 0
 #endif
+// A/B knob: the step kernel's per-env outputs (reward, done, truncated, step count, lengths, err)
+// with non-temporal stores
+#ifndef ACX_NT_STEP_SCALARS
+#define ACX_NT_STEP_SCALARS 0
+#endif
+// Non-temporal tile loads (NTL): the state rows are read once per launch.  Taken where it
+// measured faster (same buffers, profiles/r04/r04z_ab_ld*.json): the L = 128 step (CodeTile:
+// 0.2587 -> 0.2432 ms, lengths-carrying 0.2105 -> 0.1991) and the rollout's state in (int8
+// trajectory 0.4635 -> 0.4402 ms, int32 1.3235 -> 1.3131); not the L = 36 step, whose write-back
+// of relators that are not sector-aligned (288-B rows) then went 0.0699 -> 0.0944 ms.
+template <bool NT>
+__device__ __forceinline__ int4 ld_tile(const int4* p) {
+    if constexpr (NT) {
+        const v4i_t x = __builtin_nontemporal_load(reinterpret_cast<const v4i_t*>(p));
+        return make_int4(x[0], x[1], x[2], x[3]);
+    } else {
+        return *p;
+    }
+}
+constexpr int tile_cpol(bool nt) { return nt ? 2 : 0; }  // buffer-load cache policy: the gfx94x/950 NT bit
 // A/B knob: extra LDS bytes per step-kernel block (occupancy probes; 0 in the product)
 #ifndef ACX_STEP_LDS_PAD
 #define ACX_STEP_LDS_PAD 0
@@ -291,7 +311,7 @@ struct FastTile {
     // loop is unrolled already).  LIVE (the lengths-carrying step; lim[] set for every row): only
     // the chunks inside each relator's letters are read, the rest of the image is zero (the rows
     // are canonical: letters, then zero padding)
-    template <bool PIPE = false, bool LIVE = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));  // keep the address math here (no hoisting into the caller)
@@ -319,10 +339,10 @@ struct FastTile {
                     lv[u] = true;
                     if constexpr (LIVE) {
                         const uint32_t off = live(c / CPR, c % CPR) ? (uint32_t)c * 16u : 0x80000000u;
-                        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, 0, 0);
+                        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, 0, tile_cpol(NTL));
                         v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
                     } else {
-                        v[u] = src[(u0 + u) * WAVE];
+                        v[u] = ld_tile<NTL>(src + (u0 + u) * WAVE);
                     }
                 }
 #pragma unroll
@@ -350,7 +370,7 @@ struct FastTile {
                     bool bad = false;
                     uint32_t p = 0;
                     if (!LIVE || live(r, c - r * CPR)) {
-                        const int4 v = src[u * WAVE];
+                        const int4 v = ld_tile<NTL>(src + u * WAVE);
                         p = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) | (to_i8(v.w, bad) << 24);
                     }
                     lds[r * S + (c - r * CPR)] = p;
@@ -459,6 +479,7 @@ struct FastTile {
     // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load).
     // [UB, UE): a range of the lane's chunk slots only (the rollout's split obs store)
     static constexpr bool SPLIT_OK = true;
+    static constexpr bool NT_STEP_LOADS = false;  // see ld_tile
     template <bool NT, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
         int ln = lane;
@@ -844,6 +865,7 @@ struct CodeTile {
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
+    static constexpr bool NT_STEP_LOADS = true;  // see ld_tile
     __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
         flags[lane] = (uint8_t)code;
         tile_bad = __any(code != 0u);
@@ -903,7 +925,7 @@ struct CodeTile {
 
     // PIPE (the step kernel; the rollout keeps the plain loop, whose register budget the
     // in-flight batch pair would exceed): full tiles software-pipelined, see below
-    template <bool PIPE = false, bool LIVE = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -947,10 +969,10 @@ struct CodeTile {
                             const uint64_t m = ((1ull << l0) - 1ull) | (((1ull << l1) - 1ull) << 32);
                             uint32_t off;
                             asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(off) : "v"(oob), "v"(lane_off), "s"(m));
-                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, (u0 + u) * WAVE * 16, 0);
+                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rows, off, (u0 + u) * WAVE * 16, tile_cpol(NTL));
                             v[u] = make_int4((int)x[0], (int)x[1], (int)x[2], (int)x[3]);
                         } else {
-                            v[u] = src[(u0 + u) * WAVE];
+                            v[u] = ld_tile<NTL>(src + (u0 + u) * WAVE);
                         }
                     }
                 };
@@ -1023,7 +1045,7 @@ struct CodeTile {
             auto issue = [&](int4* v, int u0) {
 #pragma unroll
                 for (int u = 0; u < LOAD_BATCH; ++u)
-                    if (lv(u0 + u)) v[u] = src[(u0 + u) * WAVE];
+                    if (lv(u0 + u)) v[u] = ld_tile<NTL>(src + (u0 + u) * WAVE);
             };
             auto convert = [&](const int4* v, int u0) {
 #pragma unroll
@@ -1063,7 +1085,7 @@ struct CodeTile {
             for (int u = 0; u < LOAD_BATCH; ++u) {
                 const int c = ln + (u0 + u) * WAVE;
                 lv[u] = c < nc && (!LIVE || live(c / CPR, c % CPR));
-                if (lv[u]) v[u] = src[(u0 + u) * WAVE];
+                if (lv[u]) v[u] = ld_tile<NTL>(src + (u0 + u) * WAVE);
             }
 #pragma unroll
             for (int u = 0; u < LOAD_BATCH; ++u) {
@@ -1510,6 +1532,7 @@ struct CodeTile {
 template <int NW, int LC, int VEC>
 struct GenericTile {
     static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
+    static constexpr bool NT_STEP_LOADS = false;  // see ld_tile
     static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
     int L, twoL, rowb;
     char* base;
@@ -1580,7 +1603,7 @@ struct GenericTile {
     };
 
     // PIPE, LIVE: see CodeTile::load (the runtime-L path reads and writes whole rows)
-    template <bool PIPE = false, bool LIVE = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         flags[lane] = 0;
         wave_sync();
@@ -1880,6 +1903,7 @@ struct StepArgs {
 template <int NW, int LC, int VEC, bool LEARN, bool LIVE>
 __device__ __forceinline__ void step_body(const StepArgs& a) {
     using Tile = TileFor<NW, LC, VEC>;
+    constexpr bool NT_SC = ACX_NT_STEP_SCALARS != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
     if (!wave_ctx(a.B, w)) return;
@@ -1909,9 +1933,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         tile.set_lim(w.lane, n_in0, n_in1);
         wave_sync();
-        tile.template load<ACX_PIPE_LOAD != 0, true>(a.state_in + w.r0 * twoL, w.R, w.lane);
+        tile.template load<ACX_PIPE_LOAD != 0, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     } else {
-        tile.template load<ACX_PIPE_LOAD != 0>(a.state_in + w.r0 * twoL, w.R, w.lane);
+        tile.template load<ACX_PIPE_LOAD != 0, false, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     }
 
     bool fin = false;    // done | truncated (the curriculum's "finished")
@@ -1956,9 +1980,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         const bool trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
         // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does
         const int32_t rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
-        if (a.reward) a.reward[env] = rwd;
-        if (a.done) a.done[env] = triv;
-        if (a.truncated) a.truncated[env] = trunc;
+        if (a.reward) st_scalar<NT_SC, int32_t>(a.reward + env, rwd);
+        if (a.done) st_scalar<NT_SC, uint8_t>(a.done + env, (uint8_t)triv);
+        if (a.truncated) st_scalar<NT_SC, uint8_t>(a.truncated + env, (uint8_t)trunc);
         fin = triv || trunc;
         if constexpr (LEARN) {
             if (a.reward_f32) a.reward_f32[env] = (float)rwd;
@@ -2007,14 +2031,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (reset) cnt = 0;
     }
     if (w.active) {
-        if (a.step_count) a.step_count[env] = cnt;
+        if (a.step_count) st_scalar<NT_SC, int32_t>(a.step_count + env, cnt);
         if (a.lengths_out) {
             // lengths-carrying step: an out-of-domain row is read whole on the next call (L, L)
             const bool whole = LIVE && e == ACX_ERR_DOMAIN;
-            a.lengths_out[2 * env] = whole ? L : p.n0;
-            a.lengths_out[2 * env + 1] = whole ? L : p.n1;
+            st_scalar<NT_SC, int32_t>(a.lengths_out + 2 * env, whole ? L : p.n0);
+            st_scalar<NT_SC, int32_t>(a.lengths_out + 2 * env + 1, whole ? L : p.n1);
         }
-        if (a.err) a.err[env] = (uint8_t)e;
+        if (a.err) st_scalar<NT_SC, uint8_t>(a.err + env, (uint8_t)e);
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
     if constexpr (LEARN) {
@@ -2108,7 +2132,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     bool bad_reset = false;  // the out-of-domain row is the env's starting row (FB_RESET)
     constexpr int PW = Tile::PW;
     PlaneRegs<PW> p;
-    tile.load(a.state + w.r0 * twoL, w.R, w.lane);
+    tile.template load<false, false, true>(a.state + w.r0 * twoL, w.R, w.lane);
     int first_err = ACX_ERR_NONE;
     int cnt = 0;
     const bool cyc = a.cyclical != 0;
