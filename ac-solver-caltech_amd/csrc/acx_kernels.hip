@@ -165,6 +165,15 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_NT_STATE
 #define ACX_NT_STATE 0
 #endif
+// expand12's parent loads and packed-key stores non-temporal (keys as 16-B stores): same buffers,
+// 4M parents (profiles/r04/r04z_ab_keys.json): 0.4246 ms (0.71 of 8 TB/s) -> 0.380 ms (0.79) with
+// both; the loads alone 0.4085, the stores alone 0.5101 (slower); the children kernel unchanged
+#ifndef ACX_NT_EXPAND_LOADS
+#define ACX_NT_EXPAND_LOADS 1
+#endif
+#ifndef ACX_NT_KEYS
+#define ACX_NT_KEYS 1
+#endif
 // A/B knob: the step kernel's per-env outputs (reward, done, truncated, step count, lengths, err)
 // with non-temporal stores
 #ifndef ACX_NT_STEP_SCALARS
@@ -414,7 +423,7 @@ struct FastTile {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = (int)threadIdx.x + u * BLOCK;
-            if (c < nc) v[u] = src[c];
+            if (c < nc) v[u] = ld_tile<ACX_NT_EXPAND_LOADS != 0>(src + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1121,7 +1130,7 @@ struct CodeTile {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = (int)threadIdx.x + u * BLOCK;
-            if (c < nc) v[u] = src[c];
+            if (c < nc) v[u] = ld_tile<ACX_NT_EXPAND_LOADS != 0>(src + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -2558,7 +2567,18 @@ __global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
     }
     __syncthreads();
     uint64_t* dst = a.child_key + r0 * 12 * kw;
-    for (int i = threadIdx.x; i < R * 12 * kw; i += BLOCK) dst[i] = kst[i];
+    if constexpr (ACX_NT_KEYS != 0) {
+        // 16-B non-temporal stores (dst is 16-B aligned: r0 is a multiple of 64), odd tail word apart
+        const int nw = R * 12 * kw;
+        for (int i = threadIdx.x; 2 * i + 1 < nw; i += BLOCK) {
+            typedef unsigned long long v2u_t __attribute__((ext_vector_type(2)));
+            const v2u_t x = {kst[2 * i], kst[2 * i + 1]};
+            __builtin_nontemporal_store(x, reinterpret_cast<v2u_t*>(dst) + i);
+        }
+        if ((nw & 1) && threadIdx.x == 0) dst[nw - 1] = kst[nw - 1];
+    } else {
+        for (int i = threadIdx.x; i < R * 12 * kw; i += BLOCK) dst[i] = kst[i];
+    }
     if (nerr && a.err_count) atomicAdd(a.err_count, nerr);
 }
 
