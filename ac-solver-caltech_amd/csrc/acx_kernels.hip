@@ -184,6 +184,9 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 // 0.2587 -> 0.2432 ms, lengths-carrying 0.2105 -> 0.1991) and the rollout's state in (int8
 // trajectory 0.4635 -> 0.4402 ms, int32 1.3235 -> 1.3131); not the L = 36 step, whose write-back
 // of relators that are not sector-aligned (288-B rows) then went 0.0699 -> 0.0944 ms.
+#ifndef ACX_NT_STEP_LOADS36
+#define ACX_NT_STEP_LOADS36 0  // FastTile (L % 4 == 0, not CodeTile) step loads: A/B knob
+#endif
 template <bool NT>
 __device__ __forceinline__ int4 ld_tile(const int4* p) {
     if constexpr (NT) {
@@ -488,7 +491,7 @@ struct FastTile {
     // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load).
     // [UB, UE): a range of the lane's chunk slots only (the rollout's split obs store)
     static constexpr bool SPLIT_OK = true;
-    static constexpr bool NT_STEP_LOADS = false;  // see ld_tile
+    static constexpr bool NT_STEP_LOADS = ACX_NT_STEP_LOADS36 != 0;  // see ld_tile
     template <bool NT, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
         int ln = lane;
