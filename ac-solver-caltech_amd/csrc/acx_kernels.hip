@@ -165,6 +165,14 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_NT_STATE
 #define ACX_NT_STATE 0
 #endif
+// The rollout's int32 trajectory stores (full tiles) through a buffer store with this cache policy
+// (gfx950 cpol bits: sc0 1, nt 2, sc1 16; -1: the global non-temporal store of ACX_NT_OBS).  sc1
+// (the line is not kept in the XCD's L2): same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059
+// and 1.3241 -> 1.3027 ms against nt, plain 1.2267 / 1.3195; K = 200 within 0.3 %
+// (profiles/r04/r04s_ab_obs_cpol*.json; the bare store pattern, r04s_cpol.json, orders them alike)
+#ifndef ACX_OBS_CPOL
+#define ACX_OBS_CPOL 16
+#endif
 // expand12's parent loads and packed-key stores non-temporal (keys as 16-B stores): same buffers,
 // 4M parents (profiles/r04/r04z_ab_keys.json): 0.4246 ms (0.71 of 8 TB/s) -> 0.380 ms (0.79) with
 // both; the loads alone 0.4085, the stores alone 0.5101 (slower); the children kernel unchanged
@@ -499,6 +507,31 @@ struct FastTile {
         int4* dst = reinterpret_cast<int4*>(g);
         const int nc = R * CPR;
         if (R == WAVE) {
+#if ACX_OBS_CPOL >= 0
+            if constexpr (NT) {  // the trajectory store with an explicit cache policy (A/B knob)
+                const uint64_t b = reinterpret_cast<uint64_t>(g);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, WAVE * CPR * 16, 0x00020000);
+#pragma unroll
+                for (int u0 = UB; u0 < UE; u0 += STAGE_UNROLL) {
+                    uint32_t p[STAGE_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < STAGE_UNROLL; ++u)
+                        if (u0 + u < UE) p[u] = lds[lds_index(ln, u0 + u)];
+#pragma unroll
+                    for (int u = 0; u < STAGE_UNROLL; ++u)
+                        if (u0 + u < UE) {
+                            const int4 v = widen4(p[u]);
+                            const v4i_t x = {v.x, v.y, v.z, v.w};
+                            __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (u0 + u) * WAVE) * 16u, 0,
+                                                                   ACX_OBS_CPOL);
+                        }
+                }
+                return;
+            }
+#endif
             store_flat<NT, false, true, UB, UE>(dst + ln, ln, nc);
             return;
         }

@@ -26,6 +26,28 @@ __device__ __forceinline__ void st_nt(int4* p, int4 v) {
     __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(p));
 }
 
+// the same 16-B store with the gfx950 cache-policy bits through a buffer store (aux = cpol:
+// sc0 = 1, nt = 2, sc1 = 16): sc1 stores do not keep the line in the XCD's L2
+template <int CPOL>
+__global__ __launch_bounds__(256) void tile_pol(int4* __restrict__ dst, int64_t rows, int cpr, int K, int v) {
+    typedef int v4i_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * WAVE;
+    if (r0 >= rows) return;
+    const int nch = WAVE * cpr;
+    for (int t = 0; t < K; ++t) {
+        // the wave's slice of step row t as one buffer (scalar base), lanes at their 16-B offsets
+        const uint64_t b = reinterpret_cast<uint64_t>(dst + ((int64_t)t * rows + r0) * cpr);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nch * 16, 0x00020000);
+        for (int c = lane; c < nch; c += WAVE) {
+            const v4i_t x = {v, t, c, lane};
+            __builtin_amdgcn_raw_buffer_store_b128(x, r, (uint32_t)c * 16u, 0, CPOL);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void fill_oneshot(int4* __restrict__ dst, int64_t n16, int v) {
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i < n16) st_nt(dst + i, make_int4(v, v, v, (int)i));
@@ -87,7 +109,8 @@ __global__ __launch_bounds__(256) void tile_oneshot(int4* __restrict__ dst, int6
 }
 
 extern "C" {
-// kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot, 4 tile_grouped (n = GE: 8, 16, 32); n: stores in flight per wave
+// kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot, 4 tile_grouped (n = GE: 8, 16, 32),
+// 5 tile with buffer stores of cache policy n (0 plain, 1 sc0, 2 nt, 16 sc1, 17 sc0 sc1, 18 sc1 nt); n: stores in flight per wave
 // (0 = unthrottled; 1, 2, 4, 8, 16); returns a hip error code
 int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin, int resident_blocks, void* stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -107,6 +130,11 @@ int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin
         switch (n) { case 0: T(0); break; case 1: T(1); break; case 2: T(2); break; case 4: T(4); break;
                      case 8: T(8); break; default: T(16); }
 #undef T
+    } else if (kind == 5) {
+#define Q(NN) tile_pol<NN><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7)
+        switch (n) { case 0: Q(0); break; case 1: Q(1); break; case 2: Q(2); break; case 16: Q(16); break;
+                     case 17: Q(17); break; default: Q(18); }
+#undef Q
     } else if (kind == 4) {
 #define G(NN) tile_grouped<NN><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7)
         switch (n) { case 8: G(8); break; case 16: G(16); break; default: G(32); }
