@@ -165,6 +165,13 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_NT_STATE
 #define ACX_NT_STATE 0
 #endif
+// The L = 128 in-place step's write-back (CodeTile) through a buffer store with this cache policy
+// (-1: the global store of ACX_NT_WRITEBACK).  sc1 (16), same buffers: lengths-carrying 0.1993 ->
+// 0.1791 ms, acx_step 0.2423 -> 0.2182 against nt; nt + sc1 0.1989 (profiles/r04/r04s_ab_wb_cpol.json).
+// sc1 / sc0 sc1 on the tile LOADS instead of nt: 0.2327 (r04s_ab_ld_cpol.json), so those stay nt.
+#ifndef ACX_WB_CPOL
+#define ACX_WB_CPOL 16
+#endif
 // The rollout's int32 trajectory stores (full tiles) through a buffer store with this cache policy
 // (gfx950 cpol bits: sc0 1, nt 2, sc1 16; -1: the global non-temporal store of ACX_NT_OBS).  sc1
 // (the line is not kept in the XCD's L2): same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059
@@ -204,7 +211,10 @@ __device__ __forceinline__ int4 ld_tile(const int4* p) {
         return *p;
     }
 }
-constexpr int tile_cpol(bool nt) { return nt ? 2 : 0; }  // buffer-load cache policy: the gfx94x/950 NT bit
+#ifndef ACX_LD_CPOL
+#define ACX_LD_CPOL 2  // A/B knob: the cache policy of the non-temporal buffer tile loads (nt = 2)
+#endif
+constexpr int tile_cpol(bool nt) { return nt ? ACX_LD_CPOL : 0; }  // buffer-load cache policy (gfx94x/950 bits)
 // A/B knob: extra LDS bytes per step-kernel block (occupancy probes; 0 in the product)
 #ifndef ACX_STEP_LDS_PAD
 #define ACX_STEP_LDS_PAD 0
@@ -864,8 +874,10 @@ struct FastTile {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < STAGE_UNROLL; ++u)
-                if (wr[u]) out16<NT, false>(dst + ln + (u0 + u) * WAVE, widen4(p[u]));
+            for (int u = 0; u < STAGE_UNROLL; ++u) {
+                if (!wr[u]) continue;
+                out16<NT, false>(dst + ln + (u0 + u) * WAVE, widen4(p[u]));
+            }
         }
     }
 
@@ -1489,6 +1501,13 @@ struct CodeTile {
             // address, row r's dirty bits and live counts read from lane r's registers (scalars)
             const uint16_t* mine = reinterpret_cast<const uint16_t*>(lds) + ln;
             const int hs = ln >= HALF ? 1 : 0;
+#if ACX_WB_CPOL >= 0
+            const uint64_t gb = reinterpret_cast<uint64_t>(g);
+            const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
+            const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
+#endif
             for (int r0 = 0; r0 < R; r0 += STAGE_UNROLL) {
                 uint32_t p[STAGE_UNROLL];
                 bool wr[STAGE_UNROLL];
@@ -1505,8 +1524,14 @@ struct CodeTile {
                 for (int u = 0; u < STAGE_UNROLL; ++u) {
                     if (!wr[u]) continue;
                     const uint32_t nz4 = (p[u] >> 8) & 0xfu;
+#if ACX_WB_CPOL >= 0
+                    const int4 v = widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4)));
+                    const v4i_t x = {v.x, v.y, v.z, v.w};
+                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (r0 + u) * WAVE) * 16u, 0, ACX_WB_CPOL);
+#else
                     out16<NT, false>(dst + ln + (r0 + u) * WAVE,
                                      widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
+#endif
                 }
             }
             return;
