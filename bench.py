@@ -737,12 +737,14 @@ def run_rank(args):
                              "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
                                            "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
                                            "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
-                                           "relator's last live chunk brings its sector's dead ones (PMC 1.30x these "
-                                           "bytes, profiles/r04/r04n_step128_summary.json)",
-                             "compute_note": "the tile conversion spends VALU on every chunk slot of a row, live or "
-                                             "not: early in a horizon (short relators) the kernel is VALU-issue-bound "
-                                             "(SQ_INSTS_VALU / (256 CUs x 2.4 GHz) = 0.111 ms of a 0.134 ms launch, "
-                                             "profiles/r04/r04o_step_sq_counters.json), later HBM-bound"},
+                                           "relator's last live chunk brings its sector's dead ones (PMC 1.13x these "
+                                           "bytes over this command's 200 launches, profiles/r04/"
+                                           "r04w_step128_summary.json; 1.30x early in a horizon)",
+                             "compute_note": "mid-horizon the launch runs at ~0.93 of the bare cost of its own "
+                                             "access pattern (live-chunk reads + changed-relator write-back, "
+                                             "profiles/r04/r04z_live_shape_ceiling.json); early in a horizon (short "
+                                             "relators) VALU issue is most of the launch "
+                                             "(profiles/r04/r04w_step_horizon.json)"},
                 "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
             }
             del st2, cnt2, lens2
@@ -917,7 +919,7 @@ def committed_step_traffic(B, L, launch_bytes, kernel):
     measured/algorithmic ratio applied to this launch's algorithmic bytes (the changed-relator
     rate, hence the bytes, vary slightly with the walk); or (None, None)"""
     want = kernel.replace(" ", "")
-    for tag in ("r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
+    for tag in ("r04w_step128", "r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
         prof = os.path.join(REPO, "profiles", "r04", f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
