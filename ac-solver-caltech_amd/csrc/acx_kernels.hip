@@ -172,6 +172,12 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_WB_CPOL
 #define ACX_WB_CPOL 16
 #endif
+// A/B knob: the rollout's int8 trajectory stores (full aligned FastTile tiles) through a buffer
+// store with this cache policy (-1: the global non-temporal store).  nt stays: K = 20 0.4626 ms
+// vs sc1 0.4862, plain 0.494 (profiles/r04/r04s_ab_obs8_cpol.json)
+#ifndef ACX_OBS8_CPOL
+#define ACX_OBS8_CPOL -1
+#endif
 // The rollout's int32 trajectory stores (full tiles) through a buffer store with this cache policy
 // (gfx950 cpol bits: sc0 1, nt 2, sc1 16; -1: the global non-temporal store of ACX_NT_OBS).  sc1
 // (the line is not kept in the XCD's L2): same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059
@@ -582,11 +588,24 @@ struct FastTile {
                 // read and one 16-byte store per lane and chunk, no per-dword guards (the general
                 // loop below costs ~150 VALU per wave-step at L = 36)
                 constexpr int ND = WAVE * CPR;
+#if ACX_OBS8_CPOL >= 0
+                const uint64_t gb = reinterpret_cast<uint64_t>(g);
+                const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
+                const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, ND * 4, 0x00020000);
+#endif
 #pragma unroll
                 for (int u = 0; u < (ND + 4 * WAVE - 1) / (4 * WAVE); ++u) {
                     const int d0 = 4 * (ln + u * WAVE);
                     if ((u + 1) * 4 * WAVE > ND && d0 >= ND) continue;  // the last, partial chunk row
                     const v4i_t x = *reinterpret_cast<const v4i_t*>(lds + d0);
+#if ACX_OBS8_CPOL >= 0
+                    if constexpr (NT) {
+                        __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)d0 * 4u, 0, ACX_OBS8_CPOL);
+                        continue;
+                    }
+#endif
                     if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(dst + d0));
                     else *reinterpret_cast<v4i_t*>(dst + d0) = x;
                 }
