@@ -172,6 +172,11 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_WB_CPOL
 #define ACX_WB_CPOL 16
 #endif
+// A/B knob: the same write-back policy for FastTile (L % 4 == 0, not CodeTile; e.g. L = 36): sc1
+// 0.0757 vs nt 0.0698 ms per 2^20-env step (profiles/r04/r04s_ab_wb36_cpol.json), so nt stays
+#ifndef ACX_WB_CPOL36
+#define ACX_WB_CPOL36 -1
+#endif
 // A/B knob: the rollout's int8 trajectory stores (full aligned FastTile tiles) through a buffer
 // store with this cache policy (-1: the global non-temporal store).  nt stays: K = 20 0.4626 ms
 // vs sc1 0.4862, plain 0.494 (profiles/r04/r04s_ab_obs8_cpol.json)
@@ -877,6 +882,15 @@ struct FastTile {
             }
             return;
         }
+#if ACX_WB_CPOL36 >= 0
+        // the whole 64-row tile as one buffer (scalar base, built before the loop; rows >= R are
+        // never written), lanes at their 16-B chunk offsets
+        const uint64_t gb = reinterpret_cast<uint64_t>(g);
+        const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
+        const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
+#endif
 #pragma unroll
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
@@ -895,7 +909,13 @@ struct FastTile {
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
                 if (!wr[u]) continue;
+#if ACX_WB_CPOL36 >= 0
+                const int4 v = widen4(p[u]);
+                const v4i_t x = {v.x, v.y, v.z, v.w};
+                __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (u0 + u) * WAVE) * 16u, 0, ACX_WB_CPOL36);
+#else
                 out16<NT, false>(dst + ln + (u0 + u) * WAVE, widen4(p[u]));
+#endif
             }
         }
     }
