@@ -68,7 +68,6 @@ class CurriculumRecord:
         buffer, as for LearnerEnv.place).  Returns [(env, state index)] for every restart."""
         d = np.asarray(done.cpu() if hasattr(done, "cpu") else done).astype(bool)
         t = np.asarray(truncated.cpu() if hasattr(truncated, "cpu") else truncated).astype(bool)
-        h = np.asarray(needs_host.cpu() if hasattr(needs_host, "cpu") else needs_host).astype(bool)
         fin = np.nonzero(d | t)[0]
         if fin.size == 0:
             return []
@@ -80,11 +79,18 @@ class CurriculumRecord:
         else:
             acts = {i: env.episode_actions(i) for i in solved}
         out = []
+        hv = np.asarray(needs_host.cpu() if hasattr(needs_host, "cpu") else needs_host)
+        if (hv == 3).any():
+            raise RuntimeError("LearnerEnv: the device could not rank the finished envs (needs_host 3: a curriculum "
+                               "workspace shared by concurrent launches)")
         for i in fin.tolist():
             if d[i]:
                 self.on_done(i, acts[i])
-            if h[i]:
+            if hv[i] == 1:  # round 1 complete: the reference's random draw (training.py:337-348)
                 k = self.draw()
+                env.place(i, k, obs_out=obs_out)
+            elif hv[i] == 2:  # round 1, an initial state the device did not load: placed as it is
+                k = int(dev_idx[i])
                 env.place(i, k, obs_out=obs_out)
             else:
                 k = int(dev_idx[i])

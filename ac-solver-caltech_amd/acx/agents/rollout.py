@@ -3,8 +3,8 @@
 The reference steps a gymnasium SyncVectorEnv on the host each step (`envs.step(action.cpu()
 .numpy())`, training.py:238-240), copies obs/reward/done back to the device (:241, :354-356)
 and runs a Python loop over the envs for episode bookkeeping and the start-state curriculum
-(:262-352).  LearnerEnv keeps all of it on the GPU, one acx_learner_step call (a step kernel
-and one curriculum pass) per step:
+(:262-352).  LearnerEnv keeps all of it on the GPU, one acx_learner_step call -- ONE kernel
+launch, the curriculum's ranking fused into the step -- per step:
 
   * the policy's int64 actions go straight in;
   * the next observation is written as float32 into whatever (B, 2L) buffer the caller names
@@ -14,7 +14,10 @@ and one curriculum pass) per step:
   * the round-1 curriculum (training.py:319-336, 349-352) runs on the device: finished envs
     take the next unprocessed initial state in env order.  Once every initial state has been
     used the reference draws random solved/unsolved states with Python `random` (:337-346);
-    those envs are flagged in `needs_host` and placed by `place()`.
+    those envs are flagged in `needs_host` and placed by `place()`.  needs_host 2: the next
+    initial state is outside the packed domain and was not loaded on the device (the env reset to
+    its own row, curr_index holds the state to place); 3: the device could not rank the env (a
+    workspace shared by concurrent launches) -- CurriculumRecord.process raises.
 """
 
 from __future__ import annotations
@@ -74,7 +77,7 @@ class LearnerEnv:
         obs_out / reward_out / done_out: float32 (B, 2L) / (B,) / (B,) device views to fill
         (next_obs, rewards[t], next_done).  Returns (done, truncated, episode_len, needs_host)
         uint8/int32 device tensors; no host synchronisation.  fused (default): one
-        acx_learner_step call (2 launches); else acx_step_learner + acx_curriculum_assign."""
+        acx_learner_step call (one launch); else acx_step_learner + acx_curriculum_assign (four)."""
         lib = _lib.load()
         B, L, dev = self.num_envs, self.L, self.device
         for name, t, shape in (("obs_out", obs_out, (B, 2 * L)), ("reward_out", reward_out, (B,)),

@@ -283,12 +283,13 @@ class VecACEnv:
         self.single_observation_space = Box(np.full(2 * L, -2, np.int8), np.full(2 * L, 2, np.int8))
 
     def reset(self, *, seed=None, options=None):
-        """Reset every env to its starting state (options["starting_states"] replaces them)."""
+        """Reset every env to its starting state (options["starting_states"] replaces them).
+        Like the reference's ACEnv.reset (ac_env.py:113-129) the rows are taken as they are, with
+        no validation: a row outside the packed domain (a zero inside a relator, a letter other
+        than +-1/+-2) is held as its exact values and every step reports it with err 3
+        (ACX_ERR_DOMAIN), as the step kernels do for such starting rows."""
         if options and "starting_states" in options:
             rows = np.asarray(options["starting_states"]).reshape(tuple(self.reset_state.shape))
-            if _invalid_rows(rows).any():
-                raise ValueError("starting_states must be valid presentations")
-            _check_domain(rows)
             self.reset_state.copy_(torch.as_tensor(rows.astype(np.int32)).to(self.device))
         self.state.copy_(self.reset_state)
         # (reset_state may also have been rewritten on the device, e.g. by the learner's curriculum)
@@ -394,7 +395,18 @@ class VecACEnv:
                 done_traj=None, trunc_traj=None):
         """T = actions.shape[0] steps in one launch; trajectories optional (T, B, ...).  obs_traj
         is int32, or int8 -- the observation_space dtype (ac_env.py:64-70) and what
-        SyncVectorEnv returns -- at a quarter of the bytes."""
+        SyncVectorEnv returns -- at a quarter of the bytes.
+
+        Same-step autoreset only: the fused rollout resets an env on the step its episode ends.
+        With autoreset_mode="next_step" (acx_step_next's pending flags) or record_actions (the
+        per-episode move history acx_step_record keeps) a rollout would leave that per-env state
+        stale, so it raises instead."""
+        if self.autoreset_mode == "next_step":
+            raise ValueError("VecACEnv.rollout implements same-step autoreset only; with autoreset_mode='next_step' "
+                             "step the env with step()")
+        if self.record_actions:
+            raise ValueError("VecACEnv.rollout does not record episode moves; with record_actions=True step the env "
+                             "with step()")
         ops.rollout(self.state, actions, self.reset_state, self.step_count, horizon=self.horizon_length,
                     cyclical=self.cyclical, obs_traj=obs_traj, reward_traj=reward_traj, done_traj=done_traj,
                     trunc_traj=trunc_traj, err=self.err, err_count=self.err_count)

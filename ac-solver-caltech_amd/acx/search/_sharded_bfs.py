@@ -214,8 +214,6 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
                 exp_out[5 + W] = len(failed)
                 rows = comm.all_gather_rows(exp_out)  # (W, 6 + W)
                 agree(rows[:, 5 + W].sum(), "a C call")
-                if rows[:, 4].any():
-                    raise _lib.ACXError("sharded bfs: hash table overflow")
                 succ_seq, err_seq = int(rows[:, 0].min()), int(rows[:, 1].min())
                 chunk_min = int(rows[:, 2].min())
                 send_counts = rows[comm.rank, 5 : 5 + W]
@@ -240,9 +238,13 @@ def sharded_bfs(presentation, max_nodes_to_explore=10000, verbose=False, cyclica
                     raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
                 succ_seq, err_seq, chunk_min = int(com_out[5]), int(com_out[6]), int(com_out[7])
             else:
-                st_rows = comm.sum_rows([com_out[4], len(failed)])
-                agree(st_rows[1], "a C call")
+                # overflow bits (acx_sbfs_commit out[4]): bit 0 the insert's hash probe, bit 1 the commit's
+                # node store / table rewrite -- decoded as the one-rank branch does
+                st_rows = comm.sum_rows([int(com_out[4] & 1), int((com_out[4] >> 1) != 0), len(failed)])
+                agree(st_rows[2], "a C call")
                 if st_rows[0]:
+                    raise _lib.ACXError("sharded bfs: hash table overflow")
+                if st_rows[1]:
                     raise _lib.ACXError("sharded bfs: a rank's node store or hash table is full")
             total_new, cut_p, nodes_at_cut = int(com_out[0]), int(com_out[1]), int(com_out[2])
             cut = cut_p if cut_p >= 0 else None

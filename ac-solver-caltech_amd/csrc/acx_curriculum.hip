@@ -133,53 +133,6 @@ __global__ __launch_bounds__(TPB) void assign_kernel(Args a) {
     }
 }
 
-// The same assignment in one launch after acx_learner_step's step kernel, which wrote the
-// finished-env count of every 64-env wave as a byte (fin4: the 4 waves of a 256-env block
-// are one dword) and copied *next_index into *base.  Block b sums the dwords of blocks
-// < b itself (b <= ceil(B/256) loads spread over the block, L2-resident) instead of a
-// count + scan kernel pair; the last block advances *next_index.
-__global__ __launch_bounds__(TPB) void assign_fused_kernel(Args a, const uint32_t* __restrict__ fin4) {
-    __shared__ uint32_t sh[TPB / WAVE];
-    const int b = blockIdx.x;
-    uint32_t s = 0;
-    for (int j = threadIdx.x; j < b; j += TPB) {
-        const uint32_t v = fin4[j];
-        s += (v & 0xffu) + ((v >> 8) & 0xffu) + ((v >> 16) & 0xffu) + (v >> 24);
-    }
-    uint32_t before;
-    block_excl_scan(s, sh, before);  // total = finished envs in blocks < b
-    __syncthreads();
-    const int64_t i = (int64_t)b * TPB + threadIdx.x;
-    const bool f = finished(a, i);
-    uint32_t tot;
-    const uint32_t r = block_excl_scan(f ? 1u : 0u, sh, tot);
-    const int32_t base = *a.base;
-    if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {
-        const int64_t n = (int64_t)base + before + tot;
-        *a.next_index = (int32_t)(n < a.n_states ? n : a.n_states);
-    }
-    if (i >= a.B) return;
-    if (!f) {
-        a.needs_host[i] = 0;
-        return;
-    }
-    const int64_t idx = (int64_t)base + before + r;
-    if (idx >= a.n_states) {
-        a.needs_host[i] = 1;
-        return;
-    }
-    a.needs_host[i] = 0;
-    a.curr_index[i] = (int32_t)idx;
-    const int twoL = 2 * a.L;
-    const int32_t* src = a.states + idx * twoL;
-    for (int k = 0; k < twoL; ++k) {
-        const int32_t v = src[k];
-        a.state[i * twoL + k] = v;
-        if (a.reset_state) a.reset_state[i * twoL + k] = v;
-        if (a.obs_f32) a.obs_f32[i * twoL + k] = (float)v;
-    }
-}
-
 }  // namespace cur
 }  // namespace acx
 
@@ -187,7 +140,11 @@ using namespace acx::cur;
 
 extern "C" {
 
-int64_t acx_curriculum_workspace(int64_t B) { return (B + TPB - 1) / TPB + 2; }
+int64_t acx_internal_curriculum_fused_offset(int64_t B);
+int64_t acx_curriculum_workspace(int64_t B) {
+    if (B < 0) return 0;
+    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + (B + WAVE - 1) / WAVE);
+}
 
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
                           int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
@@ -208,19 +165,14 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
     return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 
-// The curriculum half of acx_learner_step (acx_kernels.hip), after its step kernel.
-// workspace (acx_curriculum_workspace(B) words): [0] next_index before the step, [2, 2 + nb)
-// the per-wave finished counts as bytes.  Not part of the public header.
-int acx_internal_curriculum_fused(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
-                                  int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
-                                  int32_t* state, int32_t* reset_state, float* obs_f32, int32_t* workspace, int64_t B,
-                                  int32_t L, void* stream) {
-    const int nb = (int)((B + TPB - 1) / TPB);
-    Args a{done, truncated, curriculum_states, n_states, next_index, curr_index, needs_host, state, reset_state,
-           obs_f32, nullptr, workspace, B, L};
-    assign_fused_kernel<<<dim3(nb), dim3(TPB), 0, (hipStream_t)stream>>>(
-        a, reinterpret_cast<const uint32_t*>(workspace + 2));
-    return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
+// acx_learner_step (acx_kernels.hip) ranks the finished envs inside its step kernel with a
+// look-back over per-64-env-tile status words; its part of the workspace starts after this
+// file's (next_index copy + per-block counts), so either call may use one workspace:
+// [off, off + 2) the launch sequence number, [off + 2, off + 6) reserved, then one uint64 per
+// 64-env tile (acx_kernels.hip cur_lookback).
+int64_t acx_internal_curriculum_fused_offset(int64_t B) {
+    const int64_t own = (B + TPB - 1) / TPB + 2;
+    return (own + 1) & ~(int64_t)1;  // 8-byte aligned
 }
 
 }  // extern "C"

@@ -53,6 +53,14 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lane r's pointer p, read by every lane (all 64 lanes must execute it: ds_bpermute)
+__device__ __forceinline__ const int32_t* lane_ptr(const int32_t* p, int r) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, r, WAVE);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), r, WAVE);
+    return reinterpret_cast<const int32_t*>(((uint64_t)hi << 32) | lo);
+}
+
 // int32 letter -> int8; values outside {-2..2} become 0x7F and set `bad`
 __device__ __forceinline__ uint32_t to_i8(int32_t v, bool& bad) {
     const bool ok = (uint32_t)(v + 2) <= 4u;
@@ -172,17 +180,11 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
 #ifndef ACX_WB_CPOL
 #define ACX_WB_CPOL 16
 #endif
-// A/B knob: the same write-back policy for FastTile (L % 4 == 0, not CodeTile; e.g. L = 36): sc1
-// 0.0757 vs nt 0.0698 ms per 2^20-env step (profiles/r04/r04s_ab_wb36_cpol.json), so nt stays
-#ifndef ACX_WB_CPOL36
-#define ACX_WB_CPOL36 -1
-#endif
-// A/B knob: the rollout's int8 trajectory stores (full aligned FastTile tiles) through a buffer
-// store with this cache policy (-1: the global non-temporal store).  nt stays: K = 20 0.4626 ms
-// vs sc1 0.4862, plain 0.494 (profiles/r04/r04s_ab_obs8_cpol.json)
-#ifndef ACX_OBS8_CPOL
-#define ACX_OBS8_CPOL -1
-#endif
+// (FastTile, e.g. L = 36, keeps the global non-temporal write-back: sc1 measured 0.0757 vs nt
+// 0.0698 ms per 2^20-env step, profiles/r04/r04s_ab_wb36_cpol.json; that A/B knob was removed in
+// round 5 -- DESIGN.md "Buffer descriptors")
+// (the rollout's int8 trajectory keeps global non-temporal stores: K = 20 0.4626 ms vs sc1 buffer
+// stores 0.4862, plain 0.494, profiles/r04/r04s_ab_obs8_cpol.json; that knob was removed in round 5)
 // The rollout's int32 trajectory stores (full tiles) through a buffer store with this cache policy
 // (gfx950 cpol bits: sc0 1, nt 2, sc1 16; -1: the global non-temporal store of ACX_NT_OBS).  sc1
 // (the line is not kept in the XCD's L2): same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059
@@ -352,7 +354,7 @@ struct FastTile {
     // loop is unrolled already).  LIVE (the lengths-carrying step; lim[] set for every row): only
     // the chunks inside each relator's letters are read, the rest of the image is zero (the rows
     // are canonical: letters, then zero padding)
-    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false, int BATCH = 0>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));  // keep the address math here (no hoisting into the caller)
@@ -369,12 +371,15 @@ struct FastTile {
             const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
             const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
+            // BATCH (the small-batch step instance): loads in flight per batch, up to the whole
+            // tile row (CPR: one round trip); LOAD_BATCH otherwise (the 8-wave/SIMD VGPR budget)
+            constexpr int LB = BATCH > 0 ? BATCH : LOAD_BATCH;
 #pragma unroll
-            for (int u0 = 0; u0 < CPR; u0 += LOAD_BATCH) {
-                int4 v[LOAD_BATCH];
-                bool lv[LOAD_BATCH];
+            for (int u0 = 0; u0 < CPR; u0 += LB) {
+                int4 v[LB];
+                bool lv[LB];
 #pragma unroll
-                for (int u = 0; u < LOAD_BATCH; ++u) {
+                for (int u = 0; u < LB; ++u) {
                     if (u0 + u >= CPR) continue;
                     const int c = ln + (u0 + u) * WAVE;
                     lv[u] = true;
@@ -387,7 +392,7 @@ struct FastTile {
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < LOAD_BATCH; ++u) {
+                for (int u = 0; u < LB; ++u) {
                     if (u0 + u >= CPR) continue;
                     bool bad = false;
                     uint32_t p = 0;
@@ -474,7 +479,16 @@ struct FastTile {
     // the rows of the lanes in the wave-uniform mask `rows` only (a few resetting envs),
     // cooperatively: lane l loads 16-byte chunk l % CPR of the (l / CPR)-th selected row, so a
     // wave-instruction fetches 64 / CPR whole rows (3 at L = 36) with one round trip per group
-    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
+    }
+    // the same with a per-lane source row: row r comes from lane r's `src` (the learner's resets)
+    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
+    }
+    // rp(r): row r's source (called by every lane of the wave: it may read across lanes)
+    template <class RowPtr>
+    __device__ __forceinline__ void load_rows_from(RowPtr rp, uint64_t rows, int, int lane) {
         constexpr int RPI = WAVE / CPR;
         static_assert(RPI >= 1, "a row must fit one wave-instruction");
         const int s = lane / CPR, c = lane - s * CPR;
@@ -484,11 +498,13 @@ struct FastTile {
         bool any_bad = false;
         for (int k0 = 0; k0 < n; k0 += RPI) {
             const int k = k0 + s;
-            if (s < RPI && k < n) {
-                uint64_t m = rows;
-                for (int i = 0; i < k; ++i) m &= m - 1;
-                const int r = __builtin_ctzll(m);
-                const int4 v = reinterpret_cast<const int4*>(g + (int64_t)r * twoL)[c];
+            const bool on = s < RPI && k < n;
+            uint64_t m = rows;
+            for (int i = 0; i < (on ? k : 0); ++i) m &= m - 1;
+            const int r = __builtin_ctzll(m);
+            const int32_t* row_src = rp(r);
+            if (on) {
+                const int4 v = reinterpret_cast<const int4*>(row_src)[c];
                 bool bad = false;
                 lds[r * S + c] = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
                                  (to_i8(v.w, bad) << 24);
@@ -593,24 +609,11 @@ struct FastTile {
                 // read and one 16-byte store per lane and chunk, no per-dword guards (the general
                 // loop below costs ~150 VALU per wave-step at L = 36)
                 constexpr int ND = WAVE * CPR;
-#if ACX_OBS8_CPOL >= 0
-                const uint64_t gb = reinterpret_cast<uint64_t>(g);
-                const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
-                const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, ND * 4, 0x00020000);
-#endif
 #pragma unroll
                 for (int u = 0; u < (ND + 4 * WAVE - 1) / (4 * WAVE); ++u) {
                     const int d0 = 4 * (ln + u * WAVE);
                     if ((u + 1) * 4 * WAVE > ND && d0 >= ND) continue;  // the last, partial chunk row
                     const v4i_t x = *reinterpret_cast<const v4i_t*>(lds + d0);
-#if ACX_OBS8_CPOL >= 0
-                    if constexpr (NT) {
-                        __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)d0 * 4u, 0, ACX_OBS8_CPOL);
-                        continue;
-                    }
-#endif
                     if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(dst + d0));
                     else *reinterpret_cast<v4i_t*>(dst + d0) = x;
                 }
@@ -882,15 +885,6 @@ struct FastTile {
             }
             return;
         }
-#if ACX_WB_CPOL36 >= 0
-        // the whole 64-row tile as one buffer (scalar base, built before the loop; rows >= R are
-        // never written), lanes at their 16-B chunk offsets
-        const uint64_t gb = reinterpret_cast<uint64_t>(g);
-        const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
-        const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
-#endif
 #pragma unroll
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
@@ -909,13 +903,7 @@ struct FastTile {
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
                 if (!wr[u]) continue;
-#if ACX_WB_CPOL36 >= 0
-                const int4 v = widen4(p[u]);
-                const v4i_t x = {v.x, v.y, v.z, v.w};
-                __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (u0 + u) * WAVE) * 16u, 0, ACX_WB_CPOL36);
-#else
                 out16<NT, false>(dst + ln + (u0 + u) * WAVE, widen4(p[u]));
-#endif
             }
         }
     }
@@ -1021,7 +1009,7 @@ struct CodeTile {
 
     // PIPE (the step kernel; the rollout keeps the plain loop, whose register budget the
     // in-flight batch pair would exceed): full tiles software-pipelined, see below
-    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false, int BATCH = 0>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
@@ -1236,14 +1224,22 @@ struct CodeTile {
 
     // the rows of the lanes in `rows` only (see FastTile::load_rows); a row is >= one
     // wave-instruction here (CPR >= 16 chunks), so row by row, lanes over its chunks
-    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
+    }
+    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
+    }
+    template <class RowPtr>
+    __device__ __forceinline__ void load_rows_from(RowPtr rp, uint64_t rows, int, int lane) {
         if ((rows >> lane) & 1ull) flags[lane] = 0;
         wave_sync();
         bool any_bad = false;
         for (uint64_t m = rows; m; m &= m - 1) {
             const int r = __builtin_ctzll(m);
+            const int32_t* row_src = rp(r);
             for (int c = lane; c < CPR; c += WAVE) {
-                const int4 v = reinterpret_cast<const int4*>(g + (int64_t)r * twoL)[c];
+                const int4 v = reinterpret_cast<const int4*>(row_src)[c];
                 bool bad = false;
                 const uint32_t d = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
                                    (to_i8(v.w, bad) << 24);
@@ -1680,14 +1676,22 @@ struct GenericTile {
     __device__ __forceinline__ int32_t letter(int r, int k) const { return row(r)[k]; }
     // the rows of the lanes in `rows` only, row by row (the generic-L instantiations serve
     // parity, not speed)
-    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int, int lane) {
+    __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
+    }
+    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
+        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
+    }
+    template <class RowPtr>
+    __device__ __forceinline__ void load_rows_from(RowPtr rp, uint64_t rows, int, int lane) {
         if ((rows >> lane) & 1ull) flags[lane] = 0;
         wave_sync();
         for (uint64_t m = rows; m; m &= m - 1) {
             const int r = __builtin_ctzll(m);
+            const int32_t* row_src = rp(r);
             bool bad = false;
             for (int k = lane; k < twoL; k += WAVE)
-                row(r)[k] = (int8_t)to_i8(g[(int64_t)r * twoL + k], bad);
+                row(r)[k] = (int8_t)to_i8(row_src[k], bad);
             if (__any(bad) && lane == 0) flags[r] = 1;
         }
         wave_sync();
@@ -1712,7 +1716,7 @@ struct GenericTile {
     };
 
     // PIPE, LIVE: see CodeTile::load (the runtime-L path reads and writes whole rows)
-    template <bool PIPE = false, bool LIVE = false, bool NTL = false>
+    template <bool PIPE = false, bool LIVE = false, bool NTL = false, int BATCH = 0>
     __device__ __forceinline__ void load(const int32_t* __restrict__ g, int R, int lane) {
         flags[lane] = 0;
         wave_sync();
@@ -1992,11 +1996,15 @@ struct StepArgs {
     int32_t* episode_len;
     int64_t B;
     int L, horizon, cyclical, hist_cap;
-    // acx_learner_step: finished-env count per 64-env wave (bytes) for the fused curriculum
-    // pass, and the curriculum's next_index copied to next_base before that pass advances it
-    uint8_t* fin_wave;
-    const int32_t* next_index;
-    int32_t* next_base;
+    // acx_learner_step: the round-1 curriculum fused into the step (training.py:319-352).
+    // cur_ws NULL: none.  cur_ws (uint64 words): [0] launch sequence number, [1, 2] reserved,
+    // [3 + t] tile t's look-back status (cur_lookback)
+    uint64_t* cur_ws;
+    const int32_t* cur_states;  // (n_states, 2L) initial states
+    int64_t n_states;
+    int32_t* cur_next;          // [1] max(states_processed) + 1
+    int32_t* curr_index;        // (B)
+    uint8_t* needs_host;        // (B)
     // state_out == state_in (set by the launcher): the state store writes changed relators only
     int in_place;
     // next-step autoreset (acx_step_next; NULL: same-step): per env, its episode ended on the
@@ -2007,15 +2015,148 @@ struct StepArgs {
     int live;
 };
 
+// ---------------------------------------------------------------------------------
+// The curriculum's ranking inside the step kernel (acx_learner_step, one launch).  Finished envs
+// (done | truncated) take the initial states next_index, next_index + 1, ... in env order
+// (training.py:329-336), so an env needs the number of finished envs before it -- a prefix count
+// over the whole batch.  Single-pass chained scan with decoupled look-back, one 64-env tile per
+// wave, tiles in launch order (blockIdx):
+//   * a tile's status is one 64-bit word (flag 2 bits | launch sequence number 30 | value 32),
+//     written and polled with agent-scope atomics (the word is the whole hand-off: MI355X_MICROARCH
+//     "8-B agent atomics both sides"); flag 1 = the tile's own count, flag 2 = inclusive prefix;
+//     tile 0's prefix starts at *next_index, so a tile's exclusive prefix IS the first index it
+//     hands out.  Each wave publishes its count before it looks back;
+//   * words of an earlier launch carry another sequence number and read as "not ready".  Every
+//     wave reads the sequence number (cur_ws[0]) before it publishes, so once the LAST tile's
+//     look-back is through -- every tile has published by then -- no wave of this launch reads it
+//     again, and the last tile advances it (and next_index) for the next launch.  No ticket or
+//     arrival counter: one word per tile, no same-address atomics (MI355X_MICROARCH "dequeue":
+//     ~88 per us on one word);
+//   * HIP promises no dispatch order: a wave that polls too long (2^20 polls, ~seconds -- a
+//     predecessor never scheduled, or a workspace shared by concurrent launches) gives up, so the
+//     launch always ends; that tile and every later one publish CUR_FAIL and flag their finished
+//     envs needs_host = 3 (CurriculumRecord.process raises).
+// ---------------------------------------------------------------------------------
+constexpr uint64_t CUR_AGG = 1ull << 62, CUR_INC = 2ull << 62;
+constexpr uint32_t CUR_FAIL = 0xffffffffu;
+constexpr uint32_t CUR_SEQ_MASK = (1u << 30) - 1u;
+
+// one lane copies a (2L) int32 row (the rare per-env row writes: a reset row the curriculum set)
+__device__ __forceinline__ void copy_row(int32_t* dst, const int32_t* src, int twoL) {
+    if ((twoL & 3) == 0) {
+        for (int k = 0; k < twoL / 4; ++k) reinterpret_cast<int4*>(dst)[k] = reinterpret_cast<const int4*>(src)[k];
+    } else {
+        for (int k = 0; k < twoL; ++k) dst[k] = src[k];
+    }
+}
+
+__device__ __forceinline__ uint64_t cur_word(uint64_t flag, uint32_t seq, uint32_t v) {
+    return flag | ((uint64_t)(seq & CUR_SEQ_MASK) << 32) | v;
+}
+__device__ __forceinline__ uint64_t cur_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cur_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the tile's first index (next_index + finished envs of all earlier tiles), or CUR_FAIL;
+// publishes this tile's inclusive prefix.  Wave-uniform control flow; fm = ballot of finished.
+// Each poll reads CUR_LANE predecessors per lane (64 * CUR_LANE tiles, one round trip): the
+// look-back walks back that far per round trip while the inclusive prefixes propagate forward,
+// so a synchronised start (every resident wave publishing at once) settles in ~t / (128 CUR_LANE)
+// round trips instead of ~t / 128 (16,384 tiles at 2^20 envs)
+constexpr int CUR_LANE = 8;
+__device__ __forceinline__ uint32_t cur_lookback(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint64_t fm) {
+    uint64_t* st = a.cur_ws + 3;
+    const int64_t t = w.r0 / WAVE;
+    const uint32_t agg = (uint32_t)__popcll(fm);
+    uint32_t excl;
+    if (t == 0) {
+        excl = (uint32_t)*a.cur_next;  // the scan starts at next_index (read by tile 0 alone)
+    } else {
+        if (w.lane == 0) cur_store(st + t, cur_word(CUR_AGG, seq, agg));
+        excl = 0;
+        int64_t j = t - 1;  // the nearest predecessor not yet summed (wave-uniform)
+        uint32_t polls = 0;
+        bool fail = false;
+        const uint32_t sq = seq & CUR_SEQ_MASK;
+        while (true) {
+            // lane l holds predecessors j - (l * CUR_LANE + i), i = 0 (nearest) .. CUR_LANE - 1
+            uint64_t v[CUR_LANE];
+#pragma unroll
+            for (int i = 0; i < CUR_LANE; ++i) {
+                const int64_t q = j - ((int64_t)w.lane * CUR_LANE + i);
+                v[i] = q >= 0 ? cur_load(st + q) : (CUR_AGG | ((uint64_t)sq << 32));  // past tile 0: ready, 0
+            }
+            int first = CUR_LANE;  // this lane's nearest inclusive prefix
+            bool all_ready = true, ready_before = true;
+#pragma unroll
+            for (int i = CUR_LANE - 1; i >= 0; --i) {
+                const bool mine = ((uint32_t)(v[i] >> 32) & CUR_SEQ_MASK) == sq;
+                const uint32_t fl = (uint32_t)(v[i] >> 62);
+                const bool rdy = mine && fl != 0;
+                all_ready = all_ready && rdy;
+                if (mine && fl == 2) first = i;
+            }
+#pragma unroll
+            for (int i = 0; i < CUR_LANE; ++i)
+                if (i < first) ready_before = ready_before && (((uint32_t)(v[i] >> 32) & CUR_SEQ_MASK) == sq && (v[i] >> 62) != 0);
+            const uint64_t incm = __ballot(first < CUR_LANE);
+            const int ls = incm ? __builtin_ctzll(incm) : WAVE;  // the lane of the nearest inclusive prefix
+            const uint64_t below = ls >= WAVE ? ~0ull : ((1ull << ls) - 1ull);
+            const bool wait_lane = (w.lane < ls && !all_ready) || (w.lane == ls && !ready_before);
+            if (__ballot(wait_lane)) {
+                if (++polls > (1u << 20)) {
+                    fail = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            (void)below;
+            uint32_t x = 0;
+            bool bad = false;
+            if (w.lane < ls) {
+#pragma unroll
+                for (int i = 0; i < CUR_LANE; ++i) x += (uint32_t)v[i];
+            } else if (w.lane == ls) {
+#pragma unroll
+                for (int i = 0; i < CUR_LANE; ++i)
+                    if (i <= first) x += (uint32_t)v[i];
+#pragma unroll
+                for (int i = 0; i < CUR_LANE; ++i)
+                    if (i == first) bad = (uint32_t)v[i] == CUR_FAIL;
+            }
+            if (__ballot(bad)) {  // an earlier tile gave up
+                fail = true;
+                break;
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, WAVE);
+            excl += x;
+            if (incm || j < (int64_t)WAVE * CUR_LANE) break;
+            j -= (int64_t)WAVE * CUR_LANE;
+        }
+        if (fail) excl = CUR_FAIL;
+    }
+    if (w.lane == 0) cur_store(st + t, cur_word(CUR_INC, seq, excl == CUR_FAIL ? CUR_FAIL : excl + agg));
+    return excl;
+}
+
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
 // LIVE: the lengths-carrying step (its own kernel, so the plain step's registers stay its own)
-template <int NW, int LC, int VEC, bool LEARN, bool LIVE>
+template <int NW, int LC, int VEC, bool LEARN, bool LIVE, int BATCH = 0>
 __device__ __forceinline__ void step_body(const StepArgs& a) {
     using Tile = TileFor<NW, LC, VEC>;
     constexpr bool NT_SC = ACX_NT_STEP_SCALARS != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
+    // acx_learner_step: the curriculum fused in (cur_lookback)
+    const bool cur = LEARN && a.cur_ws != nullptr;  // kernel argument: uniform
     if (!wave_ctx(a.B, w)) return;
+    // the launch's sequence number, read before this tile publishes (cur_lookback)
+    const uint32_t cseq = cur ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws)) : 0u;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2044,7 +2185,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         wave_sync();
         tile.template load<ACX_PIPE_LOAD != 0, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     } else {
-        tile.template load<ACX_PIPE_LOAD != 0, false, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
+        tile.template load<ACX_PIPE_LOAD != 0, false, Tile::NT_STEP_LOADS, BATCH>(a.state_in + w.r0 * twoL, w.R, w.lane);
     }
 
     bool fin = false;    // done | truncated (the curriculum's "finished")
@@ -2105,6 +2246,37 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
     }
+    // the curriculum (acx_learner_step, training.py:319-336): a finished env takes initial state
+    // next_index + (finished envs before it); past the table's end (round 1 complete) the host
+    // draws (needs_host = 1)
+    const int32_t* cur_row = nullptr;  // the start row this env takes, or NULL
+    int64_t cur_idx = -1;
+    if (cur) {
+        const uint64_t fm = __ballot(fin);
+        const uint32_t first = cur_lookback(a, w, cseq, fm);
+        if (w.r0 + w.R == a.B && w.lane == 0) {
+            // the last tile: every tile has published, so no wave reads next_index or the sequence
+            // number again in this launch -- advance both for the next one
+            if (first != CUR_FAIL) {
+                const int64_t n = (int64_t)first + __popcll(fm);
+                *a.cur_next = (int32_t)(n < a.n_states ? n : a.n_states);
+            }
+            cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
+        }
+        if (w.active) {
+            uint8_t nh = 0;
+            if (fin) {
+                if (first == CUR_FAIL) {
+                    nh = 3;
+                } else {
+                    cur_idx = (int64_t)first + __popcll(fm & ((1ull << w.lane) - 1ull));
+                    if (cur_idx < a.n_states) cur_row = a.cur_states + cur_idx * twoL;
+                    else nh = 1;
+                }
+            }
+            a.needs_host[env] = nh;
+        }
+    }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
     tile.flag_rows(w.lane, (w.active && e == ACX_ERR_DOMAIN) ? FB_IN : 0u);
@@ -2115,7 +2287,29 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // env's row becomes that row's exact values (copied from reset_state, FB_RESET), its
         // step count 0 and its err ACX_ERR_DOMAIN; from then on it is an out-of-domain row.
         bool rbad = false;
-        if (__popcll(rb) > RESET_TILE_MIN) {
+        if (cur) {
+            // learner: each resetting env loads its own next start row, the curriculum's or its
+            // starting row (per-lane sources, so never the whole-tile reload)
+            tile.load_rows_src(cur_row ? cur_row : a.reset_state + env * twoL, rb, w.R, w.lane);
+            if (reset) rbad = tile.pack(w.lane, p);
+            // a curriculum row outside the packed domain is not taken here: the env resets to its
+            // own starting row and the host places that initial state as it is (needs_host = 2)
+            const uint64_t badc = __ballot(reset && rbad && cur_row != nullptr);
+            if (badc) {
+                if ((badc >> w.lane) & 1ull) {
+                    cur_row = nullptr;
+                    a.needs_host[env] = 2;
+                    a.curr_index[env] = (int32_t)cur_idx;
+                }
+                tile.load_rows(a.reset_state + w.r0 * twoL, badc, w.R, w.lane);
+                if ((badc >> w.lane) & 1ull) rbad = tile.pack(w.lane, p);
+            }
+            if (reset) {
+                if (!rbad) tile.unpack(w.lane, p);
+                dm = 3u;
+            }
+            tile.flag_rows(w.lane, rbad ? FB_RESET : 0u);
+        } else if (__popcll(rb) > RESET_TILE_MIN) {
             // many lanes (a synchronised truncation): one coalesced load of the tile's starting
             // states (per-lane reads of every row cost ~1 ms on a whole-batch truncation step);
             // the other lanes re-stage their state, rows left as loaded copy state_in
@@ -2139,6 +2333,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
         if (reset) cnt = 0;
     }
+    if (cur && reset && cur_row) {
+        // the env now starts (and later resets) from that initial state (training.py:349-352)
+        a.curr_index[env] = (int32_t)cur_idx;
+        copy_row(const_cast<int32_t*>(a.reset_state) + env * twoL, cur_row, twoL);  // acx_learner_step: writable
+    }
     if (w.active) {
         if (a.step_count) st_scalar<NT_SC, int32_t>(a.step_count + env, cnt);
         if (a.lengths_out) {
@@ -2149,13 +2348,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         if (a.err) st_scalar<NT_SC, uint8_t>(a.err + env, (uint8_t)e);
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
-    }
-    if constexpr (LEARN) {
-        if (a.fin_wave) {
-            const uint64_t m = __ballot(fin);
-            if (w.lane == 0) a.fin_wave[w.r0 >> 6] = (uint8_t)__popcll(m);
-            if (w.r0 == 0 && w.lane == 0) *a.next_base = *a.next_index;
-        }
     }
     if (a.in_place) {
         // state_out == state_in: write only the relators that changed (a gated move, a
@@ -2186,6 +2378,29 @@ template <int NW, int LC, int VEC, bool LEARN>
 __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
     step_body<NW, LC, VEC, LEARN, false>(a);
 }
+// Small batches (BASELINE configs[1]: 65,536 envs = 1,024 waves, one per SIMD): no other wave
+// hides a wave's load -> move -> store chain, so the whole tile's loads are issued at once (one
+// round trip instead of CPR / LOAD_BATCH of them) with the VGPR budget two waves per SIMD leave.
+// FastTile instantiations (compile-time L % 4 == 0, L < 64: the L = 36 configs); launch_step
+// takes it for B <= SMALL_STEP_MAX_B
+// A/B knobs: ACX_SMALL_STEP=0 keeps every batch on step_kernel; ACX_SMALL_BATCH loads in flight
+// per batch (0: the whole row, LC / 2)
+#ifndef ACX_SMALL_STEP
+#define ACX_SMALL_STEP 1
+#endif
+#ifndef ACX_SMALL_BATCH
+#define ACX_SMALL_BATCH 0
+#endif
+constexpr int64_t SMALL_STEP_MAX_B = ACX_SMALL_STEP ? (int64_t)2 * 4 * 256 * WAVE : -1;  // <= 2 waves per SIMD on 256 CUs
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK, 2) void step_small_kernel(StepArgs a) {
+    step_body<NW, LC, VEC, false, false, (ACX_SMALL_BATCH > 0 ? ACX_SMALL_BATCH : LC / 2)>(a);
+}
+template <int NW, int LC, int VEC>
+constexpr bool small_step_ok() {
+    return std::is_same<TileFor<NW, LC, VEC>, FastTile<NW, LC>>::value;
+}
+
 // acx_step_lengths (in place, lengths in and out).  At L = 128 the tile's LDS allows 4 waves per
 // SIMD; the live-chunk predicates took the register count just past 128 VGPRs (3 waves), so
 // the allocator is held to 4
@@ -3021,10 +3236,17 @@ static inline unsigned grid_for(int64_t rows) {
 template <int NW, int LC, int VEC, bool LEARN>
 int launch_step(StepArgs a, hipStream_t s) {
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L) + ACX_STEP_LDS_PAD;
-    if (!LEARN && a.live)
+    if (!LEARN && a.live) {
         step_lengths_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
-    else
-        step_kernel<NW, LC, VEC, LEARN><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+        return finish_launch();
+    }
+    if constexpr (!LEARN && small_step_ok<NW, LC, VEC>()) {
+        if (a.B <= SMALL_STEP_MAX_B) {
+            step_small_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+            return finish_launch();
+        }
+    }
+    step_kernel<NW, LC, VEC, LEARN><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }
 template <int NW, int LC, int VEC, int OBS>
@@ -3270,11 +3492,8 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
     return dispatch(L, f);
 }
 
-// acx_curriculum.hip (not in the public header)
-int acx_internal_curriculum_fused(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
-                                  int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
-                                  int32_t* state, int32_t* reset_state, float* obs_f32, int32_t* workspace, int64_t B,
-                                  int32_t L, void* stream);
+// acx_curriculum.hip: where acx_learner_step's part of the shared workspace starts (int32 words)
+int64_t acx_internal_curriculum_fused_offset(int64_t B);
 
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
@@ -3283,22 +3502,23 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
                      int32_t* curr_index, uint8_t* needs_host, int32_t* workspace, int64_t B, int32_t L,
                      int32_t horizon, int32_t cyclical, void* stream) {
     if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || n_states < 0 || n_states > INT32_MAX) return ACX_E_ARG;
+    if (B >= (1ll << 31)) return ACX_E_ARG;  // the look-back's 32-bit prefixes (next_index + finished envs)
     if (B == 0) return ACX_OK;
     if (!state || !step_count || (!action == !action_i64) || (action_hist && hist_cap == 0)) return ACX_E_ARG;
     if (!done || !truncated || !reset_state || !curriculum_states || !next_index || !curr_index || !needs_host ||
         !workspace)
         return ACX_E_ARG;
     if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
-    // workspace = acx_curriculum_workspace(B) words: [0] next_index before the step, [2..] one
-    // finished-count byte per 64-env wave (4 per 256-env block dword)
+    // one launch: the step kernel ranks the finished envs itself (cur_lookback) in its part of the
+    // workspace (acx_curriculum_workspace(B) int32 words, zeroed before the first call, 8-byte aligned)
+    int32_t* ws = workspace + acx_internal_curriculum_fused_offset(B);
+    if ((reinterpret_cast<uintptr_t>(ws) & 7u) != 0) return ACX_E_ARG;
     StepArgs a{state, state, action, reset_state, step_count, nullptr, done, truncated, nullptr, nullptr, err,
                err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
-               cyclical, hist_cap, reinterpret_cast<uint8_t*>(workspace + 2), next_index, workspace};
+               cyclical, hist_cap, reinterpret_cast<uint64_t*>(ws), curriculum_states, n_states, next_index,
+               curr_index, needs_host};
     StepLaunch f{a, (hipStream_t)stream, true};
-    const int st = dispatch(L, f);
-    if (st != ACX_OK) return st;
-    return acx_internal_curriculum_fused(done, truncated, curriculum_states, n_states, next_index, curr_index,
-                                         needs_host, state, reset_state, obs_f32, workspace, B, L, stream);
+    return dispatch(L, f);
 }
 
 int acx_rollout(int32_t* state, const int32_t* actions, const int32_t* reset_state, int32_t* step_count,

@@ -704,8 +704,17 @@ struct Shard {
     int chunk_npar = 0;       // local parents of the last committed chunk
     int64_t* look_host = nullptr;
     void* bounce = nullptr;  // pinned (copy_to_host)
+    // a read-back that timed out (sync_ctl) left its kernels on the stream: `fence` is recorded
+    // behind them, the shard refuses work (`stalled`) until acx_sbfs_reset has waited for it, and
+    // the destructor waits for it before freeing anything those kernels may still use
+    hipEvent_t fence = nullptr;
+    bool stalled = false;
 
     ~Shard() {
+        if (fence) {
+            (void)hipEventSynchronize(fence);
+            (void)hipEventDestroy(fence);
+        }
         void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.sslot, a.srf,
                         a.lost, a.mine, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
@@ -778,7 +787,7 @@ __global__ void sbfs_publish_kernel(Ctl* c, Pub* host, uint64_t seq, int reset) 
 // stream is queried (a failed launch), and a control block not published within 30 s (a kernel
 // that does not finish) is an error.
 static int sync_ctl(Shard* S, hipStream_t st, int reset = 0) {
-    if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
+    if (S->stalled || hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
     const uint64_t want = ++S->pub_seq;
     sbfs_publish_kernel<<<dim3(1), dim3(WAVE), 0, st>>>(S->a.ctl, S->pub, want, reset);
     if (hipGetLastError() != hipSuccess) return ACX_E_LAUNCH;
@@ -792,7 +801,13 @@ static int sync_ctl(Shard* S, hipStream_t st, int reset = 0) {
                 return ACX_E_LAUNCH;
             }
             if (e != hipErrorNotReady) return ACX_E_LAUNCH;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return ACX_E_LAUNCH;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+                // the kernels are still queued or running: fence them (see Shard::fence)
+                if (!S->fence) (void)hipEventCreateWithFlags(&S->fence, hipEventDisableTiming);
+                if (S->fence) (void)hipEventRecord(S->fence, st);
+                S->stalled = true;
+                return ACX_E_LAUNCH;
+            }
         }
     }
     memcpy(S->ctl_host, (const void*)&S->pub->c, sizeof(Ctl));
@@ -879,6 +894,10 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
     Shard* S = static_cast<Shard*>(h);
     if (!S || !presentation) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
+    if (S->stalled) {  // a timed-out read-back: its kernels must be done before the buffers are reused
+        if (hipEventSynchronize(S->fence) != hipSuccess) return ACX_E_LAUNCH;
+        S->stalled = false;
+    }
     const int own = acx_sbfs_owner(presentation, S->L, S->world);
     if (own < 0) return own;
     S->nloc = 0;
@@ -904,6 +923,7 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
 // out (int64[5 + world]): succ_seq, err_seq, min_len, local parents, overflow, send counts
 int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, int32_t read_back, void* stream) {
     Shard* S = static_cast<Shard*>(h);
+    if (S && S->stalled) return ACX_E_LAUNCH;  // see Shard::fence
     if (!S || (read_back && !out) || P < 1 || P > S->pmax || head < 0) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;
@@ -939,6 +959,7 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, int32_t read
 // the expanded children into `send` ((sum of counts, kw + 1) uint64), grouped by owner rank
 int acx_sbfs_pack(void* h, uint64_t* send, void* stream) {
     Shard* S = static_cast<Shard*>(h);
+    if (S && S->stalled) return ACX_E_LAUNCH;  // see Shard::fence
     if (!S || !send) return ACX_E_ARG;
     uint64_t nsend = 0;  // the counts acx_sbfs_expand read back (the rank's own group is empty)
     for (int o = 0; o < S->world; ++o) nsend += S->ctl_host->cnt[o];
@@ -952,6 +973,7 @@ int acx_sbfs_pack(void* h, uint64_t* send, void* stream) {
 // probe / insert; this rank's survivors as bits of gmask ((P) int32, written here).  end = min(success seq, move-error seq) over all ranks.
 int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, uint32_t* gmask, void* stream) {
     Shard* S = static_cast<Shard*>(h);
+    if (S && S->stalled) return ACX_E_LAUNCH;  // see Shard::fence
     if (!S || !gmask || nrecv < 0 || nrecv > S->rcap || (nrecv > 0 && !recv)) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;
@@ -975,6 +997,7 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
 // overflow flags
 int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t need, int64_t* out, void* stream) {
     Shard* S = static_cast<Shard*>(h);
+    if (S && S->stalled) return ACX_E_LAUNCH;  // see Shard::fence
     if (!S || !gmask || !out) return ACX_E_ARG;
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;

@@ -13,14 +13,99 @@
 //     speculatively in one launch; children are cached until their parent is popped.
 // Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
 // acx_key_words(L) uint64 words.
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "acx.h"
 
 namespace {
+
+// A fixed set of worker threads for the BFS batch phases: run(fn) calls fn(t) for t = 0..T-1,
+// t = 0 on the calling thread, and returns when all are done.
+class Pool {
+  public:
+    explicit Pool(int n) : n_(n < 1 ? 1 : n) {
+        for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return n_; }
+    void run(const std::function<void(int)>& fn) {
+        if (n_ == 1) {
+            fn(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            left_ = n_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void loop(int t) {
+        uint64_t seen = 0;
+        while (true) {
+            const std::function<void(int)>* fn;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (quit_) return;
+                fn = fn_;
+            }
+            (*fn)(t);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int left_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
+// host threads for the BFS engine: ACX_HOST_THREADS, else the CPUs this process may run on,
+// at most 16 (the GPU box's CPU share per GPU)
+int host_threads() {
+    if (const char* e = std::getenv("ACX_HOST_THREADS")) {
+        const int v = std::atoi(e);
+        if (v >= 1) return v < 64 ? v : 64;
+    }
+    cpu_set_t cs;
+    int n = 0;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+    if (n < 1) n = (int)std::thread::hardware_concurrency();
+    return n < 1 ? 1 : (n > 16 ? 16 : n);
+}
 
 constexpr int ACT = 12;
 constexpr size_t PREFETCH = 6;  // parents of lookahead for hash-slot prefetches (BFS)
@@ -146,11 +231,66 @@ struct Engine {
                    std::chrono::steady_clock::now().time_since_epoch()).count();
     }
 
+    // ---- BFS (mode 0): each fed batch of parents is processed by T threads (feed_bfs) ----
+    // The visited set is partitioned by hash over T tables, one per thread, so a thread probes
+    // and inserts in its own table only.  Entry: (node id + 1) << 24 | tag; while a batch is being
+    // processed, a child it inserts holds a provisional entry PROV | (batch seq + 1) << 24 | tag
+    // (its key is in the fed child keys) until the commit gives it its node id.
+    static constexpr uint64_t PROV = 1ull << 63;
+    static constexpr uint64_t ID_MASK = (1ull << 39) - 1;
+    struct Part {
+        std::vector<uint64_t> table;
+        uint64_t mask = 0;
+        int64_t n = 0;
+        std::vector<int64_t> own;  // the batch's children this partition owns, in sequence order
+    };
+    Pool* pool = nullptr;
+    std::vector<Part> parts;
+    std::vector<uint64_t> b_hash;  // per child of the batch
+    std::vector<int16_t> b_len;    // total length, -1: the move failed
+    std::vector<uint8_t> b_own, b_new;
+    std::vector<uint64_t> b_slot;
+    std::vector<int64_t> b_base;  // per parent: the first node id its new children get
+    int n_threads = 1;
+
+    int owner(uint64_t h) const { return (int)((((h >> 24) & 0xffffull) * (uint64_t)n_threads) >> 16); }
+
     Engine(int mode_, int L_, int64_t max_nodes_) : mode(mode_), L(L_), kw(acx_key_words(L_)), max_nodes(max_nodes_) {
         table.assign(1 << 12, 0);
         mask = table.size() - 1;
         pk = (HDR + 6 * L + 63) / 64;
         frontier.pk = unexpanded.pk = pk;
+        if (mode == 0) {
+            n_threads = host_threads();
+            pool = new Pool(n_threads);
+            parts.resize(n_threads);
+            for (Part& P : parts) {
+                P.table.assign(1 << 12, 0);
+                P.mask = P.table.size() - 1;
+            }
+        }
+    }
+    ~Engine() { delete pool; }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    // partition P holds committed entries only (between batches): rehash into >= `want` slots
+    void grow_part(Part& P, uint64_t want) {
+        uint64_t sz = P.table.size();
+        while (sz < want) sz <<= 1;
+        if (sz == P.table.size()) return;
+        std::vector<uint64_t> old;
+        old.swap(P.table);
+        P.table.assign(sz, 0);
+        P.mask = sz - 1;
+        for (uint64_t e : old)
+            if (e) {
+                const int64_t id = (int64_t)((e >> 24) & ID_MASK) - 1;
+                const uint64_t h = hash_key(&keys[(size_t)id * kw]);
+                uint64_t q = h & P.mask;
+                while (P.table[q]) q = (q + 1) & P.mask;
+                P.table[q] = e;
+            }
     }
 
     uint64_t hash_key(const uint64_t* k) const {
@@ -259,14 +399,25 @@ struct Engine {
     void start(const uint64_t* k) {
         uint64_t slot = 0;
         const uint64_t h = hash_key(k);
-        find(k, h, &slot);
         const int tot = key_len(k, L);
         min_length = tot;
-        const int64_t id = add_node(k, h, slot, -1, -1, tot, 0);
-        if (mode == 0) queue.push_back(id);
-        else {
-            push_frontier(id, k);
+        if (mode == 0) {  // the root in its partition of the visited set
+            Part& P = parts[owner(h)];
+            keys.insert(keys.end(), k, k + kw);
+            parent.push_back(-1);
+            action.push_back(-1);
+            total.push_back((int16_t)tot);
+            depth.push_back(0);
+            cache_pos.push_back(-1);
+            P.table[h & P.mask] = entry(0, h);
+            P.n = 1;
+            n_set = 1;
+            queue.push_back(0);
+            return;
         }
+        find(k, h, &slot);
+        const int64_t id = add_node(k, h, slot, -1, -1, tot, 0);
+        push_frontier(id, k);
     }
 
     int64_t next_batch(uint64_t* out, int64_t cap) {
@@ -365,7 +516,196 @@ struct Engine {
         return ended;
     }
 
+    // BFS: the fed batch = the parents queue[head, head + P) in FIFO order, their children (P, 12,
+    // kw) in the reference's order (parent, then action: sequence number c = 12 g + a).  Same
+    // result as visiting them one by one (visit()):
+    //   1. (threads, by child) hash, total length / move error, owner partition;
+    //   2. (one thread) the first move error and the first success in sequence order, and the
+    //      new minimum totals up to there (breadth_first.py:76-89);
+    //   3. (threads, by partition) every child before that point, in sequence order within the
+    //      partition: probe, and insert the ones not seen -- the first occurrence in sequence order
+    //      wins, as the reference's sequential `in tree_nodes` test;
+    //   4. (one thread, per parent) node ids in FIFO order and the budget cut after the first parent
+    //      that brings len(tree_nodes) to max_nodes (breadth_first.py:91);
+    //   5. (threads, by parent) the new nodes written at their ids; (by partition) their entries.
+    int feed_bfs(const uint64_t* ck, int64_t P) {
+        const int64_t t0 = now_ns();
+        const int T = n_threads;
+        const int64_t C = P * ACT;
+        b_hash.resize((size_t)C);
+        b_len.resize((size_t)C);
+        b_own.resize((size_t)C);
+        b_new.assign((size_t)C, 0);
+        b_slot.resize((size_t)C);
+        b_base.resize((size_t)P + 1);
+        pool->run([&](int t) {
+            const int64_t c0 = C * t / T, c1 = C * (t + 1) / T;
+            for (int64_t c = c0; c < c1; ++c) {
+                const uint64_t* k = ck + (size_t)c * kw;
+                const uint64_t h = hash_key(k);
+                b_hash[(size_t)c] = h;
+                b_len[(size_t)c] = key_is_error(k, L) ? (int16_t)-1 : (int16_t)key_len(k, L);
+                b_own[(size_t)c] = (uint8_t)owner(h);
+            }
+        });
+        const int64_t t1 = now_ns();
+        ns_store += t1 - t0;
+        // 2. the reference's per-child order: move error (utils.py:264-266, before any test), new
+        // minimum (breadth_first.py:79-82), success (:84-88), then the dedup insert -- the first
+        // error or success ends the search there (if the budget has not ended it before)
+        int64_t end = C, succ = -1, err_c = -1;
+        for (int64_t c = 0; c < C; ++c) {
+            const int len = b_len[(size_t)c];
+            if (len < 0 || len == 2) {
+                (len < 0 ? err_c : succ) = c;
+                end = c;
+                break;
+            }
+        }
+        // 3. probe / insert by partition
+        pool->run([&](int t) {
+            Part& Pt = parts[t];
+            Pt.own.clear();
+            for (int64_t c = 0; c < end; ++c)
+                if (b_own[(size_t)c] == t) Pt.own.push_back(c);
+            grow_part(Pt, 2 * (uint64_t)(Pt.n + (int64_t)Pt.own.size()) + 2);
+            const size_t m = Pt.own.size();
+            for (size_t i = 0; i < m; ++i) {
+                if (i + 8 < m) __builtin_prefetch(&Pt.table[b_hash[(size_t)Pt.own[i + 8]] & Pt.mask], 0, 1);
+                const int64_t c = Pt.own[i];
+                const uint64_t h = b_hash[(size_t)c];
+                const uint64_t* k = ck + (size_t)c * kw;
+                const uint64_t tag = h >> 40;
+                uint64_t q = h & Pt.mask;
+                bool seen = false;
+                while (true) {
+                    const uint64_t e = Pt.table[q];
+                    if (!e) break;
+                    if ((e & 0xffffffull) == tag) {
+                        const int64_t v = (int64_t)((e >> 24) & ID_MASK) - 1;
+                        const uint64_t* o = (e & PROV) ? ck + (size_t)v * kw : &keys[(size_t)v * kw];
+                        if (std::memcmp(o, k, sizeof(uint64_t) * kw) == 0) {
+                            seen = true;
+                            break;
+                        }
+                    }
+                    q = (q + 1) & Pt.mask;
+                }
+                if (!seen) {
+                    Pt.table[q] = PROV | ((uint64_t)(c + 1) << 24) | tag;
+                    b_slot[(size_t)c] = q;
+                    b_new[(size_t)c] = 1;
+                    ++Pt.n;
+                }
+            }
+        });
+        // 4. ids in FIFO order; where the batch stops (an error / success inside parent g, or the
+        // budget after parent g)
+        int64_t n = n_set, stop = P - 1;
+        bool budget = false;
+        for (int64_t g = 0; g < P; ++g) {
+            b_base[(size_t)g] = n;
+            const int64_t c0 = g * ACT, c1 = c0 + ACT < end ? c0 + ACT : end;
+            for (int64_t c = c0; c < c1; ++c) n += b_new[(size_t)c];
+            if (end < c0 + ACT) {
+                stop = g;
+                break;
+            }
+            if (n >= max_nodes) {
+                stop = g;
+                budget = true;
+                break;
+            }
+        }
+        const int64_t limit = std::min<int64_t>(end, (stop + 1) * ACT);  // children committed: c < limit
+        const bool ended_here = end < (stop + 1) * ACT;  // the error / success is inside the last visited parent
+        // the new minimum totals over the children the reference tests, in order (the successful
+        // child included, the failing one not)
+        const int64_t trace_end = ended_here && succ >= 0 ? succ + 1 : limit;
+        for (int64_t c = 0; c < trace_end; ++c) {
+            const int len = b_len[(size_t)c];
+            if (len < min_length) {
+                min_length = len;
+                trace.push_back(len);
+            }
+        }
+        // 5. commit
+        const int64_t n0 = n_set;
+        keys.resize((size_t)n * kw);
+        parent.resize((size_t)n);
+        action.resize((size_t)n);
+        total.resize((size_t)n);
+        depth.resize((size_t)n);
+        cache_pos.resize((size_t)n, -1);
+        queue.resize((size_t)n);
+        const int64_t qh = (int64_t)head;
+        pool->run([&](int t) {
+            const int64_t g0 = (stop + 1) * t / T, g1 = (stop + 1) * (t + 1) / T;
+            for (int64_t g = g0; g < g1; ++g) {
+                const int64_t par = queue[(size_t)(qh + g)];
+                int64_t id = b_base[(size_t)g];
+                const int64_t c0 = g * ACT, c1 = c0 + ACT < limit ? c0 + ACT : limit;
+                for (int64_t c = c0; c < c1; ++c) {
+                    if (!b_new[(size_t)c]) continue;
+                    std::memcpy(&keys[(size_t)id * kw], ck + (size_t)c * kw, sizeof(uint64_t) * kw);
+                    parent[(size_t)id] = par;
+                    action[(size_t)id] = (int8_t)(c - c0);
+                    total[(size_t)id] = b_len[(size_t)c];
+                    depth[(size_t)id] = depth[(size_t)par] + 1;
+                    queue[(size_t)id] = id;
+                    b_slot[(size_t)c] |= (uint64_t)id << 32;  // slot < 2^32 (a partition's size)
+                    ++id;
+                }
+            }
+        });
+        pool->run([&](int t) {
+            Part& Pt = parts[t];
+            for (const int64_t c : Pt.own) {
+                if (!b_new[(size_t)c]) continue;
+                const uint64_t q = b_slot[(size_t)c] & 0xffffffffull;
+                // a child past the cut keeps its provisional entry: the search ends with this batch
+                if (c < limit) Pt.table[q] = entry((int64_t)(b_slot[(size_t)c] >> 32), b_hash[(size_t)c]);
+            }
+        });
+        n_set = n;
+        (void)n0;
+        // bookkeeping as visit() leaves it
+        const int64_t visited = stop + 1;
+        for (int64_t g = 0; g < visited; ++g) popped.push_back(queue[(size_t)(qh + g)]);
+        st_pops += visited;
+        last_popped = queue[(size_t)(qh + stop)];
+        head += (size_t)visited;
+        const int64_t last_c = ended_here ? (err_c >= 0 ? err_c - 1 : succ) : limit - 1;
+        if (last_c >= 0) {
+            last_action = (int)(last_c % ACT);
+            last_len = b_len[(size_t)last_c];
+        }
+        if (ended_here && err_c >= 0) {
+            status = 3;
+        } else if (ended_here) {
+            status = 1;
+            const int64_t g = succ / ACT;
+            found_parent = queue[(size_t)(qh + g)];
+            found_action = (int)(succ % ACT);
+            found_len = 2;
+            found_explored = qh + g + 1;  // n_set - (len(queue) - head) with every node queued once
+            std::memcpy(found_key, ck + (size_t)succ * kw, sizeof(uint64_t) * kw);
+        } else if (budget) {
+            status = 2;
+            budget_hit = 1;
+        } else if (head >= queue.size()) {
+            status = 2;  // the queue ran out (breadth_first.py:97)
+        }
+        ns_visit += now_ns() - t1;
+        return status;
+    }
+
     int feed(const uint64_t* child_keys, int64_t count) {
+        if (mode == 0) {
+            if (count != (int64_t)batch.size() || (int64_t)head + count != (int64_t)requested) return -1;
+            batch.clear();
+            return count > 0 ? feed_bfs(child_keys, count) : status;
+        }
         const int64_t t0 = now_ns();
         for (int64_t i = 0; i < count && i < (int64_t)batch.size(); ++i)
             store_children(batch[i], child_keys + (size_t)i * ACT * kw);

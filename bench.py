@@ -30,9 +30,12 @@ torchrun starts the ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the envi
 script itself (children, never an exec) and exits with their status.  Every rank checks that the
 process group it joined has exactly --gpus ranks.
 
-CPU baseline (rank 0, N = 1): oracle/np_port.py -- a numpy restatement with the reference's
-per-env ACEnv.step call pattern -- one process per host core (bounded at 16), 64 envs each,
-~10 s, same starting states and action stream.  Run before the GPU is touched.
+CPU baseline (every N): oracle/np_port.py -- a numpy restatement with the reference's per-env
+ACEnv.step call pattern -- one process per host core (bounded at 16), 64 envs each, ~10 s, same
+starting states and action stream, plus the C oracle on one core and on every core.  Measured
+once per run before any rank touches the GPU: by the launcher before it starts the ranks (`--gpus
+N` on its own; handed to rank 0 through a JSON file named in ACX_BENCH_CPU_JSON), or by rank 0
+before it joins the process group (torchrun), so every line -- N = 1, 2, 4, 8 -- carries it.
 
 `--dry-run` exercises the launcher, the process group, the world-size check and the line's
 per-rank fields with no GPU (gloo, a numpy pass per step instead of the kernels); its line says
@@ -158,6 +161,36 @@ def cpu_baseline_c_all(L: int, horizon: int, seconds: float, max_procs: int = 16
         total += n / el
     return {"value": total, "unit": "env-steps/s", "cores": procs_n, "kind": "port",
             "sample": f"oracle/acx_oracle.c env_step, {procs_n} procs x 16384 envs x {seconds:.0f}s"}
+
+
+CPU_JSON_ENV = "ACX_BENCH_CPU_JSON"  # the launcher's CPU baselines, handed to rank 0
+
+
+def cpu_baselines(args, where: str) -> dict:
+    """the three CPU baselines of the line (numpy port on every core, C oracle on one core and on
+    every core), measured here and now -- before anything in this process touches the GPU"""
+    if args.no_cpu:
+        return {}
+    L, H = args.L, args.horizon
+    out = {"cpu_baseline": cpu_baseline(L, H, args.cpu_seconds),
+           "cpu_baseline_c_oracle": cpu_baseline_c(L, H, min(5.0, args.cpu_seconds)),
+           "cpu_baseline_c_oracle_all_cores": cpu_baseline_c_all(L, H, min(5.0, args.cpu_seconds))}
+    for v in out.values():
+        v["measured"] = where
+    return out
+
+
+def cpu_for_rank(args, rank: int, world: int) -> dict:
+    """this rank's CPU baselines for the line: rank 0 takes the launcher's (ACX_BENCH_CPU_JSON) or
+    measures them itself before it joins the process group; other ranks report none"""
+    if rank != 0 or args.no_cpu:
+        return {}
+    path = os.environ.get(CPU_JSON_ENV)
+    if path:
+        with open(path) as f:
+            return json.load(f)
+    return cpu_baselines(args, f"rank 0 of {world}, before the process group and the GPU" if world > 1
+                         else "before the GPU is touched")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -305,7 +338,21 @@ def main():
     if args.gpus < 1:
         sys.exit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        # the CPU baselines on the host's cores before any rank starts (none of them is busy yet)
+        tmp = None
+        if not args.no_cpu:
+            import tempfile
+
+            fd, tmp = tempfile.mkstemp(prefix="acx_bench_cpu_", suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(cpu_baselines(args, f"launcher, before the {args.gpus} ranks started"), f)
+            os.environ[CPU_JSON_ENV] = tmp
+        try:
+            rc = spawn_ranks(args.gpus, sys.argv[1:])
+        finally:
+            if tmp:
+                os.unlink(tmp)
+        sys.exit(rc)
     run_rank(args)
 
 
@@ -332,11 +379,70 @@ def _per_rank_rows(rows):
     return [{"rank": i, "value": r[0], "kernel_ms": r[1], "frac": r[2], "wall_ms": r[3]} for i, r in enumerate(rows)]
 
 
+def restore(snap, tensors) -> None:
+    for x, y in zip(tensors, snap):
+        x.copy_(y)
+
+
+def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=None) -> dict:
+    """What the n steps step_fn(0..n-1) will do from here, counted off the clock: they are run
+    from a snapshot of `tensors` (every buffer the steps read and write; the kernels are
+    deterministic, so the timed pass that follows takes this same walk) and the snapshot is put
+    back.  Per env-step: "changed" relators (the in-place write-back's unit), with `lens` (the
+    lengths-carrying step's (B, 2) lengths) the "live_read" / "live_written" bytes of 16-byte
+    chunks, with `finished` ((done, truncated) uint8 tensors) the "finished" envs."""
+    import torch
+
+    snap = [t.clone() for t in tensors]
+    B = state.shape[0]
+    chg = rd = wr = fin = 0.0
+    for t in range(n):
+        before = state.clone()
+        n_before = lens.clone() if lens is not None else None
+        step_fn(t)
+        ch = (before.view(B, 2, L) != state.view(B, 2, L)).any(2)
+        chg += float(ch.sum().item())
+        if lens is not None:
+            c_old = (n_before.clamp(0, L) + 3) // 4
+            c_new = (lens.clamp(0, L) + 3) // 4
+            rd += float(c_old.sum().item()) * 16
+            wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16
+        if finished is not None:
+            fin += float((finished[0] | finished[1]).sum().item())
+        del before, n_before
+    restore(snap, tensors)
+    d = max(1, n) * B
+    return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d}
+
+
+def learner_buffers(lenv) -> list:
+    """every device tensor a LearnerEnv step reads or writes (its own and its VecACEnv's)"""
+    import torch
+
+    out, seen = [], set()
+    for obj in (lenv, lenv.vec):
+        for v in vars(obj).values():
+            if torch.is_tensor(v) and v.is_cuda and v.data_ptr() not in seen:
+                seen.add(v.data_ptr())
+                out.append(v)
+    return out
+
+
+def learner_bytes(L: int, changed: float, finished: float) -> float:
+    """algorithmic bytes per env-step of acx_learner_step (one launch, curriculum fused): state
+    read 8L, obs float32 8L, action int64 8, step count in/out 8, reward / done float32 8,
+    done / truncated 2, move history 1, episode length 4, err 1, needs_host 1; changed relators
+    x 4L written in place; per finished env its next start row read 8L (curriculum or reset
+    row), its reset row written 8L and curr_index 4"""
+    return 16 * L + 33 + 4 * L * changed + finished * (16 * L + 4)
+
+
 def dry_run(args, rank: int, local_rank: int, world: int) -> None:
     """Launcher / process-group / line plumbing with no GPU: a numpy pass over this rank's
-    (B, 2L) int32 shard per step stands in for the kernels."""
+    (B, 2L) int32 shard per step stands in for the kernels (the CPU baselines are real)."""
     import torch.distributed as dist
 
+    cpu = cpu_for_rank(args, rank, world)
     dev = dist_setup(local_rank, world, "gloo", cpu=True)
     seen = _check_world(args, rank)
     (B, scaling), L, K, W = per_rank_batch(args, seen), args.L, args.steps, args.warmup
@@ -363,6 +469,8 @@ def dry_run(args, rank: int, local_rank: int, world: int) -> None:
         "dry_run": True, "world_size_seen": seen, "per_rank": _per_rank_rows(rows),
         "config": {"workload": f"dry run ({args.workload})", "global_batch": seen * B, "envs_per_gpu": B,
                    "max_relator_length": L, "parallelism": f"env-index shards x{seen}, no data-path collective"},
+        "cpu_baseline": cpu.get("cpu_baseline"), "cpu_baseline_c_oracle": cpu.get("cpu_baseline_c_oracle"),
+        "cpu_baseline_c_oracle_all_cores": cpu.get("cpu_baseline_c_oracle_all_cores"),
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -378,14 +486,8 @@ def run_rank(args):
         return dry_run(args, rank, local_rank, world)
     (B, scaling), L, K, W, H = per_rank_batch(args, world), args.L, args.steps, args.warmup, args.horizon
 
-    cpu = None
-    cpu_c = None
-    cpu_c_all = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        # before anything touches the GPU
-        cpu = cpu_baseline(L, H, args.cpu_seconds)
-        cpu_c = cpu_baseline_c(L, H, min(5.0, args.cpu_seconds))
-        cpu_c_all = cpu_baseline_c_all(L, H, min(5.0, args.cpu_seconds))
+    # before anything touches the GPU (rank 0 at every N: the launcher's, or measured here)
+    cpus = cpu_for_rank(args, rank, world)
 
     import torch
     import torch.distributed as dist
@@ -625,7 +727,6 @@ def run_rank(args):
                          "kernel": f"acx::rollout_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,2>"}}
         del obs8, rew8, dn8, tr8, st8, cnt8
 
-    chg_rate = None  # changed relators per env-step of the in-place step (step_api)
     if not args.no_step_api or not rollout_head:
         # per-call acx_step API: one launch per env step, state in place in HBM, autoreset
         rew1 = torch.empty(B, dtype=torch.int32, device=dev)
@@ -647,25 +748,20 @@ def run_rank(args):
             for t in range(K):
                 step(actions[W + t])
 
+        # The in-place step writes back only the relators that changed (gated moves, no-op cyclic
+        # conjugations and failed envs leave their rows as they are in HBM), so its bytes depend on
+        # the walk: counted over exactly the K timed steps, run first off the clock from a snapshot
+        # (the kernel is deterministic, so the timed pass -- and the hipGraph replay below, started
+        # from the same snapshot -- takes this same walk).
+        snap1 = (st1.clone(), cnt1.clone(), err_count.clone())
+        chg = replay_walk(lambda t: step(actions[W + t]), st1, (st1, cnt1, err_count), K, L)["changed"]
         wall_api, s_api, wall_api_local = timed(go_steps)
         n_err_api = int(err_count.item())
-        # The in-place step writes back only the relators that changed (gated moves, no-op
-        # cyclic conjugations and failed envs leave their rows as they are in HBM), so the bytes
-        # it must move depend on the walk: measured off the clock over the next 8 steps of the
-        # same walk as the mean number of changed relators per env-step.
-        chg = 0.0
-        for t in range(8):
-            before = st1.clone()
-            step(actions[(W + K + t) % actions.shape[0]])
-            chg += float(((before.view(B, 2, L) != st1.view(B, 2, L)).any(2)).sum().item()) / B
-            del before
-        chg /= 8
-        chg_rate = chg
         # per env-step: state in 8L + action 4 + count in 4 + changed relators x 4L + lengths 8 +
         # reward 4 + done 1 + truncated 1 + count out 4 + err 1 (SURVEY 8d counts full-row
         # writes, 8L out; the in-place kernel skips unchanged relators, PMC-checked r02h)
         sb = 8 * L + 27 + 4 * L * chg
-        step_kernel = f"acx::step_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,false>"
+        step_kernel = ops.step_kernel_name(B, L)
         variants["step_api"] = {
             "value": seen * B * K / wall_api, "unit": "env-steps/s", "ms_per_step": wall_api / K * 1e3,
             "kernel_ms": s_api * 1e3,
@@ -673,13 +769,15 @@ def run_rank(args):
                          "unit": "GB/s", "frac": B * sb / (s_api / K) / 1e9 / HBM_PEAK_GBS, "kernel": step_kernel,
                          "bytes_per_env_step": sb, "changed_relators_per_env_step": chg,
                          "bytes_note": "state read 8L + changed relators x 4L written + 27 B of scalars "
-                                       "(in place: unchanged relators are not written)"},
+                                       "(in place: unchanged relators are not written); changed relators "
+                                       "counted over exactly the timed steps (an untimed replay from a snapshot)"},
             "env_errors": n_err_api,
         }
         # the same walk through the lengths-carrying step (acx_step_lengths), where VecACEnv.step
         # takes it (ops.LENGTHS_STEP_L) or with --workload step; at L = 36 it ties with acx_step
         # (DESIGN.md "The lengths-carrying step") and the default line leaves it out
         run_len = not rollout_head or L in ops.LENGTHS_STEP_L
+        same = True
         if run_len:
             st2 = starts.clone()
             cnt2 = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -698,34 +796,17 @@ def run_rank(args):
                 for t in range(K):
                     step2(actions[W + t])
 
-            # algorithmic bytes of exactly the timed steps: the same K steps are first run off the
-            # clock from a snapshot (the kernel is deterministic, so the timed pass replays this
-            # walk): per relator its live 16-byte chunks read (ceil(n/4)), for a changed relator the
-            # chunks inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.
-            # The live bytes follow the walk's lengths, which grow through a horizon and drop at the
+            # algorithmic bytes of exactly the timed steps (replayed off the clock from a snapshot):
+            # per relator its live 16-byte chunks read (ceil(n/4)), for a changed relator the chunks
+            # inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.  The
+            # live bytes follow the walk's lengths, which grow through a horizon and drop at the
             # synchronised resets, so a sample of other steps would not do.
-            snap = (st2.clone(), cnt2.clone(), lens2.clone(), err_count.clone())
-            rd = wr = 0.0
-            for t in range(K):
-                before, n_before = st2.clone(), lens2.clone()
-                step2(actions[W + t])
-                ch = (before.view(B, 2, L) != st2.view(B, 2, L)).any(2)
-                c_old = (n_before.clamp(0, L) + 3) // 4
-                c_new = (lens2.clamp(0, L) + 3) // 4
-                rd += float(c_old.sum().item()) * 16 / B
-                wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16 / B
-                del before, n_before
-            rd, wr = rd / K, wr / K
+            rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, err_count), K, L, lens=lens2)
+            rd, wr = rp["live_read"], rp["live_written"]
             sb_len = rd + wr + 16 + 27
-            for x, y in zip((st2, cnt2, lens2, err_count), snap):
-                x.copy_(y)
-            del snap
-
             wall_len, s_len, wall_len_local = timed(go_steps2)
             n_err_len = int(err_count.item())
-            for t in range(8):  # the step_api walk took 8 more steps (its changed-relator sample)
-                step2(actions[(W + K + t) % actions.shape[0]])
-            same = bool(torch.equal(st1, st2))  # both walks took the same W + K + 8 steps
+            same = bool(torch.equal(st1, st2))  # both walks took the same W + K steps
             len_kernel = f"acx::step_lengths_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4>"
             a_len = B * sb_len / (s_len / K) / 1e9
             variants["step_api_lengths"] = {
@@ -737,19 +818,14 @@ def run_rank(args):
                              "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
                                            "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
                                            "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
-                                           "relator's last live chunk brings its sector's dead ones (PMC 1.13x these "
-                                           "bytes over this command's 200 launches, profiles/r04/"
-                                           "r04w_step128_summary.json; 1.30x early in a horizon)",
-                             "compute_note": "mid-horizon the launch runs at ~0.93 of the bare cost of its own "
-                                             "access pattern (live-chunk reads + changed-relator write-back, "
-                                             "profiles/r04/r04z_live_shape_ceiling.json); early in a horizon (short "
-                                             "relators) VALU issue is most of the launch "
-                                             "(profiles/r04/r04w_step_horizon.json)"},
+                                           "relator's last live chunk brings its sector's dead ones"},
                 "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
             }
+            if not same:  # a lengths-path regression must not publish a headline
+                variants["step_api_lengths"]["error"] = "states differ from acx_step's on the same walk"
             del st2, cnt2, lens2
-        if not rollout_head and L not in ops.LENGTHS_STEP_L:
-            # whole-row tiles: the env's step is acx_step (the step_api variant)
+        if not rollout_head and (L not in ops.LENGTHS_STEP_L or not same):
+            # whole-row tiles (or a lengths walk that left acx_step's states): the headline is acx_step
             a_api = B * sb / (s_api / K) / 1e9
             head = {
                 "elapsed": wall_api, "kernel_s": s_api, "wall_local": wall_api_local, "frac": a_api / HBM_PEAK_GBS,
@@ -757,7 +833,7 @@ def run_rank(args):
                                  launch_bytes=B * sb),
                 "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step, {B} envs/GPU, L={L}, "
                              f"horizon {H}, cyclical=True, in-place state, same-step autoreset; {K} launches"),
-                "env_errors": n_err_api,
+                "env_errors": n_err_api + (0 if same else 1),
             }
         elif not rollout_head:
             head = {
@@ -771,7 +847,8 @@ def run_rank(args):
             }
 
         # the same K per-call steps captured once into a hipGraph (torch.cuda.CUDAGraph over
-        # the ctypes launches on the capture stream) and replayed: no per-launch host cost
+        # the ctypes launches on the capture stream) and replayed from the timed walk's snapshot:
+        # no per-launch host cost, the same bytes as step_api
         if not args.no_graph:
             gs = torch.cuda.Stream(device=dev)
             gs.wait_stream(torch.cuda.current_stream(dev))
@@ -780,21 +857,24 @@ def run_rank(args):
                 with torch.cuda.graph(graph, stream=gs):
                     go_steps()
             torch.cuda.synchronize()
+            restore(snap1, (st1, cnt1, err_count))
             graph.replay()  # warm
+            restore(snap1, (st1, cnt1, err_count))
             wall_g, s_g, _ = timed(graph.replay)
             variants["step_api_hipgraph"] = {
                 "value": seen * B * K / wall_g, "unit": "env-steps/s", "ms_per_step": wall_g / K * 1e3,
-                "kernel_ms": s_g * 1e3,
+                "kernel_ms": s_g * 1e3, "env_errors": int(err_count.item()),
                 "roofline": {"bound": "hbm", "achieved": B * sb / (s_g / K) / 1e9, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": B * sb / (s_g / K) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_env_step": sb},
             }
             del graph
+        del snap1
 
     if not args.no_learner and world == 1:
-        # PPO plumbing (acx.agents.LearnerEnv): per step one acx_step_learner (int64 policy
+        # PPO plumbing (acx.agents.LearnerEnv): per step one acx_learner_step launch (int64 policy
         # actions in, float32 obs straight into the learner's (T+1,B,2L) buffer, float32
-        # reward/done, episode move history) + one acx_curriculum_assign
+        # reward/done, episode move history, the round-1 curriculum assignment fused in)
         from acx.agents import LearnerEnv
         KL = min(K, 50)
         lenv = LearnerEnv(np.concatenate([ms_starts(L, B), ms_starts(L, 4096, offset=B)]), B, horizon_length=H,
@@ -806,24 +886,31 @@ def run_rank(args):
         lobs.zero_()
         lenv.step(la[0], obs_out=lobs[1], reward_out=lrew[0], done_out=ldone[0])
 
+        def lstep(t):
+            lenv.step(la[t], obs_out=lobs[t + 1], reward_out=lrew[t], done_out=ldone[t])
+
         def go_learn():
             for t in range(KL):
-                lenv.step(la[t], obs_out=lobs[t + 1], reward_out=lrew[t], done_out=ldone[t])
+                lstep(t)
 
+        # the learner's own walk, replayed off the clock from a snapshot of every buffer it owns:
+        # changed relators and finished envs per env-step of exactly the timed steps
+        lbufs = learner_buffers(lenv)
+        rp = replay_walk(lstep, lenv.state, lbufs, KL, L, finished=(lenv.done, lenv.truncated))
         _, s_l, _ = timed(go_learn)
-        # per env-step: state in/out 16L + action 8 + count in/out 8 + obs f32 8L + reward f32 4
-        # + done f32 4 + done/trunc u8 2 + history 1 + episode_len 4 + err 1 + curriculum
-        # (done/trunc re-read 2, needs_host 1).  The state store is in place (changed relators
-        # only, see step_api): the same walk distribution as the step_api variant, so its
-        # measured changed-relator rate prices the state write-back.
-        lb_full = 24 * L + 35
-        lb = lb_full if chg_rate is None else lb_full - 8 * L + 4 * L * chg_rate
+        lb = learner_bytes(L, rp["changed"], rp["finished"])
         variants["learner_step"] = {
             "value": B * KL / s_l, "unit": "env-steps/s", "steps": KL, "ms_per_step": s_l / KL * 1e3,
             "roofline": {"bound": "hbm", "achieved": B * lb / (s_l / KL) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb},
+                         "frac": B * lb / (s_l / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb,
+                         "changed_relators_per_env_step": rp["changed"], "finished_per_env_step": rp["finished"],
+                         "kernel": f"acx::step_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,true> "
+                                   "(curriculum fused, one launch)",
+                         "bytes_note": "16L state read + obs f32 write + 32 B of per-env scalars + changed relators "
+                                       "x 4L + per finished env 8L + 8L + 4 (curriculum row in, reset row out, "
+                                       "curr_index) + needs_host 1; counted over exactly the timed steps"},
         }
-        del lobs, lrew, ldone, lenv
+        del lobs, lrew, ldone, lenv, lbufs
 
     if not args.no_config2 and world == 1 and rollout_head:
         variants["config2_step"] = config2_variant(dev, H, timed)
@@ -873,9 +960,9 @@ def run_rank(args):
         "dist_backend": backend if seen > 1 else None,
         "per_rank": _per_rank_rows(rows),
         "roofline": head["roofline"],
-        "cpu_baseline": cpu,
-        "cpu_baseline_c_oracle": cpu_c,
-        "cpu_baseline_c_oracle_all_cores": cpu_c_all,
+        "cpu_baseline": cpus.get("cpu_baseline"),
+        "cpu_baseline_c_oracle": cpus.get("cpu_baseline_c_oracle"),
+        "cpu_baseline_c_oracle_all_cores": cpus.get("cpu_baseline_c_oracle_all_cores"),
         "variants": variants,
         "env_errors": head["env_errors"],
     }
@@ -940,8 +1027,9 @@ def config2_variant(dev, H: int, timed) -> dict:
     """BASELINE configs[1]: 65,536 envs, L = 36, Miller-Schupp starts, uniform random move ids
     (device generator, seed 0), per-call step API in place with same-step autoreset (SURVEY 8(d)
     config 2), 200 timed steps after 10 warm-up steps; eager launches and the same 200 launches
-    replayed from one hipGraph.  At this batch a launch moves ~24 MB, so launch latency, not HBM,
-    bounds it ("bound": "launch"; frac is against HBM anyway)."""
+    replayed from one hipGraph.  A launch moves ~24 MB: the small-batch step instance
+    (ops.step_kernel_name) keeps the whole tile's loads in flight so that the one wave per SIMD
+    this batch gives is not exposed three round trips deep."""
     import torch
 
     from acx import ops
@@ -966,27 +1054,25 @@ def config2_variant(dev, H: int, timed) -> dict:
 
     for t in range(W2):
         step(acts[t])
-    snap = (st.clone(), cnt.clone())
+    snap = (st.clone(), cnt.clone(), ec.clone())
 
     def go():
         for t in range(K2):
             step(acts[W2 + t])
 
+    # changed relators per env-step (the in-place write-back) over exactly the timed steps, replayed
+    # off the clock from the snapshot (the eager and the hipGraph passes both start from it)
+    chg = replay_walk(lambda t: step(acts[W2 + t]), st, (st, cnt, ec), K2, L2)["changed"]
     wall, s_k, _ = timed(go)
     n_err = int(ec.item())
-    chg = 0.0  # changed relators per env-step (the in-place write-back), off the clock
-    for t in range(8):
-        before = st.clone()
-        step(acts[W2 + K2 + t])
-        chg += float(((before.view(B2, 2, L2) != st.view(B2, 2, L2)).any(2)).sum().item()) / B2 / 8
     sb = 8 * L2 + 27 + 4 * L2 * chg
     out = {"value": B2 * K2 / wall, "unit": "env-steps/s", "ms_per_step": wall / K2 * 1e3, "kernel_ms": s_k * 1e3,
            "env_errors": n_err, "envs": B2, "steps": K2,
-           "roofline": {"bound": "launch", "achieved": B2 * sb / (s_k / K2) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": B2 * sb / (s_k / K2) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": sb},
+           "roofline": {"bound": "hbm", "achieved": B2 * sb / (s_k / K2) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": B2 * sb / (s_k / K2) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": sb,
+                        "changed_relators_per_env_step": chg, "kernel": ops.step_kernel_name(B2, L2)},
            "workload": "BASELINE configs[1]: 65536 envs, L=36, Miller-Schupp starts, uniform random actions, per-call "
                        "acx_step in place, horizon 200, same-step autoreset; 200 launches"}
-    st.copy_(snap[0]), cnt.copy_(snap[1])
     gs = torch.cuda.Stream(device=dev)
     gs.wait_stream(torch.cuda.current_stream(dev))
     graph = torch.cuda.CUDAGraph()
@@ -994,11 +1080,14 @@ def config2_variant(dev, H: int, timed) -> dict:
         with torch.cuda.graph(graph, stream=gs):
             go()
     torch.cuda.synchronize()
-    st.copy_(snap[0]), cnt.copy_(snap[1])
+    restore(snap, (st, cnt, ec))
     graph.replay()  # warm
-    st.copy_(snap[0]), cnt.copy_(snap[1])
+    restore(snap, (st, cnt, ec))
     wall_g, s_g, _ = timed(graph.replay)
-    out["hipgraph"] = {"value": B2 * K2 / wall_g, "ms_per_step": wall_g / K2 * 1e3, "kernel_ms": s_g * 1e3}
+    out["hipgraph"] = {"value": B2 * K2 / wall_g, "ms_per_step": wall_g / K2 * 1e3, "kernel_ms": s_g * 1e3,
+                       "env_errors": int(ec.item()),
+                       "roofline": {"bound": "hbm", "achieved": B2 * sb / (s_g / K2) / 1e9, "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": B2 * sb / (s_g / K2) / 1e9 / HBM_PEAK_GBS}}
     del graph
     return out
 

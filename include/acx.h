@@ -173,7 +173,9 @@ int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* ac
  * its state, reset_state (nullable) and obs_f32 (nullable) rows are set to that state and
  * curr_index[env] = k.  When k reaches n_states round 1 is complete and the env is flagged in
  * needs_host[env] = 1 (the reference then draws a random solved/unsolved state on the host).
- * workspace: acx_curriculum_workspace(B) int32 device words.
+ * workspace: acx_curriculum_workspace(B) int32 device words, 8-byte aligned, zeroed before the
+ * first call and not written by the caller afterwards (acx_learner_step keeps its look-back state
+ * there; one workspace serves both calls, but not two launches at once).
  */
 int64_t acx_curriculum_workspace(int64_t B);
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
@@ -182,11 +184,18 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
                           int32_t L, void* stream);
 
 /*
- * One PPO env step = acx_step_learner (final_obs NULL) followed by acx_curriculum_assign, in
- * two launches instead of four: the step kernel also writes each 64-env wave's finished
- * count, from which the curriculum pass ranks the finished envs directly.  Same results as
- * the two calls; done, truncated, reset_state and the curriculum arguments are required;
- * workspace = acx_curriculum_workspace(B) int32 words.
+ * One PPO env step = acx_step_learner (final_obs NULL) followed by acx_curriculum_assign
+ * (training.py:238-241, 319-352), in ONE launch: the step kernel ranks the finished envs in env
+ * order itself (a single-pass scan with decoupled look-back over 64-env tiles) and a finished env
+ * resets straight to its curriculum state -- state, obs_f32 and reset_state rows, curr_index[env]
+ * = k.  Same results as the two calls, except that a curriculum row outside the packed domain
+ * (letters other than +-1/+-2, a zero inside a relator) is not loaded: the env resets to its own
+ * reset_state row, curr_index[env] = k and needs_host[env] = 2 -- the host places that state as
+ * it is (acx.agents.LearnerEnv.place), as acx_curriculum_assign would have copied it.
+ * needs_host[env] = 3: the look-back gave up (a predecessor tile not scheduled within ~seconds, or a
+ * workspace shared by concurrent launches); the env reset to its own row and was not ranked.
+ * done, truncated, reset_state and the curriculum
+ * arguments are required; B < 2^31; workspace = acx_curriculum_workspace(B) int32 words (above).
  */
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,

@@ -4,7 +4,9 @@ per step in place of the kernels).
 * `bench.py --gpus 2` with no torchrun environment starts two rank processes itself, both join one
   process group, and rank 0 prints ONE line with n_gpus 2, world_size_seen 2 and a per-rank block;
 * a torchrun group whose size differs from --gpus fails with a non-zero status (no line);
-* a rank that fails makes the launcher fail with that rank's status."""
+* a rank that fails makes the launcher fail with that rank's status;
+* every line carries the CPU baselines, N > 1 included (measured by the launcher before it starts
+  the ranks, or by rank 0 before it joins the process group under torchrun)."""
 import json
 import os
 import socket
@@ -29,7 +31,7 @@ def _lines(out):
 
 def test_launcher_spawns_two_ranks_one_line():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "4", "--warmup", "1",
-                        "--batch", "512"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
+                        "--batch", "512", "--no-cpu"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _lines(p.stdout)
     assert len(lines) == 1, p.stdout
@@ -42,7 +44,7 @@ def test_launcher_spawns_two_ranks_one_line():
 
 
 def test_one_rank_line_has_the_same_shape():
-    p = subprocess.run([sys.executable, BENCH, "--dry-run", "--steps", "3", "--warmup", "0", "--batch", "256"],
+    p = subprocess.run([sys.executable, BENCH, "--dry-run", "--steps", "3", "--warmup", "0", "--batch", "256", "--no-cpu"],
                        cwd=REPO, capture_output=True, text=True, timeout=120, env=_env())
     assert p.returncode == 0, p.stderr[-3000:]
     (d,) = _lines(p.stdout)
@@ -61,7 +63,7 @@ def test_world_size_mismatch_fails():
     # torchrun starts 2 ranks but the command says --gpus 3: every rank refuses to measure
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH, "--gpus", "3",
-                        "--dry-run", "--steps", "2", "--warmup", "0", "--batch", "64"],
+                        "--dry-run", "--steps", "2", "--warmup", "0", "--batch", "64", "--no-cpu"],
                        cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
     assert p.returncode != 0
     assert not _lines(p.stdout)
@@ -122,11 +124,44 @@ def test_line_guard_disarms_on_exit():
 def test_strong_scaling_splits_the_global_batch():
     """--global-batch: the total is fixed and split over the ranks (SURVEY 8(d) strong scaling)."""
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1",
-                        "--global-batch", "1024"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
+                        "--global-batch", "1024", "--no-cpu"], cwd=REPO, capture_output=True, text=True, timeout=180, env=_env())
     assert p.returncode == 0, p.stderr[-3000:]
     (d,) = _lines(p.stdout)
     assert d["scaling"] == "strong" and d["n_gpus"] == 2
     assert d["config"]["global_batch"] == 1024 and d["config"]["envs_per_gpu"] == 512
-    bad = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--global-batch", "1000"], cwd=REPO,
+    bad = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--global-batch", "1000", "--no-cpu"], cwd=REPO,
                          capture_output=True, text=True, timeout=180, env=_env())
     assert bad.returncode != 0 and "multiple of 64" in bad.stderr
+
+
+def _check_cpu(d, where):
+    for k in ("cpu_baseline", "cpu_baseline_c_oracle", "cpu_baseline_c_oracle_all_cores"):
+        c = d[k]
+        assert c and c["value"] > 0 and c["cores"] >= 1 and c["unit"] == "env-steps/s", k
+        assert where in c["measured"], (k, c["measured"])
+    assert d["cpu_baseline"]["kind"] == "port"
+
+
+def test_launcher_line_carries_cpu_baseline():
+    """`bench.py --gpus 2` (the launcher) puts the CPU baselines -- measured on
+    the host's cores before any rank started -- into rank 0's line."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "0",
+                        "--batch", "256", "--cpu-seconds", "1"], cwd=REPO, capture_output=True, text=True,
+                       timeout=240, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    (d,) = _lines(p.stdout)
+    assert d["n_gpus"] == 2
+    _check_cpu(d, "launcher")
+
+
+def test_torchrun_line_carries_cpu_baseline():
+    """Under torchrun (the driver's N > 1 command) rank 0 measures the CPU baselines before it joins
+    the process group."""
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH, "--gpus", "2",
+                        "--dry-run", "--steps", "2", "--warmup", "0", "--batch", "256", "--cpu-seconds", "1"],
+                       cwd=REPO, capture_output=True, text=True, timeout=240, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    (d,) = _lines(p.stdout)
+    assert d["n_gpus"] == 2
+    _check_cpu(d, "rank 0 of 2")

@@ -230,10 +230,14 @@ def test_engine_miller_schupp_cases_on_oracle_expansions():
     assert paths == case["paths"]
 
 
-def test_engine_matches_reference_on_random_searches():
+@pytest.mark.parametrize("threads", ["1", "3", "16"])
+def test_engine_matches_reference_on_random_searches(threads, monkeypatch):
     """kat_search_extra.json: 240 reference bfs/greedy runs on random small presentations
     (budgets 1..5000, both cyclical flags), including runs where a move raises
-    AssertionError and the node count the budget message prints."""
+    AssertionError and the node count the budget message prints.  The BFS engine's batch phases
+    run on ACX_HOST_THREADS threads (visited set partitioned by hash): any count gives the
+    reference's result."""
+    monkeypatch.setenv("ACX_HOST_THREADS", threads)
     with open(os.path.join(GOLDEN, "kat_search_extra.json")) as f:
         cases = json.load(f)
     for c in cases:

@@ -86,3 +86,45 @@ def test_next_step_mode_rejects_final_info_layout():
                  autoreset_mode="next_step")
     with pytest.raises(ValueError):
         VecACEnv(_starts(36, 64), device=DEV, autoreset_mode="bogus")
+
+
+def test_rollout_refuses_per_env_state_it_cannot_keep():
+    """The fused rollout is same-step autoreset with no move history: in next-step
+    mode or with record_actions it raises instead of leaving pending flags / histories stale,
+    and step() after the refused call still matches a fresh env stepped the same way."""
+    from acx.envs.ac_env import VecACEnv
+    B, L = 256, 36
+    acts = torch.randint(0, 12, (4, B), dtype=torch.int32, device=DEV)
+    a = VecACEnv(_starts(L, B), horizon_length=3, device=DEV, autoreset_mode="next_step")
+    b = VecACEnv(_starts(L, B), horizon_length=3, device=DEV, autoreset_mode="next_step")
+    a.step(acts[0])
+    b.step(acts[0])
+    with pytest.raises(ValueError):
+        a.rollout(acts[1:3])
+    for t in (1, 2, 3):
+        a.step(acts[t])
+        b.step(acts[t])
+        assert torch.equal(a.state, b.state) and torch.equal(a.pending, b.pending)
+    r = VecACEnv(_starts(L, B), device=DEV, record_actions=True)
+    with pytest.raises(ValueError):
+        r.rollout(acts[:2])
+
+
+def test_reset_takes_starting_states_unvalidated():
+    """reset(options={"starting_states": rows}) copies the rows as the reference's ACEnv.reset
+    does (ac_env.py:113-129, no validation); an out-of-domain row is then held as it is and
+    reported with err 3 by every step, its exact values kept."""
+    from acx.envs.ac_env import VecACEnv
+    B, L = 128, 36
+    env = VecACEnv(_starts(L, B), horizon_length=50, device=DEV)
+    rows = _starts(L, B)
+    assert rows[5, 2] != 0
+    rows[5, 1] = 0  # a zero inside relator 0 (its letters continue after it)
+    rows[9, L] = 7  # a letter outside the packed domain
+    env.reset(options={"starting_states": rows})
+    assert torch.equal(env.state.cpu(), torch.as_tensor(rows))
+    env.step(torch.zeros(B, dtype=torch.int32, device=DEV))
+    err = env.err.cpu().numpy()
+    assert err[5] == 3 and err[9] == 3 and (np.delete(err, [5, 9]) == 0).all()
+    st = env.state.cpu().numpy()
+    assert np.array_equal(st[5], rows[5]) and np.array_equal(st[9], rows[9])

@@ -186,3 +186,83 @@ def test_learner_env_matches_reference_training_loop(case, fused):
             assert np.array_equal(obs.cpu().numpy(), g["post_state"][t].astype(np.float32)), (name, t)
             assert np.array_equal(env.state.cpu().numpy(), g["post_state"][t].astype(np.int32)), (name, t)
     check_final(rec, m)
+
+
+def test_fused_learner_step_full_size_lookback():
+    """The fused step's look-back at a full per-GPU batch (2^20 envs = 16,384 tiles, two resident
+    rounds): desynchronised episodes (about B/H finished envs per step, scattered), then a step
+    where every env finishes (the whole batch ranked in one launch) across round-1 completion --
+    state, outputs, curriculum indices, next_index and host flags equal to the four-launch path
+    (acx_step_learner + acx_curriculum_assign)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import ms_starts
+    from acx.agents import LearnerEnv
+    L, B, H = 36, 1 << 20, 7
+    N = B + (H + 2) * B // H + B // 2  # round 1 completes inside the all-finish step
+    init = ms_starts(L, N)
+    ea = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    eb = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    desync = (torch.arange(B, dtype=torch.int32, device=DEV) * 5) % H
+    ea.vec.step_count.copy_(desync)
+    eb.vec.step_count.copy_(desync)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    outs = [[torch.empty((B, 2 * L), dtype=torch.float32, device=DEV), torch.empty(B, dtype=torch.float32, device=DEV),
+             torch.empty(B, dtype=torch.float32, device=DEV)] for _ in range(2)]
+    n_fin = []
+    for t in range(2 * H + 2):
+        if t == H + 1:  # every env finishes on this step
+            ea.vec.step_count.fill_(H - 1)
+            eb.vec.step_count.fill_(H - 1)
+        a = torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)
+        ra = ea.step(a, *outs[0], fused=True)
+        rb = eb.step(a, *outs[1], fused=False)
+        for x, y in zip(ra, rb):
+            assert torch.equal(x, y), t
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), t
+        assert torch.equal(ea.state, eb.state) and torch.equal(ea.vec.reset_state, eb.vec.reset_state), t
+        assert torch.equal(ea.curr_index, eb.curr_index) and torch.equal(ea.next_index, eb.next_index), t
+        n_fin.append(int((ra[0] | ra[1]).sum().item()))
+        nh = ra[3] != 0
+        ea.needs_host[nh] = 0
+        eb.needs_host[nh] = 0
+    assert n_fin[H + 1] == B and int(ea.next_index.item()) == N
+    assert min(n_fin[: H]) > B // (2 * H)
+    del ea, eb, outs
+    torch.cuda.empty_cache()
+
+
+def test_fused_learner_step_out_of_domain_curriculum_row():
+    """A curriculum row outside the packed domain is not loaded by the fused step: the env resets
+    to its own row with needs_host = 2 and curr_index = that state's index; placed by the host
+    (CurriculumRecord.process -> LearnerEnv.place) it ends exactly as the four-launch path, which
+    copies the row as it is (acx_curriculum_assign); later steps report it as err 3 on both."""
+    from acx.agents import CurriculumRecord, LearnerEnv
+    L, B, N, H = 36, 256, 900, 2
+    init = _ms_states(L, N)
+    for k in (B + 3, B + 70, B + 300):
+        init[k, 5] = 3  # a letter outside +-1 / +-2
+    init[B + 130, 1] = 0  # a zero inside relator 0
+    ea = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    eb = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    ra_rec = CurriculumRecord(N, B, 0.5)
+    rb_rec = CurriculumRecord(N, B, 0.5)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    codes = set()
+    for t in range(2 * H + 1):
+        a = torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)
+        oa = torch.empty((B, 2 * L), dtype=torch.float32, device=DEV)
+        ob = torch.empty((B, 2 * L), dtype=torch.float32, device=DEV)
+        da, ta, _, ha = ea.step(a, obs_out=oa, fused=True)
+        db, tb, _, hb = eb.step(a, obs_out=ob, fused=False)
+        codes |= set(ha.cpu().numpy().tolist())
+        pa = ra_rec.process(ea, da, ta, ha, obs_out=oa)
+        pb = rb_rec.process(eb, db, tb, hb, obs_out=ob)
+        assert pa == pb, t
+        assert torch.equal(ea.state, eb.state) and torch.equal(ea.vec.reset_state, eb.vec.reset_state), t
+        assert torch.equal(oa, ob) and torch.equal(ea.curr_index, eb.curr_index), t
+        assert torch.equal(ea.vec.step_count, eb.vec.step_count), t
+    assert 2 in codes

@@ -189,3 +189,138 @@ def test_vec_env_lengths_after_rollout_and_direct_writes(L):
             assert torch.equal(x, y), t
         assert torch.equal(env.lengths, twin.lengths), t
     assert _lib.E_ARG < 0
+
+
+# ---------------------------------------------------------------------------------------------
+# acx_step_lengths pinned directly to the reference fixtures and to the oracle (VERDICT r04
+# item 3): the reference's carried lengths are ac_env.py:81-95 (self.lengths from reset, passed to
+# and returned by ACMove) and ac_moves.py:159-231.
+# ---------------------------------------------------------------------------------------------
+def _lengths_step(lib, st, at, rs, cnt, rew, dn, tr, lens, fo, err, ec, B, L, H, cyc):
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    P = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+    rc = lib.acx_step_lengths(P(st), P(at), P(rs), P(cnt), P(rew), P(dn), P(tr), P(lens), P(fo), P(err), P(ec),
+                              B, L, H, cyc, stream)
+    assert rc == 0, rc
+
+
+@pytest.mark.parametrize("L", [7, 18, 36, 128])
+@pytest.mark.parametrize("cyc", [1, 0])
+def test_step_lengths_transitions_fixture(L, cyc):
+    """The reference's random transitions (tests/golden/transitions.npz, made by running the
+    reference's ACMove): in place, with the lengths VecACEnv carries in (_row_extent); every
+    row ends as the reference's output with the reference's lengths, failed rows keep their input
+    row (and report (L, L) when out of domain, so the next call reads them whole)."""
+    from acx import _lib
+    from acx.envs.ac_env import _row_extent
+    from conftest import GOLDEN
+    import os
+    lib = _lib.load()
+    d = np.load(os.path.join(GOLDEN, "transitions.npz"))
+    k = f"L{L}_c{cyc}_"
+    s_in = d[k + "state_in"].astype(np.int32)
+    B = s_in.shape[0]
+    st = _t(s_in)
+    lens = _row_extent(st, L).contiguous()
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    _lengths_step(lib, st, _t(d[k + "action"].astype(np.int32)), None, None, None, None, None, lens, None, err,
+                  None, B, L, 10 ** 6, cyc)
+    out, e, ln = st.cpu().numpy(), err.cpu().numpy(), lens.cpu().numpy()
+    assert np.array_equal(e, d[k + "err"].astype(np.uint8))
+    ok = e == 0
+    assert ok.sum() > B // 2
+    assert np.array_equal(out[ok], d[k + "state_out"][ok].astype(np.int32))
+    assert np.array_equal(ln[ok], d[k + "lengths"][ok].astype(np.int32))
+    assert np.array_equal(out[~ok], s_in[~ok])
+    assert (ln[e == 3] == L).all()
+
+
+def test_step_lengths_reference_episodes():
+    """ACEnv episodes run by the reference (tests/golden/env_episodes.npz, explicit reset() on done
+    or truncated): acx_step_lengths with same-step autoreset reproduces every step's observation,
+    reward, flags and final observation, and its carried lengths stay the rows' letter counts."""
+    from acx import _lib
+    from conftest import GOLDEN
+    import os
+    lib = _lib.load()
+    d = np.load(os.path.join(GOLDEN, "env_episodes.npz"))
+    L, H = int(d["L"]), int(d["horizon"])
+    init = d["initial"].astype(np.int32)
+    B = init.shape[0]
+    st, rs = _t(init), _t(init)
+    lens = _t(np.stack([np.count_nonzero(init[:, :L], 1), np.count_nonzero(init[:, L:], 1)], 1).astype(np.int32))
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    rew = torch.zeros(B, dtype=torch.int32, device=DEV)
+    dn = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    tr = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    fo = torch.zeros((B, 2 * L), dtype=torch.int32, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    ec = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for t in range(d["actions"].shape[0]):
+        _lengths_step(lib, st, _t(d["actions"][t].astype(np.int32)), rs, cnt, rew, dn, tr, lens, fo, err, ec, B, L,
+                      H, 1)
+        obs = st.cpu().numpy()
+        assert np.array_equal(obs, d["obs"][t].astype(np.int32)), t
+        assert np.array_equal(rew.cpu().numpy(), d["reward"][t]), t
+        assert np.array_equal(dn.cpu().numpy(), d["done"][t].astype(np.uint8)), t
+        assert np.array_equal(tr.cpu().numpy(), d["truncated"][t].astype(np.uint8)), t
+        m = (d["done"][t] | d["truncated"][t]).astype(bool)
+        assert np.array_equal(fo.cpu().numpy()[m], d["final_obs"][t][m].astype(np.int32)), t
+        ln = lens.cpu().numpy()
+        assert np.array_equal(ln[:, 0], np.count_nonzero(obs[:, :L], 1)), t
+        assert np.array_equal(ln[:, 1], np.count_nonzero(obs[:, L:], 1)), t
+    assert int(ec.item()) == 0
+
+
+@pytest.mark.parametrize("cyc", [1, 0])
+def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc):
+    """A random walk at L = 128 (config 5's kernel) with autoreset -- short horizon, desynchronised
+    and synchronised resets, a few bad move ids -- every env, every step against the oracle's
+    ACMove (oracle/acx_oracle.c, pinned to the reference's fixtures) under acx's error contract
+    (conftest.env_step_contract: a failed move keeps state and count): state, reward, done,
+    truncated, step count, err, final observation and the carried lengths."""
+    from acx import _lib
+    from conftest import env_step_contract
+    from oracle import oracle as O
+    lib = _lib.load()
+    L, B, T, H = 128, 64 * 23 + 5, 60, 13
+    rng = np.random.default_rng(128 + cyc)
+    starts = _rows(L, B, rng)
+    count0 = (np.arange(B) % H).astype(np.int32)
+    count0[: 64 * 4] = 0  # four whole waves truncate together (the tile-reload path)
+    st, rs = _t(starts), _t(starts)
+    cnt = _t(count0)
+    lens = _t(np.stack([np.count_nonzero(starts[:, :L], 1), np.count_nonzero(starts[:, L:], 1)], 1).astype(np.int32))
+    rew = torch.zeros(B, dtype=torch.int32, device=DEV)
+    dn = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    tr = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    fo = torch.zeros((B, 2 * L), dtype=torch.int32, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    o_st, o_cnt = starts.copy(), count0.copy()
+    n_reset = n_err = 0
+    for t in range(T):
+        a = rng.integers(0, 12, size=B).astype(np.int32)
+        if t % 11 == 5:
+            a[::97] = -1  # ACX_ERR_ACTION: state and count kept
+        _lengths_step(lib, st, _t(a), rs, cnt, rew, dn, tr, lens, fo, err, None, B, L, H, cyc)
+        # the pre-reset states (final_observation), then the step under acx's error contract (a
+        # failed move keeps state and count: conftest.env_step_contract, checked against the oracle)
+        moved, _, merr = O.move_batch(o_st, a, L, cyc)
+        fin = o_st.copy()
+        fin[merr == 0] = moved[merr == 0]
+        r, d_, trn, e = env_step_contract(o_st, a, o_cnt, starts, L, H, cyc)
+        assert np.array_equal(st.cpu().numpy(), o_st), t
+        assert np.array_equal(err.cpu().numpy(), e), t
+        ok = e == 0
+        assert np.array_equal(rew.cpu().numpy(), r), t
+        assert np.array_equal(dn.cpu().numpy(), d_), t
+        assert np.array_equal(tr.cpu().numpy(), trn), t
+        assert np.array_equal(cnt.cpu().numpy(), o_cnt), t
+        m = (d_ | trn).astype(bool)
+        assert np.array_equal(fo.cpu().numpy()[m], fin[m]), t
+        got = lens.cpu().numpy()
+        assert np.array_equal(got[:, 0], np.count_nonzero(o_st[:, :L], 1)), t
+        assert np.array_equal(got[:, 1], np.count_nonzero(o_st[:, L:], 1)), t
+        n_reset += int(m.sum())
+        n_err += int((~ok).sum())
+    assert n_reset > B and n_err > 0

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-5 session b: a -m gpu subset (-k), config 2's probe (tools/config2_probe.py) and the
+# default bench line without the CPU baseline.  Each GPU step under its own limit.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r05b}
+K=${2:-}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd $R
+if [ -n "$K" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "$K" > $OUT/${TAG}_gpu_tests.log 2>&1
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/${TAG}_gpu_tests.log 2>&1
+fi
+rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/${TAG}_gpu_tests.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u tools/config2_probe.py ab5/libacx_small.so ab5/libacx_small_ntsc.so ab5/libacx_nosmall.so ab5/libacx_nosmall_ntsc.so > $OUT/${TAG}_config2_probe.json 2> $OUT/${TAG}_config2_probe.err || exit 3
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-cpu > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err || exit 4
+echo session-done

@@ -143,7 +143,12 @@ int probe_live(int wr, void* state, const void* lengths, int64_t rows, int lds_p
     return (int)hipGetLastError();
 }
 
-// kind: 0 read_grid, 1 read_tile, 2 read_tile_pipe, 3 rw_tile, 4 rw_tile_pipe; nb in {8, 16};
+// the same grid as a step launch doing nothing (the floor of a launch at this grid: config 2)
+__global__ __launch_bounds__(256) void empty_kernel(int64_t rows, int* out) {
+    if (rows < 0 && threadIdx.x == 0) out[blockIdx.x] = 1;
+}
+
+// kind: 0 read_grid, 1 read_tile, 2 read_tile_pipe, 3 rw_tile, 4 rw_tile_pipe, 5 empty; nb in {8, 16};
 // lds_per_block bytes of dynamic LDS (occupancy control); returns 0 or a hip error code
 int probe_run(int kind, int nb, void* state, int64_t rows, int L, int lds_per_block, void* out, void* stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -152,6 +157,8 @@ int probe_run(int kind, int nb, void* state, int64_t rows, int L, int lds_per_bl
     const unsigned tiles = (unsigned)((rows + 255) / 256);
     if (kind == 0) {
         read_grid<<<dim3(256 * 8 * 4), dim3(BLOCK), 0, s>>>(st, rows * cpr, (int*)out);
+    } else if (kind == 5) {
+        empty_kernel<<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>(rows, (int*)out);
     } else {
 #define GO(NB, P, W) tile_kernel<NB, P, W><<<dim3(tiles), dim3(BLOCK), lds_per_block, s>>>(st, cpr, rows, (int*)out)
         if (nb == 8) {
