@@ -143,7 +143,8 @@ extern "C" {
 int64_t acx_internal_curriculum_fused_offset(int64_t B);
 int64_t acx_curriculum_workspace(int64_t B) {
     if (B < 0) return 0;
-    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + (B + WAVE - 1) / WAVE);
+    const int64_t tiles = (B + WAVE - 1) / WAVE, groups = (tiles + WAVE - 1) / WAVE;
+    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + tiles + 2 * groups);
 }
 
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
@@ -168,8 +169,9 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
 // acx_learner_step (acx_kernels.hip) ranks the finished envs inside its step kernel with a
 // look-back over per-64-env-tile status words; its part of the workspace starts after this
 // file's (next_index copy + per-block counts), so either call may use one workspace:
-// [off, off + 2) the launch sequence number, [off + 2, off + 6) reserved, then one uint64 per
-// 64-env tile (acx_kernels.hip cur_lookback).
+// uint64 words from off: the launch sequence number, the base, one reserved word, one count per
+// 64-env tile, then per group of 64 tiles its total and its arrival word (acx_kernels.hip
+// cur_publish / cur_prefix).
 int64_t acx_internal_curriculum_fused_offset(int64_t B) {
     const int64_t own = (B + TPB - 1) / TPB + 2;
     return (own + 1) & ~(int64_t)1;  // 8-byte aligned

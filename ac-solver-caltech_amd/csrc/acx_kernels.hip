@@ -1998,7 +1998,7 @@ struct StepArgs {
     int L, horizon, cyclical, hist_cap;
     // acx_learner_step: the round-1 curriculum fused into the step (training.py:319-352).
     // cur_ws NULL: none.  cur_ws (uint64 words): [0] launch sequence number, [1, 2] reserved,
-    // [3 + t] tile t's look-back status (cur_lookback)
+    // then the tiles' counts, the groups' totals and arrival words (cur_publish, cur_prefix)
     uint64_t* cur_ws;
     const int32_t* cur_states;  // (n_states, 2L) initial states
     int64_t n_states;
@@ -2019,25 +2019,29 @@ struct StepArgs {
 // The curriculum's ranking inside the step kernel (acx_learner_step, one launch).  Finished envs
 // (done | truncated) take the initial states next_index, next_index + 1, ... in env order
 // (training.py:329-336), so an env needs the number of finished envs before it -- a prefix count
-// over the whole batch.  Single-pass chained scan with decoupled look-back, one 64-env tile per
-// wave, tiles in launch order (blockIdx):
-//   * a tile's status is one 64-bit word (flag 2 bits | launch sequence number 30 | value 32),
-//     written and polled with agent-scope atomics (the word is the whole hand-off: MI355X_MICROARCH
-//     "8-B agent atomics both sides"); flag 1 = the tile's own count, flag 2 = inclusive prefix;
-//     tile 0's prefix starts at *next_index, so a tile's exclusive prefix IS the first index it
-//     hands out.  Each wave publishes its count before it looks back;
-//   * words of an earlier launch carry another sequence number and read as "not ready".  Every
-//     wave reads the sequence number (cur_ws[0]) before it publishes, so once the LAST tile's
-//     look-back is through -- every tile has published by then -- no wave of this launch reads it
-//     again, and the last tile advances it (and next_index) for the next launch.  No ticket or
-//     arrival counter: one word per tile, no same-address atomics (MI355X_MICROARCH "dequeue":
-//     ~88 per us on one word);
-//   * HIP promises no dispatch order: a wave that polls too long (2^20 polls, ~seconds -- a
-//     predecessor never scheduled, or a workspace shared by concurrent launches) gives up, so the
-//     launch always ends; that tile and every later one publish CUR_FAIL and flag their finished
-//     envs needs_host = 3 (CurriculumRecord.process raises).
+// over the whole batch -- and the last tile needs the total (the new next_index).  Two levels,
+// no chain: a tile is one wave's 64 envs, a group is 64 consecutive tiles.
+//   * every tile publishes its count (a seq-tagged status word) and adds (1, count) to its
+//     group's arrival word with one 64-bit atomic; the add that completes the group publishes the
+//     group's total and clears the arrival word for the next launch (64 adds per address at most:
+//     MI355X_MICROARCH "dequeue" -- one word saturates at ~88 adds per us);
+//   * tile 0 publishes next_index as the scan's base;
+//   * a tile that needs its prefix -- one with finished envs -- polls the base, the totals of the
+//     groups before its own and the counts of the tiles before it in its group, until all are
+//     there (no propagation through intermediate tiles: it waits only for earlier tiles to have
+//     published once); the last tile polls every group total, writes next_index and advances the
+//     launch's sequence number;
+//   * words are written and polled with agent-scope atomics (each word is the whole hand-off:
+//     "8-B agent atomics both sides"); a word of an earlier launch carries another sequence number
+//     and reads as not there.  Every wave reads the sequence number before it publishes, so once
+//     every group is complete no wave of the launch reads it again and the last tile may advance it;
+//   * HIP promises no dispatch order: a tile that polls too long (2^20 polls, ~seconds -- an
+//     earlier tile never scheduled, or a workspace shared by concurrent launches) gives up and flags
+//     its finished envs needs_host = 3 (CurriculumRecord.process raises), so the launch always ends.
+// cur_ws (uint64 words): [0] sequence number, [1] base, [2] reserved, [3, 3 + T) tile counts,
+// [3 + T, 3 + T + G) group totals, [3 + T + G, 3 + T + 2G) group arrival words (T tiles, G groups).
 // ---------------------------------------------------------------------------------
-constexpr uint64_t CUR_AGG = 1ull << 62, CUR_INC = 2ull << 62;
+constexpr uint64_t CUR_SET = 1ull << 62;
 constexpr uint32_t CUR_FAIL = 0xffffffffu;
 constexpr uint32_t CUR_SEQ_MASK = (1u << 30) - 1u;
 
@@ -2050,8 +2054,11 @@ __device__ __forceinline__ void copy_row(int32_t* dst, const int32_t* src, int t
     }
 }
 
-__device__ __forceinline__ uint64_t cur_word(uint64_t flag, uint32_t seq, uint32_t v) {
-    return flag | ((uint64_t)(seq & CUR_SEQ_MASK) << 32) | v;
+__device__ __forceinline__ uint64_t cur_word(uint32_t seq, uint32_t v) {
+    return CUR_SET | ((uint64_t)(seq & CUR_SEQ_MASK) << 32) | v;
+}
+__device__ __forceinline__ bool cur_is(uint64_t w, uint32_t seq) {
+    return (w >> 62) == 1 && ((uint32_t)(w >> 32) & CUR_SEQ_MASK) == (seq & CUR_SEQ_MASK);
 }
 __device__ __forceinline__ uint64_t cur_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2060,88 +2067,77 @@ __device__ __forceinline__ void cur_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the tile's first index (next_index + finished envs of all earlier tiles), or CUR_FAIL;
-// publishes this tile's inclusive prefix.  Wave-uniform control flow; fm = ballot of finished.
-// Each poll reads CUR_LANE predecessors per lane (64 * CUR_LANE tiles, one round trip): the
-// look-back walks back that far per round trip while the inclusive prefixes propagate forward,
-// so a synchronised start (every resident wave publishing at once) settles in ~t / (128 CUR_LANE)
-// round trips instead of ~t / 128 (16,384 tiles at 2^20 envs)
-constexpr int CUR_LANE = 8;
-__device__ __forceinline__ uint32_t cur_lookback(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint64_t fm) {
-    uint64_t* st = a.cur_ws + 3;
-    const int64_t t = w.r0 / WAVE;
-    const uint32_t agg = (uint32_t)__popcll(fm);
-    uint32_t excl;
-    if (t == 0) {
-        excl = (uint32_t)*a.cur_next;  // the scan starts at next_index (read by tile 0 alone)
-    } else {
-        if (w.lane == 0) cur_store(st + t, cur_word(CUR_AGG, seq, agg));
-        excl = 0;
-        int64_t j = t - 1;  // the nearest predecessor not yet summed (wave-uniform)
-        uint32_t polls = 0;
-        bool fail = false;
-        const uint32_t sq = seq & CUR_SEQ_MASK;
-        while (true) {
-            // lane l holds predecessors j - (l * CUR_LANE + i), i = 0 (nearest) .. CUR_LANE - 1
-            uint64_t v[CUR_LANE];
+struct CurLayout {
+    int64_t tiles, groups;
+    uint64_t *base, *tile, *group, *arrive;
+    __device__ __forceinline__ CurLayout(const StepArgs& a) {
+        tiles = (a.B + WAVE - 1) / WAVE;
+        groups = (tiles + WAVE - 1) / WAVE;
+        base = a.cur_ws + 1;
+        tile = a.cur_ws + 3;
+        group = tile + tiles;
+        arrive = group + groups;
+    }
+};
+
+// this tile's count, its group arrival, and (tile 0) the base
+__device__ __forceinline__ void cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt) {
+    if (w.lane != 0) return;
+    const CurLayout c(a);
+    const int64_t t = w.r0 / WAVE, g = t / WAVE;
+    if (t == 0) cur_store(c.base, cur_word(seq, (uint32_t)*a.cur_next));
+    cur_store(c.tile + t, cur_word(seq, cnt));
+    const int64_t gsize = (c.tiles - g * WAVE) < WAVE ? (c.tiles - g * WAVE) : WAVE;
+    const uint64_t old = __hip_atomic_fetch_add(c.arrive + g, (1ull << 32) | cnt, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if ((int64_t)(old >> 32) + 1 == gsize) {  // the group is complete: its total, and a clean word
+        cur_store(c.group + g, cur_word(seq, (uint32_t)old + cnt));
+        cur_store(c.arrive + g, 0ull);
+    }
+}
+
+// base + the counts of every tile before this one (all_groups: + every group's total instead: the
+// last tile's next_index), or CUR_FAIL.  Wave-uniform control flow.
+__device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, bool all_groups) {
+    const CurLayout c(a);
+    const int64_t t = w.r0 / WAVE, g = t / WAVE;
+    const int64_t ng = all_groups ? c.groups : g;  // whole groups summed
+    uint32_t polls = 0;
+    while (true) {
+        bool ok = true;
+        uint32_t x = 0;
+        if (w.lane == 0) {
+            const uint64_t v = cur_load(c.base);
+            ok = cur_is(v, seq);
+            x = (uint32_t)v;
+        }
+        for (int64_t k0 = 0; k0 < ng; k0 += 4 * WAVE) {  // 4 group totals per lane per round
+            uint64_t v[4];
 #pragma unroll
-            for (int i = 0; i < CUR_LANE; ++i) {
-                const int64_t q = j - ((int64_t)w.lane * CUR_LANE + i);
-                v[i] = q >= 0 ? cur_load(st + q) : (CUR_AGG | ((uint64_t)sq << 32));  // past tile 0: ready, 0
+            for (int i = 0; i < 4; ++i) {
+                const int64_t k = k0 + 4 * w.lane + i;
+                v[i] = k < ng ? cur_load(c.group + k) : cur_word(seq, 0);
             }
-            int first = CUR_LANE;  // this lane's nearest inclusive prefix
-            bool all_ready = true, ready_before = true;
 #pragma unroll
-            for (int i = CUR_LANE - 1; i >= 0; --i) {
-                const bool mine = ((uint32_t)(v[i] >> 32) & CUR_SEQ_MASK) == sq;
-                const uint32_t fl = (uint32_t)(v[i] >> 62);
-                const bool rdy = mine && fl != 0;
-                all_ready = all_ready && rdy;
-                if (mine && fl == 2) first = i;
+            for (int i = 0; i < 4; ++i) {
+                ok = ok && cur_is(v[i], seq);
+                x += (uint32_t)v[i];
             }
-#pragma unroll
-            for (int i = 0; i < CUR_LANE; ++i)
-                if (i < first) ready_before = ready_before && (((uint32_t)(v[i] >> 32) & CUR_SEQ_MASK) == sq && (v[i] >> 62) != 0);
-            const uint64_t incm = __ballot(first < CUR_LANE);
-            const int ls = incm ? __builtin_ctzll(incm) : WAVE;  // the lane of the nearest inclusive prefix
-            const uint64_t below = ls >= WAVE ? ~0ull : ((1ull << ls) - 1ull);
-            const bool wait_lane = (w.lane < ls && !all_ready) || (w.lane == ls && !ready_before);
-            if (__ballot(wait_lane)) {
-                if (++polls > (1u << 20)) {
-                    fail = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            (void)below;
-            uint32_t x = 0;
-            bool bad = false;
-            if (w.lane < ls) {
-#pragma unroll
-                for (int i = 0; i < CUR_LANE; ++i) x += (uint32_t)v[i];
-            } else if (w.lane == ls) {
-#pragma unroll
-                for (int i = 0; i < CUR_LANE; ++i)
-                    if (i <= first) x += (uint32_t)v[i];
-#pragma unroll
-                for (int i = 0; i < CUR_LANE; ++i)
-                    if (i == first) bad = (uint32_t)v[i] == CUR_FAIL;
-            }
-            if (__ballot(bad)) {  // an earlier tile gave up
-                fail = true;
-                break;
-            }
+        }
+        if (!all_groups) {  // the tiles before this one in its group
+            const int64_t k = g * WAVE + w.lane;
+            const uint64_t v = k < t ? cur_load(c.tile + k) : cur_word(seq, 0);
+            ok = ok && cur_is(v, seq);
+            x += (uint32_t)v;
+        }
+        if (__all(ok)) {
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, WAVE);
-            excl += x;
-            if (incm || j < (int64_t)WAVE * CUR_LANE) break;
-            j -= (int64_t)WAVE * CUR_LANE;
+            return x;
         }
-        if (fail) excl = CUR_FAIL;
+        if (++polls > (1u << 20)) return CUR_FAIL;
+        __builtin_amdgcn_s_sleep(2);
     }
-    if (w.lane == 0) cur_store(st + t, cur_word(CUR_INC, seq, excl == CUR_FAIL ? CUR_FAIL : excl + agg));
-    return excl;
 }
 
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
@@ -2152,10 +2148,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     constexpr bool NT_SC = ACX_NT_STEP_SCALARS != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
-    // acx_learner_step: the curriculum fused in (cur_lookback)
+    // acx_learner_step: the curriculum fused in (cur_publish / cur_prefix)
     const bool cur = LEARN && a.cur_ws != nullptr;  // kernel argument: uniform
     if (!wave_ctx(a.B, w)) return;
-    // the launch's sequence number, read before this tile publishes (cur_lookback)
+    // the launch's sequence number, read before this tile publishes (cur_publish)
     const uint32_t cseq = cur ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws)) : 0u;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
@@ -2253,15 +2249,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     int64_t cur_idx = -1;
     if (cur) {
         const uint64_t fm = __ballot(fin);
-        const uint32_t first = cur_lookback(a, w, cseq, fm);
-        if (w.r0 + w.R == a.B && w.lane == 0) {
-            // the last tile: every tile has published, so no wave reads next_index or the sequence
-            // number again in this launch -- advance both for the next one
-            if (first != CUR_FAIL) {
-                const int64_t n = (int64_t)first + __popcll(fm);
-                *a.cur_next = (int32_t)(n < a.n_states ? n : a.n_states);
+        cur_publish(a, w, cseq, (uint32_t)__popcll(fm));
+        // a tile with finished envs waits for its prefix (their initial states' indices); the
+        // last tile for the total (the new next_index)
+        const uint32_t first = fm ? cur_prefix(a, w, cseq, false) : 0u;
+        if (w.r0 + w.R == a.B) {
+            const uint32_t tot = cur_prefix(a, w, cseq, true);
+            if (w.lane == 0) {
+                // every group is complete: no wave of this launch reads next_index or the sequence
+                // number again -- advance both for the next one
+                if (tot != CUR_FAIL) *a.cur_next = (int32_t)((int64_t)tot < a.n_states ? (int64_t)tot : a.n_states);
+                cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
             }
-            cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
         }
         if (w.active) {
             uint8_t nh = 0;
@@ -3509,7 +3508,7 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
         !workspace)
         return ACX_E_ARG;
     if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
-    // one launch: the step kernel ranks the finished envs itself (cur_lookback) in its part of the
+    // one launch: the step kernel ranks the finished envs itself (cur_publish / cur_prefix) in its part of the
     // workspace (acx_curriculum_workspace(B) int32 words, zeroed before the first call, 8-byte aligned)
     int32_t* ws = workspace + acx_internal_curriculum_fused_offset(B);
     if ((reinterpret_cast<uintptr_t>(ws) & 7u) != 0) return ACX_E_ARG;

@@ -14,6 +14,7 @@
 // Keys are the packed states of acx_expand12 (acx.h), so set membership is a hash of
 // acx_key_words(L) uint64 words.
 #include <sched.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -93,6 +94,38 @@ class Pool {
     bool quit_ = false;
 };
 
+// std::vector whose resize() leaves new trivially-constructible elements uninitialised (the BFS
+// commit writes every new node's fields once; value-initialising them first was a second pass)
+template <class T>
+struct DefaultInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInit<U>;
+    };
+    DefaultInit() noexcept = default;
+    template <class U>
+    DefaultInit(const DefaultInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using dvec = std::vector<T, DefaultInit<T>>;
+
+// transparent huge pages for a large buffer (where the kernel's THP mode is "madvise"): the BFS
+// node arrays and visited-set partitions are first touched by many threads at once, and 4-KB
+// page faults serialise on the process's address-space lock
+inline void advise_huge(const void* p, size_t bytes) {
+    constexpr uintptr_t HP = (uintptr_t)2 << 20;
+    const uintptr_t a = ((uintptr_t)p + HP - 1) & ~(HP - 1), b = ((uintptr_t)p + bytes) & ~(HP - 1);
+    if (b > a) (void)madvise((void*)a, b - a, MADV_HUGEPAGE);
+}
+
 // host threads for the BFS engine: ACX_HOST_THREADS, else the CPUs this process may run on,
 // at most 16 (the GPU box's CPU share per GPU)
 int host_threads() {
@@ -108,7 +141,6 @@ int host_threads() {
 }
 
 constexpr int ACT = 12;
-constexpr size_t PREFETCH = 6;  // parents of lookahead for hash-slot prefetches (BFS)
 constexpr int HDR = 40;         // priority-key header bits: total (9) | depth (31)
 
 inline uint64_t mix64(uint64_t x) {
@@ -125,17 +157,18 @@ struct Engine {
     int L, kw;
     int64_t max_nodes;
     // node storage
-    std::vector<uint64_t> keys;  // node * kw
-    std::vector<int64_t> parent;
-    std::vector<int8_t> action;
-    std::vector<int16_t> total;
-    std::vector<int32_t> depth;
+    dvec<uint64_t> keys;  // node * kw
+    dvec<int64_t> parent;
+    dvec<int8_t> action;
+    dvec<int16_t> total;
+    dvec<int32_t> depth;  // greedy only
     // open-addressing hash set; entry = (node id + 1) << 24 | 24-bit hash tag, 0 = empty.
     // The tag filters almost every non-matching probe without touching the node's key.
     std::vector<uint64_t> table;
     uint64_t mask = 0;
     int64_t n_set = 0;
-    // BFS queue
+    // greedy's expansion bookkeeping (BFS: every node is queued once, when it is found, so the
+    // FIFO queue is the node ids in order -- queue[i] == i -- and is not stored)
     std::vector<int64_t> queue;
     size_t head = 0, requested = 0;
     // greedy ordered frontier: the heap tuple (total, path length, state tuple) of
@@ -239,7 +272,7 @@ struct Engine {
     static constexpr uint64_t PROV = 1ull << 63;
     static constexpr uint64_t ID_MASK = (1ull << 39) - 1;
     struct Part {
-        std::vector<uint64_t> table;
+        dvec<uint64_t> table;
         uint64_t mask = 0;
         int64_t n = 0;
         std::vector<int64_t> own;  // the batch's children this partition owns, in sequence order
@@ -252,6 +285,8 @@ struct Engine {
     std::vector<uint64_t> b_slot;
     std::vector<int64_t> b_base;  // per parent: the first node id its new children get
     int n_threads = 1;
+    uint64_t part_hint = 0;  // slots per partition sized once for the budget (no rehash on the way)
+    int64_t ph_ns[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // feed_bfs phases (acx_internal_search_phases)
 
     int owner(uint64_t h) const { return (int)((((h >> 24) & 0xffffull) * (uint64_t)n_threads) >> 16); }
 
@@ -268,6 +303,20 @@ struct Engine {
                 P.table.assign(1 << 12, 0);
                 P.mask = P.table.size() - 1;
             }
+            // the node arrays and the visited set sized for the budget up front (capacity only:
+            // pages are touched when written), so no reallocation copies or rehashes on the way
+            const int64_t rn = std::min<int64_t>(max_nodes, (int64_t)1 << 27) + 12 * 65536;
+            keys.reserve((size_t)rn * kw);
+            parent.reserve((size_t)rn);
+            action.reserve((size_t)rn);
+            total.reserve((size_t)rn);
+            advise_huge(keys.data(), keys.capacity() * sizeof(uint64_t));
+            advise_huge(parent.data(), parent.capacity() * sizeof(int64_t));
+            advise_huge(action.data(), action.capacity());
+            advise_huge(total.data(), total.capacity() * sizeof(int16_t));
+            uint64_t h = 4096;
+            while (h < (uint64_t)(2.5 * (double)rn / n_threads)) h <<= 1;
+            part_hint = h;
         }
     }
     ~Engine() { delete pool; }
@@ -277,11 +326,15 @@ struct Engine {
     // partition P holds committed entries only (between batches): rehash into >= `want` slots
     void grow_part(Part& P, uint64_t want) {
         uint64_t sz = P.table.size();
+        if (sz < part_hint && P.n <= 1) sz = part_hint;  // first batch: the budget's size at once
         while (sz < want) sz <<= 1;
         if (sz == P.table.size()) return;
-        std::vector<uint64_t> old;
+        dvec<uint64_t> old;
         old.swap(P.table);
-        P.table.assign(sz, 0);
+        P.table.reserve(sz);
+        advise_huge(P.table.data(), sz * sizeof(uint64_t));
+        P.table.resize(sz);
+        std::memset(P.table.data(), 0, sz * sizeof(uint64_t));
         P.mask = sz - 1;
         for (uint64_t e : old)
             if (e) {
@@ -412,7 +465,6 @@ struct Engine {
             P.table[h & P.mask] = entry(0, h);
             P.n = 1;
             n_set = 1;
-            queue.push_back(0);
             return;
         }
         find(k, h, &slot);
@@ -429,11 +481,8 @@ struct Engine {
     int64_t next_batch_(uint64_t* out, int64_t cap) {
         batch.clear();
         if (status != 0) return 0;
-        if (mode == 0) {
-            while ((int64_t)batch.size() < cap && requested < queue.size()) {
-                const int64_t id = queue[requested++];
-                batch.push_back(id);
-            }
+        if (mode == 0) {  // the FIFO queue is the node ids in order
+            while ((int64_t)batch.size() < cap && (int64_t)requested < n_set) batch.push_back((int64_t)requested++);
         } else {
             // the smallest unpopped nodes not expanded yet (speculative: their children are
             // cached until the node is popped in the reference's order)
@@ -492,7 +541,7 @@ struct Engine {
                 found_parent = id;
                 found_action = a;
                 found_len = len;
-                found_explored = n_set - (int64_t)(mode == 0 ? queue.size() - head : frontier.id.size());
+                found_explored = n_set - (int64_t)frontier.id.size();
                 std::memcpy(found_key, k, sizeof(uint64_t) * kw);
                 ended = true;
                 break;
@@ -562,6 +611,8 @@ struct Engine {
                 break;
             }
         }
+        const int64_t t2 = now_ns();
+        ph_ns[0] += t2 - t1;
         // 3. probe / insert by partition
         pool->run([&](int t) {
             Part& Pt = parts[t];
@@ -571,7 +622,15 @@ struct Engine {
             grow_part(Pt, 2 * (uint64_t)(Pt.n + (int64_t)Pt.own.size()) + 2);
             const size_t m = Pt.own.size();
             for (size_t i = 0; i < m; ++i) {
-                if (i + 8 < m) __builtin_prefetch(&Pt.table[b_hash[(size_t)Pt.own[i + 8]] & Pt.mask], 0, 1);
+                // two prefetch stages: the table line 16 children ahead, and 8 ahead (that line is
+                // in cache by then) the stored key of a tag match, which a duplicate is compared with
+                if (i + 16 < m) __builtin_prefetch(&Pt.table[b_hash[(size_t)Pt.own[i + 16]] & Pt.mask], 0, 1);
+                if (i + 8 < m) {
+                    const uint64_t hh = b_hash[(size_t)Pt.own[i + 8]];
+                    const uint64_t e = Pt.table[hh & Pt.mask];
+                    if (e && !(e & PROV) && (e & 0xffffffull) == (hh >> 40))
+                        __builtin_prefetch(&keys[(size_t)(((e >> 24) & ID_MASK) - 1) * kw], 0, 1);
+                }
                 const int64_t c = Pt.own[i];
                 const uint64_t h = b_hash[(size_t)c];
                 const uint64_t* k = ck + (size_t)c * kw;
@@ -599,6 +658,8 @@ struct Engine {
                 }
             }
         });
+        const int64_t t3 = now_ns();
+        ph_ns[1] += t3 - t2;
         // 4. ids in FIFO order; where the batch stops (an error / success inside parent g, or the
         // budget after parent g)
         int64_t n = n_set, stop = P - 1;
@@ -629,20 +690,21 @@ struct Engine {
                 trace.push_back(len);
             }
         }
+        const int64_t t4 = now_ns();
+        ph_ns[2] += t4 - t3;
         // 5. commit
         const int64_t n0 = n_set;
         keys.resize((size_t)n * kw);
         parent.resize((size_t)n);
         action.resize((size_t)n);
         total.resize((size_t)n);
-        depth.resize((size_t)n);
-        cache_pos.resize((size_t)n, -1);
-        queue.resize((size_t)n);
         const int64_t qh = (int64_t)head;
+        const int64_t t5 = now_ns();
+        ph_ns[3] += t5 - t4;
         pool->run([&](int t) {
             const int64_t g0 = (stop + 1) * t / T, g1 = (stop + 1) * (t + 1) / T;
             for (int64_t g = g0; g < g1; ++g) {
-                const int64_t par = queue[(size_t)(qh + g)];
+                const int64_t par = qh + g;
                 int64_t id = b_base[(size_t)g];
                 const int64_t c0 = g * ACT, c1 = c0 + ACT < limit ? c0 + ACT : limit;
                 for (int64_t c = c0; c < c1; ++c) {
@@ -651,13 +713,13 @@ struct Engine {
                     parent[(size_t)id] = par;
                     action[(size_t)id] = (int8_t)(c - c0);
                     total[(size_t)id] = b_len[(size_t)c];
-                    depth[(size_t)id] = depth[(size_t)par] + 1;
-                    queue[(size_t)id] = id;
                     b_slot[(size_t)c] |= (uint64_t)id << 32;  // slot < 2^32 (a partition's size)
                     ++id;
                 }
             }
         });
+        const int64_t t6 = now_ns();
+        ph_ns[4] += t6 - t5;
         pool->run([&](int t) {
             Part& Pt = parts[t];
             for (const int64_t c : Pt.own) {
@@ -667,13 +729,13 @@ struct Engine {
                 if (c < limit) Pt.table[q] = entry((int64_t)(b_slot[(size_t)c] >> 32), b_hash[(size_t)c]);
             }
         });
+        ph_ns[5] += now_ns() - t6;
         n_set = n;
         (void)n0;
         // bookkeeping as visit() leaves it
-        const int64_t visited = stop + 1;
-        for (int64_t g = 0; g < visited; ++g) popped.push_back(queue[(size_t)(qh + g)]);
+        const int64_t visited = stop + 1;  // parents qh .. qh + stop popped (acx_search_popped: ids 0 .. st_pops - 1)
         st_pops += visited;
-        last_popped = queue[(size_t)(qh + stop)];
+        last_popped = qh + stop;
         head += (size_t)visited;
         const int64_t last_c = ended_here ? (err_c >= 0 ? err_c - 1 : succ) : limit - 1;
         if (last_c >= 0) {
@@ -685,7 +747,7 @@ struct Engine {
         } else if (ended_here) {
             status = 1;
             const int64_t g = succ / ACT;
-            found_parent = queue[(size_t)(qh + g)];
+            found_parent = qh + g;
             found_action = (int)(succ % ACT);
             found_len = 2;
             found_explored = qh + g + 1;  // n_set - (len(queue) - head) with every node queued once
@@ -693,7 +755,7 @@ struct Engine {
         } else if (budget) {
             status = 2;
             budget_hit = 1;
-        } else if (head >= queue.size()) {
+        } else if ((int64_t)head >= n_set) {
             status = 2;  // the queue ran out (breadth_first.py:97)
         }
         ns_visit += now_ns() - t1;
@@ -703,6 +765,7 @@ struct Engine {
     int feed(const uint64_t* child_keys, int64_t count) {
         if (mode == 0) {
             if (count != (int64_t)batch.size() || (int64_t)head + count != (int64_t)requested) return -1;
+            if (status != 0) return status;
             batch.clear();
             return count > 0 ? feed_bfs(child_keys, count) : status;
         }
@@ -716,23 +779,16 @@ struct Engine {
         ns_visit += now_ns() - t1;
         return st;
     }
-    int replay() {
-        // advance as far as the cache allows
+    int replay() {  // greedy: pop as far as the cached children allow
         while (status == 0) {
-            if (mode == 0) {
-                if (head >= queue.size()) { status = 2; break; }
-                const int64_t id = queue[head];
-                if (!cached(id)) return 0;
-                if (head + PREFETCH < queue.size()) prefetch_children(queue[head + PREFETCH]);
-                ++head;
-                if (visit(id)) break;
-            } else {
-                if (frontier.empty()) { status = 2; break; }
-                const int64_t id = frontier.top();
-                if (!cached(id)) return 0;
-                frontier.pop();
-                if (visit(id)) break;
+            if (frontier.empty()) {
+                status = 2;
+                break;
             }
+            const int64_t id = frontier.top();
+            if (!cached(id)) return 0;
+            frontier.pop();
+            if (visit(id)) break;
         }
         return status;
     }
@@ -800,6 +856,13 @@ int64_t acx_search_path(void* h, int32_t* actions, int32_t* totals, int64_t cap)
     return e->path(e->last_popped, actions, totals, cap, true);
 }
 
+// BFS batch phases (tools/host_bfs_bench.cpp; not in the public header): ns in 2 (scan), 3
+// (probe / insert), 4 (ids / cut), resize, 5 (node arrays), 5 (table entries)
+void acx_internal_search_phases(void* h, int64_t* out) {
+    Engine* e = static_cast<Engine*>(h);
+    for (int i = 0; i < 6; ++i) out[i] = e->ph_ns[i];
+}
+
 // statistics: out[0] = rounds, out[1] = parents expanded on the GPU, out[2] = parents popped,
 // out[3..5] = host nanoseconds in next_batch / caching fed children / the replay
 void acx_search_stats(void* h, int64_t* out) {
@@ -815,6 +878,10 @@ void acx_search_stats(void* h, int64_t* out) {
 // ids of the expanded (popped) nodes in the reference's expansion order; returns the count
 int64_t acx_search_popped(void* h, int64_t* ids, int64_t cap) {
     Engine* e = static_cast<Engine*>(h);
+    if (e->mode == 0) {  // BFS pops the node ids in order
+        for (int64_t i = 0; ids && i < e->st_pops && i < cap; ++i) ids[i] = i;
+        return e->st_pops;
+    }
     const int64_t n = (int64_t)e->popped.size();
     for (int64_t i = 0; ids && i < n && i < cap; ++i) ids[i] = e->popped[(size_t)i];
     return n;

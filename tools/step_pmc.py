@@ -3,7 +3,9 @@
 Miller-Schupp starts, uniform moves, horizon 200 -- W + K calls each, at L = 128 then L = 36.
 
     rocprofv3 --pmc SQ_WAVE_CYCLES ... -d gpurun_out/pmc -o pmc -- python3 tools/step_pmc.py
+    ... -- python3 tools/step_pmc.py --L 36 --B 65536 --K 50   (config 2's launch: step_small_kernel)
 """
+import argparse
 import os
 import sys
 
@@ -34,6 +36,11 @@ def run(L, B=1 << 20, W=2, K=5, H=200):
 
 
 if __name__ == "__main__":
-    for L in (128, 36):
-        run(L)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=0, help="one L only (default: 128 then 36)")
+    ap.add_argument("--B", type=int, default=1 << 20)
+    ap.add_argument("--K", type=int, default=5)
+    a = ap.parse_args()
+    for L in ((a.L,) if a.L else (128, 36)):
+        run(L, B=a.B, K=a.K)
     print("ok")

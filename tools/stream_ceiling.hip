@@ -38,11 +38,13 @@ __global__ __launch_bounds__(256) void tile_kernel(int4* __restrict__ st, int cp
     const int4* src = st + r0 * cpr + lane;
     const int nch = 64 * cpr / WAVE;  // chunks per lane
     int acc = 0;
+    // every load is guarded by u < nch: at L = 36 a row has 18 chunks, not a multiple of NB (an
+    // unguarded last batch read past the state's end -- the round-5 probe fault, config2_probe.py)
     if (!PIPE) {
         for (int u0 = 0; u0 < nch; u0 += NB) {
             int4 v[NB];
 #pragma unroll
-            for (int u = 0; u < NB; ++u) v[u] = src[(u0 + u) * WAVE];
+            for (int u = 0; u < NB; ++u) v[u] = u0 + u < nch ? src[(u0 + u) * WAVE] : make_int4(0, 0, 0, 0);
 #pragma unroll
             for (int u = 0; u < NB; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
             smem[threadIdx.x] = acc;  // an LDS write per batch, as the tile conversion does
@@ -50,18 +52,18 @@ __global__ __launch_bounds__(256) void tile_kernel(int4* __restrict__ st, int cp
     } else {
         int4 a[NB], b[NB];
 #pragma unroll
-        for (int u = 0; u < NB; ++u) a[u] = src[u * WAVE];
+        for (int u = 0; u < NB; ++u) a[u] = u < nch ? src[u * WAVE] : make_int4(0, 0, 0, 0);
         for (int u0 = 0; u0 < nch; u0 += 2 * NB) {
             if (u0 + NB < nch) {
 #pragma unroll
-                for (int u = 0; u < NB; ++u) b[u] = src[(u0 + NB + u) * WAVE];
+                for (int u = 0; u < NB; ++u) b[u] = u0 + NB + u < nch ? src[(u0 + NB + u) * WAVE] : make_int4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < NB; ++u) acc ^= a[u].x ^ a[u].y ^ a[u].z ^ a[u].w;
             smem[threadIdx.x] = acc;
             if (u0 + 2 * NB < nch) {
 #pragma unroll
-                for (int u = 0; u < NB; ++u) a[u] = src[(u0 + 2 * NB + u) * WAVE];
+                for (int u = 0; u < NB; ++u) a[u] = u0 + 2 * NB + u < nch ? src[(u0 + 2 * NB + u) * WAVE] : make_int4(0, 0, 0, 0);
             }
             if (u0 + NB < nch) {
 #pragma unroll
