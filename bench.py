@@ -395,7 +395,15 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
 
     snap = [t.clone() for t in tensors]
     B = state.shape[0]
-    chg = rd = wr = fin = 0.0
+    chg = rd = wr = fin = srd = swr = 0.0
+    if lens is not None:
+        # byte offset of each relator in the (B, 2L) int32 state: the 64-B sectors its chunks touch
+        rel0 = ((torch.arange(B, device=state.device, dtype=torch.int64) * 2 * L)[:, None]
+                + torch.tensor([0, L], device=state.device, dtype=torch.int64)[None, :]) * 4
+
+        def sectors(chunks):
+            nb = chunks.to(torch.int64) * 16
+            return torch.where(nb > 0, (rel0 + nb - 1) // 64 - rel0 // 64 + 1, torch.zeros_like(nb))
     for t in range(n):
         before = state.clone()
         n_before = lens.clone() if lens is not None else None
@@ -407,12 +415,15 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
             c_new = (lens.clamp(0, L) + 3) // 4
             rd += float(c_old.sum().item()) * 16
             wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16
+            srd += float(sectors(c_old).sum().item()) * 64
+            swr += float(sectors(torch.maximum(c_old, c_new) * ch).sum().item()) * 64
         if finished is not None:
             fin += float((finished[0] | finished[1]).sum().item())
         del before, n_before
     restore(snap, tensors)
     d = max(1, n) * B
-    return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d}
+    return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d,
+            "sector_read": srd / d, "sector_written": swr / d}
 
 
 def learner_buffers(lenv) -> list:
@@ -815,10 +826,14 @@ def run_rank(args):
                 "roofline": {"bound": "hbm", "achieved": a_len, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
                              "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
+                             "sector_bytes_per_env_step": rp["sector_read"] + rp["sector_written"] + 16 + 27,
                              "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
                                            "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
                                            "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
-                                           "relator's last live chunk brings its sector's dead ones"},
+                                           "relator's last live chunk brings its sector's dead ones (sector_bytes: the "
+                                           "same walk rounded to the 64-B sectors touched; PMC of config 5's command "
+                                           "1.134x the live bytes, writes within 3 %, profiles/r05/"
+                                           "r05_step128_step_variants.json)"},
                 "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
             }
             if not same:  # a lengths-path regression must not publish a headline
@@ -978,7 +993,7 @@ def committed_traffic(B, L, K, launch_bytes):
     """(HBM bytes of the headline launch from the newest committed rocprofv3 PMC profile of this
     workload, where from) or (None, None)"""
     cands = []
-    for tag in ("r04_k20", "r04", "r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h",
+    for tag in ("r05_k20", "r04_k20", "r04", "r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h",
                 "r02_k20", "r02", "r01"):
         prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
@@ -1006,8 +1021,8 @@ def committed_step_traffic(B, L, launch_bytes, kernel):
     measured/algorithmic ratio applied to this launch's algorithmic bytes (the changed-relator
     rate, hence the bytes, vary slightly with the walk); or (None, None)"""
     want = kernel.replace(" ", "")
-    for tag in ("r04w_step128", "r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
-        prof = os.path.join(REPO, "profiles", "r04", f"{tag}_summary.json")
+    for tag in ("r05_step128", "r04w_step128", "r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
+        prof = os.path.join(REPO, "profiles", tag[:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
         with open(prof) as f:
@@ -1018,7 +1033,7 @@ def committed_step_traffic(B, L, launch_bytes, kernel):
         if (pc.get("envs_per_gpu") == B and pc.get("max_relator_length") == L and rec.get("pmc_over_algorithmic")
                 and got == want):
             r = rec["pmc_over_algorithmic"]
-            return (launch_bytes * r, f"profiles/r04/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc "
+            return (launch_bytes * r, f"profiles/{tag[:3]}/{tag}_summary.json: rocprofv3 --pmc FETCH_SIZE (x2) + --pmc "
                                       f"WRITE_SIZE per step launch, measured/algorithmic = {r:.4f}")
     return None, None
 
