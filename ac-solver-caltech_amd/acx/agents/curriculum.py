@@ -89,9 +89,6 @@ class CurriculumRecord:
             if hv[i] == 1:  # round 1 complete: the reference's random draw (training.py:337-348)
                 k = self.draw()
                 env.place(i, k, obs_out=obs_out)
-            elif hv[i] == 2:  # round 1, an initial state the device did not load: placed as it is
-                k = int(dev_idx[i])
-                env.place(i, k, obs_out=obs_out)
             else:
                 k = int(dev_idx[i])
             self.restart(i, k)

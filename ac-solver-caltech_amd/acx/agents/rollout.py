@@ -14,10 +14,9 @@ launch, the curriculum's ranking fused into the step -- per step:
   * the round-1 curriculum (training.py:319-336, 349-352) runs on the device: finished envs
     take the next unprocessed initial state in env order.  Once every initial state has been
     used the reference draws random solved/unsolved states with Python `random` (:337-346);
-    those envs are flagged in `needs_host` and placed by `place()`.  needs_host 2: the next
-    initial state is outside the packed domain and was not loaded on the device (the env reset to
-    its own row, curr_index holds the state to place); 3: the device could not rank the env (a
-    workspace shared by concurrent launches) -- CurriculumRecord.process raises.
+    those envs are flagged in `needs_host` and placed by `place()`.  needs_host 3: the device
+    could not rank the env (a workspace shared by concurrent launches) -- CurriculumRecord.process
+    raises.
 """
 
 from __future__ import annotations

@@ -53,14 +53,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// lane r's pointer p, read by every lane (all 64 lanes must execute it: ds_bpermute)
-__device__ __forceinline__ const int32_t* lane_ptr(const int32_t* p, int r) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, r, WAVE);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), r, WAVE);
-    return reinterpret_cast<const int32_t*>(((uint64_t)hi << 32) | lo);
-}
-
 // int32 letter -> int8; values outside {-2..2} become 0x7F and set `bad`
 __device__ __forceinline__ uint32_t to_i8(int32_t v, bool& bad) {
     const bool ok = (uint32_t)(v + 2) <= 4u;
@@ -481,10 +473,6 @@ struct FastTile {
     // wave-instruction fetches 64 / CPR whole rows (3 at L = 36) with one round trip per group
     __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
         load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
-    }
-    // the same with a per-lane source row: row r comes from lane r's `src` (the learner's resets)
-    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
-        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
     }
     // rp(r): row r's source (called by every lane of the wave: it may read across lanes)
     template <class RowPtr>
@@ -1227,9 +1215,6 @@ struct CodeTile {
     __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
         load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
     }
-    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
-        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
-    }
     template <class RowPtr>
     __device__ __forceinline__ void load_rows_from(RowPtr rp, uint64_t rows, int, int lane) {
         if ((rows >> lane) & 1ull) flags[lane] = 0;
@@ -1679,9 +1664,6 @@ struct GenericTile {
     __device__ __forceinline__ void load_rows(const int32_t* __restrict__ g, uint64_t rows, int R, int lane) {
         load_rows_from([&](int r) { return g + (int64_t)r * twoL; }, rows, R, lane);
     }
-    __device__ __forceinline__ void load_rows_src(const int32_t* src, uint64_t rows, int R, int lane) {
-        load_rows_from([&](int r) { return lane_ptr(src, r); }, rows, R, lane);
-    }
     template <class RowPtr>
     __device__ __forceinline__ void load_rows_from(RowPtr rp, uint64_t rows, int, int lane) {
         if ((rows >> lane) & 1ull) flags[lane] = 0;
@@ -2054,6 +2036,17 @@ __device__ __forceinline__ void copy_row(int32_t* dst, const int32_t* src, int t
     }
 }
 
+__device__ __forceinline__ void copy_row_f32(float* dst, const int32_t* src, int twoL) {
+    if ((twoL & 3) == 0) {
+        for (int k = 0; k < twoL / 4; ++k) {
+            const int4 v = reinterpret_cast<const int4*>(src)[k];
+            reinterpret_cast<float4*>(dst)[k] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
+        }
+    } else {
+        for (int k = 0; k < twoL; ++k) dst[k] = (float)src[k];
+    }
+}
+
 __device__ __forceinline__ uint64_t cur_word(uint32_t seq, uint32_t v) {
     return CUR_SET | ((uint64_t)(seq & CUR_SEQ_MASK) << 32) | v;
 }
@@ -2080,17 +2073,27 @@ struct CurLayout {
     }
 };
 
-// this tile's count, its group arrival, and (tile 0) the base
-__device__ __forceinline__ void cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt) {
-    if (w.lane != 0) return;
+// this tile's count, its group arrival, and (tile 0) the base.  Returns the arrival word before
+// this tile's add (lane 0), for cur_publish_end right after: deferring that to the tile's tail
+// (so the add's return trip overlaps the stores) made the steady-state step slower, 0.217 vs
+// 0.203 ms (r05l vs r05k bench lines), since later tiles then wait longer for the group total
+__device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt) {
+    if (w.lane != 0) return 0;
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     if (t == 0) cur_store(c.base, cur_word(seq, (uint32_t)*a.cur_next));
     cur_store(c.tile + t, cur_word(seq, cnt));
+    return __hip_atomic_fetch_add(c.arrive + g, (1ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the add that completed its group publishes the group's total and clears the arrival word for
+// the next launch
+__device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
+                                                uint64_t old) {
+    if (w.lane != 0) return;
+    const CurLayout c(a);
+    const int64_t t = w.r0 / WAVE, g = t / WAVE;
     const int64_t gsize = (c.tiles - g * WAVE) < WAVE ? (c.tiles - g * WAVE) : WAVE;
-    const uint64_t old = __hip_atomic_fetch_add(c.arrive + g, (1ull << 32) | cnt, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if ((int64_t)(old >> 32) + 1 == gsize) {  // the group is complete: its total, and a clean word
+    if ((int64_t)(old >> 32) + 1 == gsize) {
         cur_store(c.group + g, cur_word(seq, (uint32_t)old + cnt));
         cur_store(c.arrive + g, 0ull);
     }
@@ -2242,39 +2245,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
     }
-    // the curriculum (acx_learner_step, training.py:319-336): a finished env takes initial state
-    // next_index + (finished envs before it); past the table's end (round 1 complete) the host
-    // draws (needs_host = 1)
-    const int32_t* cur_row = nullptr;  // the start row this env takes, or NULL
-    int64_t cur_idx = -1;
+    // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
+    // count now; the ranking itself waits until the tile's stores are issued (the tail below)
+    uint64_t fm = 0;
     if (cur) {
-        const uint64_t fm = __ballot(fin);
-        cur_publish(a, w, cseq, (uint32_t)__popcll(fm));
-        // a tile with finished envs waits for its prefix (their initial states' indices); the
-        // last tile for the total (the new next_index)
-        const uint32_t first = fm ? cur_prefix(a, w, cseq, false) : 0u;
-        if (w.r0 + w.R == a.B) {
-            const uint32_t tot = cur_prefix(a, w, cseq, true);
-            if (w.lane == 0) {
-                // every group is complete: no wave of this launch reads next_index or the sequence
-                // number again -- advance both for the next one
-                if (tot != CUR_FAIL) *a.cur_next = (int32_t)((int64_t)tot < a.n_states ? (int64_t)tot : a.n_states);
-                cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
-            }
-        }
-        if (w.active) {
-            uint8_t nh = 0;
-            if (fin) {
-                if (first == CUR_FAIL) {
-                    nh = 3;
-                } else {
-                    cur_idx = (int64_t)first + __popcll(fm & ((1ull << w.lane) - 1ull));
-                    if (cur_idx < a.n_states) cur_row = a.cur_states + cur_idx * twoL;
-                    else nh = 1;
-                }
-            }
-            a.needs_host[env] = nh;
-        }
+        fm = __ballot(fin);
+        const uint32_t cnt = (uint32_t)__popcll(fm);
+        cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt));
     }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
@@ -2286,29 +2263,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // env's row becomes that row's exact values (copied from reset_state, FB_RESET), its
         // step count 0 and its err ACX_ERR_DOMAIN; from then on it is an out-of-domain row.
         bool rbad = false;
-        if (cur) {
-            // learner: each resetting env loads its own next start row, the curriculum's or its
-            // starting row (per-lane sources, so never the whole-tile reload)
-            tile.load_rows_src(cur_row ? cur_row : a.reset_state + env * twoL, rb, w.R, w.lane);
-            if (reset) rbad = tile.pack(w.lane, p);
-            // a curriculum row outside the packed domain is not taken here: the env resets to its
-            // own starting row and the host places that initial state as it is (needs_host = 2)
-            const uint64_t badc = __ballot(reset && rbad && cur_row != nullptr);
-            if (badc) {
-                if ((badc >> w.lane) & 1ull) {
-                    cur_row = nullptr;
-                    a.needs_host[env] = 2;
-                    a.curr_index[env] = (int32_t)cur_idx;
-                }
-                tile.load_rows(a.reset_state + w.r0 * twoL, badc, w.R, w.lane);
-                if ((badc >> w.lane) & 1ull) rbad = tile.pack(w.lane, p);
-            }
-            if (reset) {
-                if (!rbad) tile.unpack(w.lane, p);
-                dm = 3u;
-            }
-            tile.flag_rows(w.lane, rbad ? FB_RESET : 0u);
-        } else if (__popcll(rb) > RESET_TILE_MIN) {
+        if (__popcll(rb) > RESET_TILE_MIN) {
             // many lanes (a synchronised truncation): one coalesced load of the tile's starting
             // states (per-lane reads of every row cost ~1 ms on a whole-batch truncation step);
             // the other lanes re-stage their state, rows left as loaded copy state_in
@@ -2331,11 +2286,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
         if (reset) cnt = 0;
-    }
-    if (cur && reset && cur_row) {
-        // the env now starts (and later resets) from that initial state (training.py:349-352)
-        a.curr_index[env] = (int32_t)cur_idx;
-        copy_row(const_cast<int32_t*>(a.reset_state) + env * twoL, cur_row, twoL);  // acx_learner_step: writable
     }
     if (w.active) {
         if (a.step_count) st_scalar<NT_SC, int32_t>(a.step_count + env, cnt);
@@ -2371,6 +2321,47 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
+    if (cur) {
+        // The curriculum's tail (training.py:329-336, 349-352).  A finished env was reset to its own
+        // starting row above like any env; now -- every store of the tile issued, so the memory
+        // system stays busy while a tile waits -- a tile with finished envs waits for its prefix
+        // and each finished env with index k = prefix + (finished envs before it in the tile) <
+        // n_states takes initial state k: its state, obs_f32 and reset_state rows are overwritten
+        // with that row as it is (acx_curriculum_assign's copy; a row outside the packed domain
+        // is then reported with err 3 by the next step) and curr_index = k; past the table's end
+        // (round 1 complete) needs_host = 1 and the host draws.  The last tile waits for the total
+        // (the new next_index).
+        const uint32_t first = fm ? cur_prefix(a, w, cseq, false) : 0u;
+        if (w.r0 + w.R == a.B) {
+            const uint32_t tot = cur_prefix(a, w, cseq, true);
+            if (w.lane == 0) {
+                // every group is complete: no wave of this launch reads next_index or the sequence
+                // number again -- advance both for the next one
+                if (tot != CUR_FAIL) *a.cur_next = (int32_t)((int64_t)tot < a.n_states ? (int64_t)tot : a.n_states);
+                cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
+            }
+        }
+        // the tile's own stores of these rows (other lanes, other instructions) complete first
+        if (fm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (w.active) {
+            uint8_t nh = 0;
+            if (fin) {
+                const int64_t k = (int64_t)first + __popcll(fm & ((1ull << w.lane) - 1ull));
+                if (first == CUR_FAIL) {
+                    nh = 3;
+                } else if (k < a.n_states) {
+                    const int32_t* src = a.cur_states + k * twoL;
+                    copy_row(a.state_out + env * twoL, src, twoL);
+                    copy_row(const_cast<int32_t*>(a.reset_state) + env * twoL, src, twoL);  // learner: writable
+                    if (a.obs_f32) copy_row_f32(a.obs_f32 + env * twoL, src, twoL);
+                    a.curr_index[env] = (int32_t)k;
+                } else {
+                    nh = 1;
+                }
+            }
+            a.needs_host[env] = nh;
+        }
+    }
 }
 
 template <int NW, int LC, int VEC, bool LEARN>

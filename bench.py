@@ -925,6 +925,27 @@ def run_rank(args):
                                        "x 4L + per finished env 8L + 8L + 4 (curriculum row in, reset row out, "
                                        "curr_index) + needs_host 1; counted over exactly the timed steps"},
         }
+        # the same with the episodes out of phase (step_count[i] = i mod H, as rollout_desync):
+        # ~B/H envs finish and take their next initial state on every step -- a PPO rollout's
+        # steady state, where the fused curriculum's ranking is on the path of the tiles that
+        # hold finished envs
+        del lenv, lbufs
+        # an initial-state table long enough that round 1 lasts through the replay and the timed steps
+        n_tab = B + 2 * (KL + 1) * (-(-B // H)) + 4096
+        lenv = LearnerEnv(ms_starts(L, n_tab), B, horizon_length=H, device=dev)
+        lenv.vec.step_count.copy_(torch.arange(B, dtype=torch.int32, device=dev) % H)
+        lenv.step(la[0], obs_out=lobs[1], reward_out=lrew[0], done_out=ldone[0])
+        lbufs = learner_buffers(lenv)
+        rp2 = replay_walk(lstep, lenv.state, lbufs, KL, L, finished=(lenv.done, lenv.truncated))
+        _, s_l2, _ = timed(go_learn)
+        lb2 = learner_bytes(L, rp2["changed"], rp2["finished"])
+        variants["learner_step_desync"] = {
+            "value": B * KL / s_l2, "unit": "env-steps/s", "steps": KL, "ms_per_step": s_l2 / KL * 1e3,
+            "roofline": {"bound": "hbm", "achieved": B * lb2 / (s_l2 / KL) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": B * lb2 / (s_l2 / KL) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": lb2,
+                         "changed_relators_per_env_step": rp2["changed"], "finished_per_env_step": rp2["finished"]},
+            "workload": "learner_step with step_count[i] = i mod H: ~B/H finished envs per step take the next "
+                        "initial states (round-1 curriculum) inside the step launch"}
         del lobs, lrew, ldone, lenv, lbufs
 
     if not args.no_config2 and world == 1 and rollout_head:

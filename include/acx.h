@@ -185,16 +185,13 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
 
 /*
  * One PPO env step = acx_step_learner (final_obs NULL) followed by acx_curriculum_assign
- * (training.py:238-241, 319-352), in ONE launch: the step kernel ranks the finished envs in env
- * order itself (a single-pass scan with decoupled look-back over 64-env tiles) and a finished env
- * resets straight to its curriculum state -- state, obs_f32 and reset_state rows, curr_index[env]
- * = k.  Same results as the two calls, except that a curriculum row outside the packed domain
- * (letters other than +-1/+-2, a zero inside a relator) is not loaded: the env resets to its own
- * reset_state row, curr_index[env] = k and needs_host[env] = 2 -- the host places that state as
- * it is (acx.agents.LearnerEnv.place), as acx_curriculum_assign would have copied it.
- * needs_host[env] = 3: the look-back gave up (a predecessor tile not scheduled within ~seconds, or a
- * workspace shared by concurrent launches); the env reset to its own row and was not ranked.
- * done, truncated, reset_state and the curriculum
+ * (training.py:238-241, 319-352), in ONE launch with the same results: the step kernel ranks the
+ * finished envs in env order itself (per-64-env-tile counts and per-group totals in the
+ * workspace) and, after a tile's own stores, a finished env with index k < n_states takes initial
+ * state k -- its state, obs_f32 and reset_state rows become that row as it is, curr_index[env] = k;
+ * past the table's end needs_host[env] = 1.  needs_host[env] = 3: the ranking gave up (an earlier
+ * tile not scheduled within ~seconds, or a workspace shared by concurrent launches); the env kept
+ * its own starting row and was not ranked.  done, truncated, reset_state and the curriculum
  * arguments are required; B < 2^31; workspace = acx_curriculum_workspace(B) int32 words (above).
  */
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
