@@ -26,8 +26,14 @@
 //   commit  -- after the mask all-reduce every rank knows all survivors: a prefix sum over
 //              parents gives each survivor's global id g and the node-budget cut (identical on
 //              all ranks); a second prefix sum over the survivors this rank owns gives their
-//              slots in its store, where they are appended (ascending g) and their table
-//              entries rewritten as node entries.
+//              slots in its store, where they are appended (ascending g).
+// Keys live in an append-only arena of records: the expansion writes a chunk's children straight
+// into it (12 per local parent, seq order), a received child that survives is copied in after
+// them, and a table entry names its record's arena position from the moment it is claimed.  So a
+// node's key is never copied and its entry never rewritten (round 4's commit copied every
+// survivor's key into a compact store and rewrote its entry: 0.63 of the search's 2.5 ms at one
+// rank); the store holds, per node, its arena position.  The arena grows by reallocation between
+// chunks (entries hold positions, not addresses).
 // Owner of a key = (fp * G) >> 32 with fp the high hash bits (table slot = low bits).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -70,16 +76,18 @@ __device__ __forceinline__ void ctl_init(Ctl* c) {
 }
 
 struct Args {
-    uint64_t* lkeys;  // (lcap, kw) owned nodes, ascending global id
+    uint64_t* arena;  // (acap, kw) records: every chunk's expanded children, received survivors
+    int64_t* lapos;   // (lcap) owned nodes, ascending global id: arena position of the key
     int64_t* lgid;    // (lcap) global node id
     int64_t* lpar;    // (lcap) global id of the parent, -1 for the root
     uint8_t* lact;    // (lcap) move id that produced the node
-    uint64_t* ckeys;  // (Pr, 12) keys of the local parents' children, parent-major (seq order)
+    uint64_t* ckeys;  // = arena + abase * kw: (Pr, 12) keys of the local parents' children,
+                      // parent-major (seq order); the chunk's received survivors follow
     uint8_t* cown;    // (Pr, 12) owner of each child, 0xff: parent not in the chunk
     uint16_t* pmin;   // (Pr) min child total per local parent (totals reach 2L = 256)
     uint32_t* sslot;  // (12 P) per chunk seq: table slot its child claimed / joined as the first
                       // occurrence, SEEN if none (a known state, past the end, or not owned here)
-    uint64_t* srf;    // (12 P) per chunk seq: the child's record << 32 | its 32-bit fingerprint
+    uint32_t* srec;   // (12 P) per chunk seq: the child's record (arena position - abase)
     uint8_t* lost;    // (12 P) per chunk seq: a smaller seq of the same state took its entry
     uint32_t* mine;   // (P) this rank's survivors per parent (bits by action)
     uint32_t* bsum;   // (nb) all survivors per block of parents -> exclusive offsets
@@ -92,25 +100,37 @@ struct Args {
     int64_t* look;         // lookup result
     uint32_t* xblk;        // (expand blocks, 2 + world) per-block min child total, parents, owner counts
     uint64_t mask;
-    int64_t head, n_before, need, lcap, nloc, lo, nrecv;
+    int64_t head, n_before, need, lcap, nloc, lo, nrecv, abase;
     int P, Pr, L, kw, cyc, world, rank;
     uint32_t end;
     int end_from_ctl;
 };
 
-// Table entries.  A committed node: (local slot + 1) << 32 | 32-bit fingerprint (bit 63 clear).
-// A child claimed in the running chunk: CHUNK | seq << 40 | record << 16 | 16-bit fingerprint;
-// atomicMin on the whole word keeps the smallest seq -- the reference's first occurrence -- and
-// its record, so a probe compares keys with the entry's own record (no seq -> record map).
-// Records: r < 12 Pr is this rank's own child in ckeys (r = 12 * local parent + action), others
-// are received records r - 12 Pr.  Chunks are <= 2^19 parents: seq < 12 * 2^19 < 2^23, r < 2^24.
-constexpr int SEQ_SHIFT = 40, REC_SHIFT = 16;
+// Table entries: (arena position + 1) << 24 | 24-bit fingerprint, final from the claim on.  An
+// entry at or past the chunk's arena base is a child of the running chunk; a probe that meets
+// an equal child there compares sequence numbers (the record's) and takes the entry with a CAS
+// when it comes first -- the reference's first occurrence -- marking the holder lost.
+// Records of the running chunk: r < 12 Pr is this rank's own child (r = 12 * local parent +
+// action, in the arena already), others are received records r - 12 Pr (read from the receive
+// buffer; the commit copies the survivors among them to arena position abase + r).  Chunks are
+// <= 2^19 parents: seq < 12 * 2^19 < 2^23.
+constexpr int POS_SHIFT = 24;
+constexpr uint64_t FP_MASK = (1ull << POS_SHIFT) - 1;
 constexpr int64_t MAX_CHUNK = 1 << 19;
-__device__ __forceinline__ uint32_t entry_seq(uint64_t v) { return (uint32_t)(v >> SEQ_SHIFT) & 0x7fffffu; }
-__device__ __forceinline__ uint32_t entry_rec(uint64_t v) { return (uint32_t)(v >> REC_SHIFT) & 0xffffffu; }
+constexpr int64_t MAX_ARENA = (1ll << (64 - POS_SHIFT)) - 2;  // positions the entry can name
+__device__ __forceinline__ uint64_t entry_of(int64_t pos, uint64_t h) {
+    return ((uint64_t)(pos + 1) << POS_SHIFT) | ((h >> 32) & FP_MASK);
+}
+__device__ __forceinline__ int64_t entry_pos(uint64_t v) { return (int64_t)(v >> POS_SHIFT) - 1; }
 __device__ __forceinline__ const uint64_t* rec_key(const Args& a, uint32_t r) {
     const uint32_t n_own = 12u * (uint32_t)a.Pr;
     return r < n_own ? a.ckeys + (int64_t)r * a.kw : a.recv + (int64_t)(r - n_own) * (a.kw + 1);
+}
+// the chunk seq of record r (its parent's position in the chunk * 12 + action)
+__device__ __forceinline__ uint32_t rec_seq(const Args& a, uint32_t r) {
+    const uint32_t n_own = 12u * (uint32_t)a.Pr;
+    if (r < n_own) return (uint32_t)(a.lgid[a.lo + r / 12u] - a.head) * 12u + r % 12u;
+    return (uint32_t)a.recv[(int64_t)(r - n_own) * (a.kw + 1) + a.kw];
 }
 
 __device__ __forceinline__ uint32_t owner_of(uint64_t h, int world) {
@@ -149,7 +169,7 @@ __global__ __launch_bounds__(TPB, NW <= 4 ? 6 : 4) void sbfs_expand_kernel(Args 
     PresRegs<NW> pr;
     bool clean = false;
     if (live) {
-        load_key<NW>(a.lkeys + (a.lo + j) * kw, kw, a.L, pr);
+        load_key<NW>(a.arena + a.lapos[a.lo + j] * kw, kw, a.L, pr);
         clean = is_clean<NW>(pr.w0, pr.n0, pr.w1, pr.n1, cyc);
     }
     __syncthreads();
@@ -365,7 +385,7 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
     const uint64_t* kp;
     if (t < n_own) {
         // own children in (parent, action) order: consecutive lanes read consecutive keys and
-        // write consecutive seqs (sslot, srf)
+        // write consecutive seqs (sslot, srec)
         const int j = (int)(t / 12);
         const int act = (int)(t - 12 * (int64_t)j);
         if (a.cown[r] != (uint8_t)a.rank) return;  // another rank's child, or a parent past the chunk
@@ -381,9 +401,9 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
     if (s > end) return;
     const Key<KWM> key = kload<KWM>(kp, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
-    const uint32_t fp = (uint32_t)(h >> 32);
+    const uint64_t fp = (h >> 32) & FP_MASK;
     uint64_t idx = h & a.mask;
-    const uint64_t my = CHUNK | ((uint64_t)s << SEQ_SHIFT) | ((uint64_t)r << REC_SHIFT) | (fp & 0xffffu);
+    const uint64_t my = entry_of(a.abase + r, h);
     uint32_t res = SEEN;
     for (uint64_t it = 0;; ++it) {
         if (it > a.mask) {
@@ -399,22 +419,34 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
             }
             v = old;
         }
-        if (v & CHUNK) {
-            if ((uint32_t)(v & 0xffffu) == (fp & 0xffffu) && keq<KWM>(rec_key(a, entry_rec(v)), key, a.kw)) {
-                const uint64_t old = atomicMin((unsigned long long*)(a.table + idx), (unsigned long long)my);
-                if (old > my) {  // this child is the first occurrence so far: the previous holder lost
-                    a.lost[entry_seq(old)] = 1;
-                    res = (uint32_t)idx;
+        if ((v & FP_MASK) == fp) {
+            const int64_t pos = entry_pos(v);
+            if (pos >= a.abase) {  // a child of this chunk
+                if (keq<KWM>(rec_key(a, (uint32_t)(pos - a.abase)), key, a.kw)) {
+                    // the same state: the smaller seq keeps the entry.  A CAS that fails found
+                    // another equal child's entry (only equal states join this slot): compare again
+                    while (true) {
+                        const uint32_t hs = rec_seq(a, (uint32_t)(entry_pos(v) - a.abase));
+                        if (hs < s) break;  // an earlier occurrence holds it
+                        const uint64_t old = atomicCAS((unsigned long long*)(a.table + idx), (unsigned long long)v,
+                                                       (unsigned long long)my);
+                        if (old == v) {  // the previous holder lost
+                            a.lost[hs] = 1;
+                            res = (uint32_t)idx;
+                            break;
+                        }
+                        v = old;
+                    }
+                    break;
                 }
-                break;
+            } else if (keq<KWM>(a.arena + pos * a.kw, key, a.kw)) {
+                break;  // already a node
             }
-        } else if ((uint32_t)v == fp && keq<KWM>(a.lkeys + (int64_t)((v >> 32) - 1) * a.kw, key, a.kw)) {
-            break;  // already a node
         }
         idx = (idx + 1) & a.mask;
     }
     a.sslot[s] = res;
-    a.srf[s] = (uint64_t)r << 32 | fp;
+    a.srec[s] = (uint32_t)r;
 }
 
 // (3b) this rank's survivors per parent -> mask bits (gmask, all-reduced next; mine, kept):
@@ -487,12 +519,13 @@ __global__ __launch_bounds__(1024) void sbfs_scan_kernel(uint32_t* x, uint32_t* 
 // (4c) global ids, the budget cut, and the appends to this rank's store.  A block's own
 // survivors take consecutive store slots (their global ids ascend with the slot), so each lane
 // stages its survivors in LDS at their block-local rank and the block then writes the slot range
-// cooperatively: keys as one coalesced run, ids / parents / moves as coalesced arrays (the
-// round-1 lane-per-parent loop wrote up to 12 scattered key copies per lane: 129 us per chunk).
+// cooperatively as coalesced arrays (ids, parents, moves, arena positions).  Keys stay where they
+// are (own children) or are copied from the receive buffer into the arena (received survivors);
+// table entries already name them.
 constexpr int CMAX = TPB * 12;  // own survivors a block can stage
 __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
-    __shared__ uint32_t srec[CMAX];  // record of the k-th own survivor (rec_key)
+    __shared__ uint32_t srec[CMAX];  // record of the k-th own survivor
     __shared__ uint32_t sinf[CMAX];  // parent within the block (8 bits) | move (4) | id offset (12)
     const int p = blockIdx.x * TPB + threadIdx.x;
     const uint32_t m = p < a.P ? a.gmask[p] : 0u;
@@ -514,7 +547,7 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
     while (mm) {
         const int act = __builtin_ctz(mm);
         mm &= mm - 1;
-        srec[k] = (uint32_t)(a.srf[(uint32_t)p * 12u + act] >> 32);
+        srec[k] = a.srec[(uint32_t)p * 12u + act];
         sinf[k] = (uint32_t)threadIdx.x << 16 | (uint32_t)act << 12 | (bex + __popc(m & ((1u << act) - 1u)));
         ++k;
     }
@@ -540,18 +573,19 @@ __global__ __launch_bounds__(TPB) void sbfs_commit_kernel(Args a) {
         a.lgid[li] = gid;
         a.lpar[li] = a.head + pp;
         a.lact[li] = (uint8_t)act;
-        const uint32_t sq = (uint32_t)pp * 12u + act;
-        a.table[a.sslot[sq]] = ((uint64_t)(li + 1) << 32) | (uint32_t)a.srf[sq];
+        a.lapos[li] = a.abase + srec[i];
     }
-    // keys: word w of the block's slot range comes from word w % kw of record srec[w / kw]
+    // received survivors' keys into the arena after the chunk's own children: word w of the
+    // block's survivors comes from word w % kw of record srec[w / kw] (own ones: already there)
+    const uint32_t n_own = 12u * (uint32_t)a.Pr;
     for (uint32_t w = threadIdx.x; w < ltot * (uint32_t)a.kw; w += TPB) {
         const uint32_t i = w / (uint32_t)a.kw, c = w - i * (uint32_t)a.kw;
-        const int64_t li = li0 + i;
-        if (g0 + (sinf[i] & 0xfffu) >= keep_below || li >= a.lcap) continue;
-        a.lkeys[li * a.kw + c] = rec_key(a, srec[i])[c];
+        const uint32_t r = srec[i];
+        if (r < n_own) continue;
+        a.arena[(a.abase + r) * a.kw + c] = a.recv[(int64_t)(r - n_own) * (a.kw + 1) + c];
     }
     uint32_t bs;
-    block_excl_scan(stored, sh, bs);  // (its barrier: every read of the block's sslot / srf is done)
+    block_excl_scan(stored, sh, bs);  // (its barrier: every read of the block's sslot / srec is done)
     if (threadIdx.x == 0 && bs) atomicAdd(&a.ctl->stored, bs);
     // the block's seqs back to SEEN / not lost for the next chunk (no per-chunk memset);
     // consecutive threads on consecutive seqs
@@ -662,7 +696,7 @@ __global__ void sbfs_lookup_kernel(Args a, int64_t g) {
     a.look[0] = 0;
     if (lo < a.nloc && a.lgid[lo] == g) {
         PresRegs<NW> pr;
-        load_key<NW>(a.lkeys + lo * a.kw, a.kw, a.L, pr);
+        load_key<NW>(a.arena + a.lapos[lo] * a.kw, a.kw, a.L, pr);
         a.look[0] = 1;
         a.look[1] = a.lpar[lo];
         a.look[2] = a.lact[lo];
@@ -677,13 +711,22 @@ struct RootKey {
 template <int KWM>
 __global__ void sbfs_root_kernel(Args a, RootKey rk) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    for (int k = 0; k < a.kw; ++k) a.lkeys[k] = rk.w[k];  // passed by value: no host copy
-    const Key<KWM> key = kload<KWM>(a.lkeys, a.kw);
+    for (int k = 0; k < a.kw; ++k) a.arena[k] = rk.w[k];  // passed by value: no host copy
+    const Key<KWM> key = kload<KWM>(a.arena, a.kw);
     const uint64_t h = khash<KWM>(key, a.kw);
-    a.table[h & a.mask] = (1ull << 32) | (uint32_t)(h >> 32);
+    a.table[h & a.mask] = entry_of(0, h);
+    a.lapos[0] = 0;
     a.lgid[0] = 0;
     a.lpar[0] = -1;
     a.lact[0] = 0xff;
+}
+
+// the first n stored nodes' keys, ascending id, into out ((n, kw))
+__global__ void sbfs_gather_keys_kernel(Args a, int64_t n, uint64_t* out) {
+    const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (t >= n * a.kw) return;
+    const int64_t i = t / a.kw, c = t - i * a.kw;
+    out[t] = a.arena[a.lapos[i] * a.kw + c];
 }
 
 struct Pub {
@@ -694,6 +737,7 @@ struct Pub {
 struct Shard {
     int dev = 0, L = 0, kw = 0, cyc = 0, rank = 0, world = 1;
     int64_t lcap = 0, pmax = 0, rcap = 0, nloc = 0, lo = 0;
+    int64_t acap = 0, abase = 0;  // arena records allocated / used
     int P = 0, Pr = 0;
     int64_t head = 0, nrecv = 0;
     uint64_t tsize = 0;
@@ -715,7 +759,7 @@ struct Shard {
             (void)hipEventSynchronize(fence);
             (void)hipEventDestroy(fence);
         }
-        void* ptrs[] = {a.lkeys, a.lgid, a.lpar, a.lact, a.ckeys, a.cown, a.pmin, a.sslot, a.srf,
+        void* ptrs[] = {a.arena, a.lapos, a.lgid, a.lpar, a.lact, a.cown, a.pmin, a.sslot, a.srec,
                         a.lost, a.mine, a.bsum, a.lbsum, a.table, a.ctl, a.look, a.xblk};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -814,6 +858,34 @@ static int sync_ctl(Shard* S, hipStream_t st, int reset = 0) {
     return ACX_OK;
 }
 
+// the arena to at least `need` records (doubling): a copy of the used records into a new
+// allocation between chunks; entries hold positions, so nothing else changes
+static int grow_arena(Shard* S, int64_t need, hipStream_t st) {
+    if (need <= S->acap) return ACX_OK;
+    if (need > MAX_ARENA) return ACX_E_ARG;
+    int64_t cap = 2 * S->acap > need ? 2 * S->acap : need;
+    if (cap > MAX_ARENA) cap = MAX_ARENA;
+    uint64_t* p = nullptr;
+    if (!dalloc(p, (size_t)(cap * S->kw))) {
+        (void)hipGetLastError();
+        cap = need;
+        if (!dalloc(p, (size_t)(cap * S->kw))) {
+            (void)hipGetLastError();
+            return ACX_E_LAUNCH;
+        }
+    }
+    if ((S->abase > 0 &&
+         hipMemcpyAsync(p, S->a.arena, (size_t)(S->abase * S->kw) * 8, hipMemcpyDeviceToDevice, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess) {  // the old arena's readers are done too
+        (void)hipFree(p);
+        return ACX_E_LAUNCH;
+    }
+    (void)hipFree(S->a.arena);
+    S->a.arena = p;
+    S->acap = cap;
+    return ACX_OK;
+}
+
 }  // namespace sbfs
 }  // namespace acx
 
@@ -835,7 +907,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     S->world = world;
     S->lcap = local_cap;
     if (chunk_parents <= 0) chunk_parents = MAX_CHUNK;  // tools/bfs_chunk_probe.py: 2^19-2^20 fastest
-    if (chunk_parents > MAX_CHUNK) { delete S; return nullptr; }  // the chunk entry's seq / record fields
+    if (chunk_parents > MAX_CHUNK) { delete S; return nullptr; }  // seqs < 12 * 2^19 (the per-seq arrays)
     S->pmax = chunk_parents;
     S->rcap = 12 * S->pmax;  // every child of a chunk may have this owner
     uint64_t ts = 1024;
@@ -845,11 +917,16 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     Args& a = S->a;
     const int64_t nb = nblocks(S->pmax);
     const int64_t pl = S->pmax < S->lcap ? S->pmax : S->lcap;  // local parents per chunk
-    bool ok = dalloc(a.lkeys, (size_t)(S->lcap * S->kw)) && dalloc(a.lgid, (size_t)S->lcap) &&
-              dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
-              dalloc(a.ckeys, (size_t)(12 * pl * S->kw)) && dalloc(a.cown, (size_t)(12 * pl)) &&
+    // the arena's first size: 12 records per expanded parent, which is ~2 per node in an AK(n)
+    // search (BASELINE config 4: 1.59M parents for 10^7 nodes), plus received records at G > 1,
+    // and room for one full chunk; it doubles when a chunk would not fit (grow_arena)
+    S->acap = 1 + 3 * S->lcap + 24 * pl;
+    if (S->acap > MAX_ARENA) S->acap = MAX_ARENA;
+    bool ok = dalloc(a.arena, (size_t)(S->acap * S->kw)) && dalloc(a.lapos, (size_t)S->lcap) &&
+              dalloc(a.lgid, (size_t)S->lcap) && dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
+              dalloc(a.cown, (size_t)(12 * pl)) &&
               dalloc(a.pmin, (size_t)pl) && dalloc(a.sslot, (size_t)(12 * S->pmax)) &&
-              dalloc(a.srf, (size_t)(12 * S->pmax)) && dalloc(a.lost, (size_t)(12 * S->pmax)) &&
+              dalloc(a.srec, (size_t)(12 * S->pmax)) && dalloc(a.lost, (size_t)(12 * S->pmax)) &&
               dalloc(a.mine, (size_t)S->pmax) &&
               dalloc(a.bsum, (size_t)nb) && dalloc(a.lbsum, (size_t)nb) && dalloc(a.table, (size_t)ts) &&
               dalloc(a.ctl, 1) && dalloc(a.look, 4) &&
@@ -902,6 +979,7 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
     if (own < 0) return own;
     S->nloc = 0;
     S->lo = 0;
+    S->abase = 0;
     S->a.nloc = 0;
     if (hipMemsetAsync(S->a.table, 0, S->tsize * 8, st) != hipSuccess) return ACX_E_LAUNCH;
     // the per-seq arrays are clean between chunks (each commit resets what its chunk used); a
@@ -915,6 +993,7 @@ int acx_sbfs_reset(void* h, const int32_t* presentation, void* stream) {
         pack_key(presentation, S->L, S->kw, rl.rk.w);
         by_nw(S->L, rl);
         S->nloc = 1;
+        S->abase = 1;  // the root's record
     }
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return ACX_E_LAUNCH;
     return own;
@@ -936,6 +1015,11 @@ int acx_sbfs_expand(void* h, int64_t head, int32_t P, int64_t* out, int32_t read
     a.Pr = S->Pr;
     a.lo = S->lo;
     a.nloc = S->nloc;
+    // the chunk's records: its own children, then (G > 1) up to rcap received ones
+    const int r0 = grow_arena(S, S->abase + 12 * (int64_t)S->Pr + (S->world > 1 ? S->rcap : 0), st);
+    if (r0 != ACX_OK) return r0;
+    a.abase = S->abase;
+    a.ckeys = a.arena + S->abase * S->kw;
     // the control block holds its initial values (the search's reset, or the previous chunk's
     // commit read-back re-initialised it)
     if (S->Pr > 0) {
@@ -975,6 +1059,7 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
     Shard* S = static_cast<Shard*>(h);
     if (S && S->stalled) return ACX_E_LAUNCH;  // see Shard::fence
     if (!S || !gmask || nrecv < 0 || nrecv > S->rcap || (nrecv > 0 && !recv)) return ACX_E_ARG;
+    if (S->abase + 12 * (int64_t)S->Pr + nrecv > S->acap) return ACX_E_ARG;  // reserved by acx_sbfs_expand
     hipStream_t st = (hipStream_t)stream;
     Args& a = S->a;
     a.recv = recv;
@@ -1023,6 +1108,7 @@ int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t ne
     out[8] = c.npar;
     S->nloc += c.stored;
     S->lo += c.npar;
+    S->abase += 12 * (int64_t)S->Pr + S->nrecv;  // the chunk's records stay (entries name them)
     S->chunk_npar = (int)c.npar;
     return ACX_OK;
 }
@@ -1097,8 +1183,19 @@ int64_t acx_sbfs_node_keys(void* h, uint64_t* keys, int64_t* gids, int64_t cap, 
     if (!S) return ACX_E_ARG;
     const int64_t n = S->nloc < cap ? S->nloc : cap;
     hipStream_t st = (hipStream_t)stream;
-    if (n > 0 && keys && copy_to_host(keys, S->a.lkeys, (size_t)(n * S->kw) * 8, st, &S->bounce) != ACX_OK)
-        return ACX_E_LAUNCH;
+    if (n > 0 && keys) {
+        uint64_t* d = nullptr;
+        if (!dalloc(d, (size_t)(n * S->kw))) {
+            (void)hipGetLastError();
+            return ACX_E_LAUNCH;
+        }
+        Args a = S->a;
+        sbfs_gather_keys_kernel<<<dim3(nblocks(n * S->kw)), dim3(TPB), 0, st>>>(a, n, d);
+        const int r = hipGetLastError() == hipSuccess ? copy_to_host(keys, d, (size_t)(n * S->kw) * 8, st, &S->bounce)
+                                                      : ACX_E_LAUNCH;
+        (void)hipFree(d);
+        if (r != ACX_OK) return ACX_E_LAUNCH;
+    }
     if (n > 0 && gids && copy_to_host(gids, S->a.lgid, (size_t)n * 8, st, &S->bounce) != ACX_OK)
         return ACX_E_LAUNCH;
     return S->nloc;

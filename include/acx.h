@@ -340,7 +340,9 @@ int64_t acx_bfs_min_trace(void* h, int32_t* out, int64_t cap);
  * (acx/search/_sharded_bfs.py) and does the exchanges between the calls:
  *   acx_sbfs_create    workspace on the current device: this rank's node store (local_cap
  *                      nodes), chunks of <= chunk_parents parents (<= 0 or the maximum: 2^19);
- *                      NULL on failure
+ *                      NULL on failure.  Keys live in an arena of expanded children that
+ *                      acx_sbfs_expand grows by doubling when a chunk would not fit (a failed
+ *                      allocation there returns ACX_E_LAUNCH)
  *   acx_sbfs_owner     owner rank of a presentation's key (HOST pointer)
  *   acx_sbfs_reset     new search from `presentation` (HOST); returns the root's owner rank
  *   acx_sbfs_expand    expands this rank's parents among global ids [head, head + P);
