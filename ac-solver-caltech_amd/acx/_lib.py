@@ -28,12 +28,14 @@ _I64 = ctypes.c_int64
 SIGNATURES = {
     "acx_step": ([_P] * 12 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_step_lengths": ([_P] * 11 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
-    "acx_step_learner": ([_P] * 11 + [_I32, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
-    "acx_step_record": ([_P] * 11 + [_I32] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
-    "acx_step_next": ([_P] * 11 + [_I32] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    # ..., action_hist, hist_cap, hist_base, hist_t, episode_len, ...
+    "acx_step_learner": ([_P] * 11 + [_I32, _P, _I64, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_step_record": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_step_next": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_curriculum_workspace": ([_I64], ctypes.c_int64),
     "acx_curriculum_assign": ([_P, _P, _P, _I64] + [_P] * 7 + [_I64, _I32, _P], ctypes.c_int),
-    "acx_learner_step": ([_P] * 11 + [_I32] + [_P] * 4 + [_I64] + [_P] * 4 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_learner_step": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 4 + [_I64] + [_P] * 4 + [_I64, _I32, _I32, _I32, _P],
+                         ctypes.c_int),
     "acx_rollout": ([_P] * 10 + [_I32, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_packed_actions_words": ([_I32, _I64], ctypes.c_int64),
     "acx_pack_actions": ([_P, _P, _I32, _I64, _P], ctypes.c_int),

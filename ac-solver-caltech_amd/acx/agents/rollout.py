@@ -50,8 +50,11 @@ class LearnerEnv:
         self.next_index = torch.tensor([num_envs], dtype=torch.int32, device=dev)  # max(states_processed) + 1
         self.needs_host = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self.hist_cap = int(hist_cap if hist_cap is not None else horizon_length)
-        # move k of env i at [k, i] (step-major: coalesced writes, acx.h)
+        # move k of env i's episode at [(hist_base[i] + k) mod hist_cap, i]: a ring, step-major, so
+        # every env writes a step's move to one row however far apart the episodes are (acx.h)
         self.action_hist = torch.zeros((self.hist_cap, num_envs), dtype=torch.uint8, device=dev)
+        self.hist_base = torch.zeros(num_envs, dtype=torch.int32, device=dev)
+        self.hist_t = 0  # steps taken: the ring row of this step's moves
         self.episode_len = torch.zeros(num_envs, dtype=torch.int32, device=dev)
         self.done = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
@@ -98,18 +101,21 @@ class LearnerEnv:
             st = lib.acx_learner_step(
                 v.state.data_ptr(), ptr(a32), ptr(a64), v.reset_state.data_ptr(), v.step_count.data_ptr(),
                 ptr(obs_out), ptr(reward_out), ptr(done_out), self.done.data_ptr(), self.truncated.data_ptr(),
-                self.action_hist.data_ptr(), self.hist_cap, self.episode_len.data_ptr(), v.err.data_ptr(),
-                v.err_count.data_ptr(), self.initial_states.data_ptr(), self.n_states, self.next_index.data_ptr(),
-                self.curr_index.data_ptr(), self.needs_host.data_ptr(), self._ws.data_ptr(), B, L,
-                self.horizon_length, int(v.cyclical), stream)
+                self.action_hist.data_ptr(), self.hist_cap, self.hist_base.data_ptr(), self.hist_t,
+                self.episode_len.data_ptr(), v.err.data_ptr(), v.err_count.data_ptr(), self.initial_states.data_ptr(),
+                self.n_states, self.next_index.data_ptr(), self.curr_index.data_ptr(), self.needs_host.data_ptr(),
+                self._ws.data_ptr(), B, L, self.horizon_length, int(v.cyclical), stream)
             _lib.check(st, "acx_learner_step")
+            self.hist_t += 1
             return self.done, self.truncated, self.episode_len, self.needs_host
         st = lib.acx_step_learner(
             v.state.data_ptr(), ptr(a32), ptr(a64), v.reset_state.data_ptr(), v.step_count.data_ptr(), ptr(obs_out),
             ptr(reward_out), ptr(done_out), self.done.data_ptr(), self.truncated.data_ptr(),
-            self.action_hist.data_ptr(), self.hist_cap, self.episode_len.data_ptr(), None, v.err.data_ptr(),
-            v.err_count.data_ptr(), B, L, self.horizon_length, int(v.cyclical), stream)
+            self.action_hist.data_ptr(), self.hist_cap, self.hist_base.data_ptr(), self.hist_t,
+            self.episode_len.data_ptr(), None, v.err.data_ptr(), v.err_count.data_ptr(), B, L, self.horizon_length,
+            int(v.cyclical), stream)
         _lib.check(st, "acx_step_learner")
+        self.hist_t += 1
         st = lib.acx_curriculum_assign(
             self.done.data_ptr(), self.truncated.data_ptr(), self.initial_states.data_ptr(), self.n_states,
             self.next_index.data_ptr(), self.curr_index.data_ptr(), self.needs_host.data_ptr(), v.state.data_ptr(),
@@ -119,10 +125,7 @@ class LearnerEnv:
 
     def episode_actions(self, i: int) -> list:
         """info["actions"] of env i's episode that ended at the last step (training.py:275-280)."""
-        n = int(self.episode_len[i].item())
-        if n > self.hist_cap:
-            raise ValueError(f"episode of {n} moves exceeds hist_cap {self.hist_cap}")
-        return [int(x) for x in self.action_hist[:n, i].cpu().numpy()]
+        return self.episode_actions_many([i])[int(i)]
 
     def episode_actions_many(self, envs) -> dict:
         """{i: info["actions"]} for the envs `envs` (host ints) whose episodes ended at the last
@@ -136,7 +139,9 @@ class LearnerEnv:
         n_max = int(lens.max())
         if n_max > self.hist_cap:
             raise ValueError(f"episode of {n_max} moves exceeds hist_cap {self.hist_cap}")
-        cols = self.action_hist[:n_max, idx].cpu().numpy()
+        rows = (self.hist_base[idx].to(torch.int64)[None, :] +
+                torch.arange(n_max, dtype=torch.int64, device=idx.device)[:, None]) % self.hist_cap
+        cols = self.action_hist[rows, idx[None, :]].cpu().numpy()  # (n_max, len(envs))
         return {i: [int(x) for x in cols[: int(lens[j]), j]] for j, i in enumerate(envs)}
 
     def place(self, i: int, state_index: int, obs_out: Optional[torch.Tensor] = None) -> None:

@@ -276,8 +276,12 @@ class VecACEnv:
         self.record_actions = bool(record_actions)
         self.info_format = info_format
         if self.record_actions:
-            # move k of env i's current episode at [k, i]; an episode never outlives the horizon
+            # move k of env i's current episode at [(hist_base[i] + k) mod H, i] (a ring, step-major:
+            # a step's moves go to one row however far apart the episodes are, acx.h); an episode
+            # never outlives the horizon
             self.action_hist = torch.zeros((max(1, self.horizon_length), B), dtype=torch.uint8, device=dev)
+            self.hist_base = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.hist_t = 0  # steps taken: the ring row of this step's moves
             self.episode_len = torch.zeros(B, dtype=torch.int32, device=dev)
         self.action_space = Discrete(12)
         self.single_observation_space = Box(np.full(2 * L, -2, np.int8), np.full(2 * L, 2, np.int8))
@@ -338,6 +342,7 @@ class VecACEnv:
             st = self._lib.acx_step_next(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln,
                                          self.pending.data_ptr(), self.action_hist.data_ptr() if rec else None,
                                          self.action_hist.shape[0] if rec else 0,
+                                         self.hist_base.data_ptr() if rec else None, self.hist_t if rec else 0,
                                          self.episode_len.data_ptr() if rec else None, err, ec, self.num_envs,
                                          self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
             _lib.check(st, "acx_step_next")
@@ -350,7 +355,8 @@ class VecACEnv:
         elif self.record_actions:
             st = self._lib.acx_step_record(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo,
                                            self.action_hist.data_ptr(), self.action_hist.shape[0],
-                                           self.episode_len.data_ptr(), err, ec, self.num_envs,
+                                           self.hist_base.data_ptr(), self.hist_t, self.episode_len.data_ptr(),
+                                           err, ec, self.num_envs,
                                            self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
             _lib.check(st, "acx_step_record")
         else:
@@ -359,6 +365,8 @@ class VecACEnv:
                                     stream)
             _lib.check(st, "acx_step")
         self._lengths_ok = True  # every step kernel writes the rows' lengths
+        if self.record_actions:
+            self.hist_t += 1
         if self.check_errors:
             self.raise_if_errors()
         info = {"final_observation": self.final_obs} if self.final_obs is not None else {}
@@ -379,7 +387,10 @@ class VecACEnv:
         if solved.size:
             idx = torch.as_tensor(solved, device=self.device)
             lens = self.episode_len[idx].cpu().numpy()
-            cols = self.action_hist[: int(lens.max()), idx].cpu().numpy()  # (max_len, n_solved)
+            n_max = int(lens.max())
+            rows = (self.hist_base[idx].to(torch.int64)[None, :] +
+                    torch.arange(n_max, dtype=torch.int64, device=self.device)[:, None]) % self.action_hist.shape[0]
+            cols = self.action_hist[rows, idx[None, :]].cpu().numpy()  # (max_len, n_solved)
             lists = {int(i): [int(a) for a in cols[: lens[k], k]] for k, i in enumerate(solved)}
         if self.info_format == "final_info":
             final_info = np.full(B, None, dtype=object)

@@ -504,6 +504,39 @@ struct FastTile {
         wave_sync();
     }
 
+    // load_rows in two halves, for rows known before they are needed (an env step's truncations:
+    // step_count + 1 >= horizon before the move): fetch_rows issues the loads of the rows in the
+    // wave-uniform mask `rows` (at most RPI of them: one wave-instruction) and returns each lane's
+    // chunk; put_rows later writes the rows in `apply` (a subset) into the tile, as load_rows does
+    static constexpr bool PREFETCH_OK = true;
+    static constexpr int RPI = WAVE / CPR;  // rows per wave-instruction
+    __device__ __forceinline__ int4 fetch_rows(const int32_t* __restrict__ g, uint64_t rows, int lane) const {
+        const int s = lane / CPR, c = lane - s * CPR;
+        uint64_t m = rows;
+        for (int i = 0; i < (s < RPI ? s : 0); ++i) m &= m - 1;
+        int4 v = {0, 0, 0, 0};
+        if (s < RPI && m) v = reinterpret_cast<const int4*>(g + (int64_t)__builtin_ctzll(m) * twoL)[c];
+        return v;
+    }
+    __device__ __forceinline__ void put_rows(const int4& v, uint64_t rows, uint64_t apply, int lane) {
+        const int s = lane / CPR, c = lane - s * CPR;
+        uint64_t m = rows;
+        for (int i = 0; i < (s < RPI ? s : 0); ++i) m &= m - 1;
+        if ((apply >> lane) & 1ull) flags[lane] = 0;
+        wave_sync();
+        bool bad = false;
+        if (s < RPI && m) {
+            const int r = __builtin_ctzll(m);
+            if ((apply >> r) & 1ull) {
+                lds[r * S + c] = to_i8(v.x, bad) | (to_i8(v.y, bad) << 8) | (to_i8(v.z, bad) << 16) |
+                                 (to_i8(v.w, bad) << 24);
+                if (bad) flags[r] = 1;
+            }
+        }
+        tile_bad = tile_bad || __any(bad);
+        wave_sync();
+    }
+
     template <bool NT, bool F32, bool FULL, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_flat(int4* dst, int ln, int nc) const {
 #pragma unroll
@@ -937,6 +970,10 @@ struct CodeTile {
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
+    static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
+    static constexpr int RPI = 1;
+    __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
+    __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
     static constexpr bool NT_STEP_LOADS = true;  // see ld_tile
     __device__ __forceinline__ void restore_flags(int lane, uint32_t code) {
         flags[lane] = (uint8_t)code;
@@ -1622,6 +1659,10 @@ struct CodeTile {
 template <int NW, int LC, int VEC>
 struct GenericTile {
     static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
+    static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
+    static constexpr int RPI = 1;
+    __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
+    __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
     static constexpr bool NT_STEP_LOADS = false;  // see ld_tile
     static constexpr int LMAX = LC > 0 ? LC : 16 * NW;
     int L, twoL, rowb;
@@ -1995,6 +2036,12 @@ struct StepArgs {
     // lengths-carrying step (acx_step_lengths): lengths_out holds the rows' relator lengths on
     // entry (canonical rows), so only their letters are read and written
     int live;
+    // move-history ring (NULL: move k of an episode at row k): per env, the row of its current
+    // episode's move 0; an episode's first move sets it to hist_t mod hist_cap (hist_t: the
+    // caller's step counter), so envs whose episodes are out of phase still write this step's
+    // moves to one row -- coalesced -- instead of one cache line per lane
+    int32_t* hist_base;
+    int64_t hist_t;
 };
 
 // ---------------------------------------------------------------------------------
@@ -2174,6 +2221,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         cnt_in = a.step_count ? a.step_count[env] : 0;
     }
 #endif
+    int hb = 0;  // the move-history ring's row of this env's episode move 0
+    if (LEARN && w.active && a.hist_base) hb = a.hist_base[env];
     if constexpr (LIVE) {
         int n_in0 = 0, n_in1 = 0;  // the rows' relator lengths on entry
         if (w.active) {
@@ -2187,6 +2236,22 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         tile.template load<ACX_PIPE_LOAD != 0, false, Tile::NT_STEP_LOADS, BATCH>(a.state_in + w.r0 * twoL, w.R, w.lane);
     }
 
+    // Truncations are known before the move (step_count + 1 >= horizon, unless the move fails):
+    // their starting rows are fetched now, under the pack and the move, and put into the tile
+    // before this step's stores -- loaded after the move instead, behind those stores, they were
+    // a second dependent round trip that doubled the life of every wave holding one (a learner
+    // step with episodes out of phase, ~B/H truncations per step: +44 us on a 124 us step)
+    constexpr bool PREF = !LIVE && Tile::PREFETCH_OK && ACX_EARLY_SCALARS != 0;
+    uint64_t pre = 0;  // wave-uniform: the rows fetched
+    int4 pv = {0, 0, 0, 0};
+    if constexpr (PREF) {
+        if (a.reset_state && a.step_count && !a.pending) {  // kernel arguments: uniform
+            pre = __ballot(w.active && cnt_in + 1 >= a.horizon);
+            if (__popcll(pre) > Tile::RPI) pre = 0;  // more (a synchronised truncation): the tile reload below
+            if (pre) pv = tile.fetch_rows(a.reset_state + w.r0 * twoL, pre, w.lane);
+        }
+    }
+
     bool fin = false;    // done | truncated (the curriculum's "finished")
     bool reset = false;  // same-step autoreset of this env
     bool keep = false;   // the env's row is left as loaded (out of domain, or its move failed)
@@ -2194,8 +2259,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     PlaneRegs<PW> p;
     int cnt0 = 0, cnt = 0, e = ACX_ERR_NONE;
     uint32_t dm = 0;     // relators of the row that differ from state_in (in-place store)
+    int act = 0;
+    bool triv = false, trunc = false;
+    int32_t rwd = 0;
     if (w.active) {
-        int act = act_in;
+        act = act_in;
 #if !ACX_EARLY_SCALARS
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
             const int64_t v = a.action64[env];
@@ -2207,11 +2275,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
 #endif
         cnt0 = cnt_in;
         cnt = a.step_count ? cnt0 + 1 : 0;
-        // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
-        // at [k][i] -- envs at the same episode position write one coalesced row segment (an
-        // (env, k) layout made every lane's byte its own cache line: 90 us of a 300 us step)
-        if (LEARN && a.action_hist && !pend && cnt - 1 < a.hist_cap)
-            a.action_hist[(int64_t)(cnt - 1) * a.B + env] = (uint8_t)act;
         const bool bad = tile.template pack<LIVE>(w.lane, p);
         const bool cyc = a.cyclical != 0;
         if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
@@ -2225,22 +2288,43 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
         if (!keep) dm = tile.template unpack_dirty<LIVE>(w.lane, p);
-        const bool triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
-        const bool trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
+        triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
+        trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
         // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does
-        const int32_t rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        fin = triv || trunc;
+        // same-step autoreset: an env that ends resets now; next-step: a pending env resets now and
+        // an env that ends is reset by the next call
+        reset = a.pending ? pend : (fin && a.reset_state && !keep);
+    }
+    if constexpr (PREF) {
+        if (pre) tile.put_rows(pv, pre, pre & __ballot(reset), w.lane);
+    }
+    if (w.active) {
+        // info["actions"] (ac_env.py:96,105): the episode's moves, one byte each, move k of env i
+        // at row k, or with the ring at row (hist_base[i] + k) mod hist_cap -- envs at the same
+        // episode position (ring: every env whose episode had no failed move) write one
+        // coalesced row segment (an (env, k) layout made every lane's byte its own cache line:
+        // 90 us of a 300 us step; (k, env) with episodes out of phase, 26 us of a 196 us one)
+        if (LEARN && a.action_hist && !pend && cnt0 < a.hist_cap) {
+            int row = cnt0;
+            if (a.hist_base) {
+                if (cnt0 == 0) {
+                    hb = (int)(a.hist_t % a.hist_cap);
+                    a.hist_base[env] = hb;
+                }
+                row = hb + cnt0 < a.hist_cap ? hb + cnt0 : hb + cnt0 - a.hist_cap;
+            }
+            a.action_hist[(int64_t)row * a.B + env] = (uint8_t)act;
+        }
         if (a.reward) st_scalar<NT_SC, int32_t>(a.reward + env, rwd);
         if (a.done) st_scalar<NT_SC, uint8_t>(a.done + env, (uint8_t)triv);
         if (a.truncated) st_scalar<NT_SC, uint8_t>(a.truncated + env, (uint8_t)trunc);
-        fin = triv || trunc;
         if constexpr (LEARN) {
             if (a.reward_f32) a.reward_f32[env] = (float)rwd;
             if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
             if (a.episode_len) a.episode_len[env] = (triv || trunc) ? cnt : 0;
         }
-        // same-step autoreset: an env that ends resets now; next-step: a pending env resets now and
-        // an env that ends is reset by the next call
-        reset = a.pending ? pend : (fin && a.reset_state && !keep);
         if (a.pending) a.pending[env] = fin ? 1 : 0;
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
@@ -2275,8 +2359,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             dm = (w.active && !keep) ? 3u : 0u;  // the tile now holds starting rows: write every kept-moving row
             tile.restore_flags(w.lane, (w.active && keep) ? FB_IN : (rbad ? FB_RESET : 0u));
         } else {
-            // a few lanes: the wave loads just their rows (scattered resets cost their rows only)
-            tile.load_rows(a.reset_state + w.r0 * twoL, rb, w.R, w.lane);
+            // a few lanes: the wave loads just their rows (scattered resets cost their rows only),
+            // those it has not fetched before the move
+            const uint64_t late = rb & ~pre;
+            if (late) tile.load_rows(a.reset_state + w.r0 * twoL, late, w.R, w.lane);
             if (reset) {
                 rbad = tile.pack(w.lane, p);
                 if (!rbad) tile.unpack(w.lane, p);
@@ -3434,9 +3520,10 @@ int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset
 
 int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
                   int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
-                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                  int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream) {
-    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                  int32_t* episode_len, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                  int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || hist_t < 0 || (hist_base && !action_hist)) return ACX_E_ARG;
     if (B == 0) return ACX_OK;
     if (!state_in || !state_out || !action || !reset_state || !step_count || !pending) return ACX_E_ARG;
     if ((action_hist != nullptr) != (hist_cap > 0) || (episode_len && !action_hist)) return ACX_E_ARG;
@@ -3445,6 +3532,8 @@ int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* ac
                err, err_count, nullptr, nullptr, nullptr, nullptr, action_hist, episode_len, B, L, horizon, cyclical,
                hist_cap};
     a.pending = pending;
+    a.hist_base = hist_base;
+    a.hist_t = hist_t;
     // with a move history: the learner instantiation (it compiles the history writes)
     StepLaunch f{a, (hipStream_t)stream, action_hist != nullptr};
     return dispatch(L, f);
@@ -3452,25 +3541,28 @@ int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* ac
 
 int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* action_i64, const int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
-                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len,
-                     int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
-                     int32_t cyclical, void* stream) {
-    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                     int32_t* episode_len, int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L,
+                     int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || hist_t < 0 || (hist_base && !action_hist)) return ACX_E_ARG;
     if (B == 0) return ACX_OK;
     if (!state || !step_count || (!action == !action_i64) || (action_hist && hist_cap == 0)) return ACX_E_ARG;
     if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
     StepArgs a{state, state, action, reset_state, step_count, nullptr, done, truncated, nullptr, final_obs, err,
                err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
                cyclical, hist_cap};
+    a.hist_base = hist_base;
+    a.hist_t = hist_t;
     StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
 }
 
 int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
                     int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
-                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                    int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream) {
-    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0) return ACX_E_ARG;
+                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                    int32_t* episode_len, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                    int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || hist_t < 0) return ACX_E_ARG;
     if (B == 0) return ACX_OK;
     if (!state_in || !state_out || !action || !step_count || !action_hist || hist_cap == 0) return ACX_E_ARG;
     if (!aligned16(state_in) || !aligned16(state_out)) return ACX_E_ARG;
@@ -3478,6 +3570,8 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
     StepArgs a{state_in, state_out, action, reset_state, step_count, reward, done, truncated, lengths_out, final_obs,
                err, err_count, nullptr, nullptr, nullptr, nullptr, action_hist, episode_len, B, L, horizon, cyclical,
                hist_cap};
+    a.hist_base = hist_base;
+    a.hist_t = hist_t;
     StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
 }
@@ -3487,11 +3581,12 @@ int64_t acx_internal_curriculum_fused_offset(int64_t B);
 
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
-                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                     int32_t* err_count, const int32_t* curriculum_states, int64_t n_states, int32_t* next_index,
-                     int32_t* curr_index, uint8_t* needs_host, int32_t* workspace, int64_t B, int32_t L,
-                     int32_t horizon, int32_t cyclical, void* stream) {
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                     int32_t* episode_len, uint8_t* err, int32_t* err_count, const int32_t* curriculum_states,
+                     int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
+                     int32_t* workspace, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream) {
     if (B < 0 || L < 1 || L > ACX_MAX_L || hist_cap < 0 || n_states < 0 || n_states > INT32_MAX) return ACX_E_ARG;
+    if (hist_t < 0 || (hist_base && !action_hist)) return ACX_E_ARG;
     if (B >= (1ll << 31)) return ACX_E_ARG;  // the look-back's 32-bit prefixes (next_index + finished envs)
     if (B == 0) return ACX_OK;
     if (!state || !step_count || (!action == !action_i64) || (action_hist && hist_cap == 0)) return ACX_E_ARG;
@@ -3507,6 +3602,8 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
                err_count, action_i64, obs_f32, reward_f32, done_f32, action_hist, episode_len, B, L, horizon,
                cyclical, hist_cap, reinterpret_cast<uint64_t*>(ws), curriculum_states, n_states, next_index,
                curr_index, needs_host};
+    a.hist_base = hist_base;
+    a.hist_t = hist_t;
     StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
 }

@@ -442,10 +442,11 @@ def learner_buffers(lenv) -> list:
 def learner_bytes(L: int, changed: float, finished: float) -> float:
     """algorithmic bytes per env-step of acx_learner_step (one launch, curriculum fused): state
     read 8L, obs float32 8L, action int64 8, step count in/out 8, reward / done float32 8,
-    done / truncated 2, move history 1, episode length 4, err 1, needs_host 1; changed relators
-    x 4L written in place; per finished env its next start row read 8L (curriculum or reset
-    row), its reset row written 8L and curr_index 4"""
-    return 16 * L + 33 + 4 * L * changed + finished * (16 * L + 4)
+    done / truncated 2, move history 1 + its ring base read 4, episode length 4, err 1,
+    needs_host 1; changed relators x 4L written in place; per finished env its next start row
+    read 8L (curriculum or reset row), its reset row written 8L, curr_index 4 and the ring base of
+    its next episode 4"""
+    return 16 * L + 37 + 4 * L * changed + finished * (16 * L + 8)
 
 
 def dry_run(args, rank: int, local_rank: int, world: int) -> None:
@@ -921,9 +922,10 @@ def run_rank(args):
                          "changed_relators_per_env_step": rp["changed"], "finished_per_env_step": rp["finished"],
                          "kernel": f"acx::step_kernel<{nw_for(L)},{L if L in (36, 128) else 0},4,true> "
                                    "(curriculum fused, one launch)",
-                         "bytes_note": "16L state read + obs f32 write + 32 B of per-env scalars + changed relators "
-                                       "x 4L + per finished env 8L + 8L + 4 (curriculum row in, reset row out, "
-                                       "curr_index) + needs_host 1; counted over exactly the timed steps"},
+                         "bytes_note": "16L state read + obs f32 write + 36 B of per-env scalars (move-history "
+                                       "ring base included) + changed relators x 4L + per finished env 8L + 8L + "
+                                       "8 (curriculum row in, reset row out, curr_index, next ring base) + "
+                                       "needs_host 1; counted over exactly the timed steps"},
         }
         # the same with the episodes out of phase (step_count[i] = i mod H, as rollout_desync):
         # ~B/H envs finish and take their next initial state on every step -- a PPO rollout's
@@ -934,6 +936,8 @@ def run_rank(args):
         n_tab = B + 2 * (KL + 1) * (-(-B // H)) + 4096
         lenv = LearnerEnv(ms_starts(L, n_tab), B, horizon_length=H, device=dev)
         lenv.vec.step_count.copy_(torch.arange(B, dtype=torch.int32, device=dev) % H)
+        # each env's episode began step_count steps ago: its move-history ring base says so
+        lenv.hist_base.copy_((-lenv.vec.step_count) % lenv.hist_cap)
         lenv.step(la[0], obs_out=lobs[1], reward_out=lrew[0], done_out=ldone[0])
         lbufs = learner_buffers(lenv)
         rp2 = replay_walk(lstep, lenv.state, lbufs, KL, L, finished=(lenv.done, lenv.truncated))

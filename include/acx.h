@@ -124,31 +124,37 @@ int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset
  *   reward_f32  (B) float32 or NULL (rewards[t], training.py:241-253).
  *   done_f32    (B) float32 or NULL: done only, as next_done = torch.Tensor(done) (:354-356).
  *   done, truncated (B) uint8 or NULL.
- *   action_hist (hist_cap, B) uint8 or NULL: the moves of each env's current episode, move k
- *               of env i at [k, i] (ACEnv.actions / info["actions"], ac_env.py:96,105;
- *               training.py:275-280); step-major so envs at the same episode position write
- *               one coalesced segment.
+ *   action_hist (hist_cap, B) uint8 or NULL: the moves of each env's current episode
+ *               (ACEnv.actions / info["actions"], ac_env.py:96,105; training.py:275-280),
+ *               step-major: with hist_base NULL move k of env i is at [k, i]; with hist_base
+ *               ((B) int32, in/out) it is at [(hist_base[i] + k) mod hist_cap, i] and an
+ *               episode's move 0 sets hist_base[i] = hist_t mod hist_cap -- hist_t is the
+ *               caller's step counter (+1 per call) -- so every env writes this step's move to one
+ *               row, coalesced, however far apart the envs' episodes are.  Read an ended
+ *               episode's moves right after its last step (the next call may start the ring
+ *               over them); an episode longer than hist_cap moves keeps its first hist_cap.
  *   episode_len (B) int32 or NULL: the length of the episode that ended this step, else 0.
  *   step_count is required (truncation, history position).
  */
 int acx_step_learner(int32_t* state, const int32_t* action, const int64_t* action_i64, const int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
-                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len,
-                     int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
-                     int32_t cyclical, void* stream);
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                     int32_t* episode_len, int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L,
+                     int32_t horizon, int32_t cyclical, void* stream);
 
 /*
  * acx_step plus the episode move history gymnasium's SyncVectorEnv hands the trainer
  * (ac_env.py:92,105-110 -> infos["final_info"][i]["actions"] / infos["actions"][i],
- * training.py:273-280): action_hist (hist_cap, B) uint8, move k of env i's current episode at
- * [k, i]; episode_len (B) int32 or NULL = the length of the episode that ended this step
+ * training.py:273-280): action_hist (hist_cap, B) uint8 and hist_base / hist_t as
+ * acx_step_learner; episode_len (B) int32 or NULL = the length of the episode that ended this step
  * (done | truncated), else 0.  step_count and action_hist are required; other arguments as
  * acx_step.
  */
 int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
                     int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
-                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                    int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+                    int32_t* final_obs, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                    int32_t* episode_len, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                    int32_t cyclical, void* stream);
 
 /*
  * acx_step with gymnasium >= 1.0's NEXT_STEP autoreset instead of the same-step one (the
@@ -157,14 +163,15 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
  * env whose flag is set is reset to its reset_state row on this call instead of stepping --
  * its action is ignored, reward 0, done = truncated = 0, step count 0 -- and every env's flag
  * becomes done | truncated of this call, so the step that ends an episode returns the terminal
- * state itself.  action_hist / hist_cap / episode_len: as acx_step_record (NULL / 0 / NULL for
- * none).  reset_state and step_count are required; other arguments as acx_step (no final_obs:
+ * state itself.  action_hist / hist_cap / hist_base / hist_t / episode_len: as acx_step_record
+ * (NULL / 0 / NULL / 0 / NULL for none).  reset_state and step_count are required; other arguments as acx_step (no final_obs:
  * the ending step's state is the observation).
  */
 int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
                   int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,
-                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                  int32_t* err_count, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+                  uint8_t* pending, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                  int32_t* episode_len, uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                  int32_t cyclical, void* stream);
 
 /*
  * Start-state curriculum of the PPO trainer, round 1 (training.py:319-352): every env whose
@@ -196,10 +203,10 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
  */
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
-                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* episode_len, uint8_t* err,
-                     int32_t* err_count, const int32_t* curriculum_states, int64_t n_states, int32_t* next_index,
-                     int32_t* curr_index, uint8_t* needs_host, int32_t* workspace, int64_t B, int32_t L,
-                     int32_t horizon, int32_t cyclical, void* stream);
+                     uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
+                     int32_t* episode_len, uint8_t* err, int32_t* err_count, const int32_t* curriculum_states,
+                     int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
+                     int32_t* workspace, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
 
 /*
  * T fused env steps (PPO rollout collection).  state (B,2L) and step_count (B) are

@@ -128,8 +128,8 @@ def test_step_learner_matches_acx_step():
         rf = torch.empty(B, dtype=torch.float32, device=DEV)
         df = torch.empty(B, dtype=torch.float32, device=DEV)
         rc = lib.acx_step_learner(st_b.data_ptr(), None, a.data_ptr(), rs.data_ptr(), cb.data_ptr(), obs.data_ptr(),
-                                  rf.data_ptr(), df.data_ptr(), None, None, None, 0, None, None, None, None, B, L, 11, 1,
-                                  stream)
+                                  rf.data_ptr(), df.data_ptr(), None, None, None, 0, None, 0, None, None, None, None, B,
+                                  L, 11, 1, stream)
         assert rc == 0
         assert torch.equal(st_a, st_b) and torch.equal(ca, cb)
         assert torch.equal(obs, st_b.to(torch.float32))
@@ -139,7 +139,8 @@ def test_step_learner_matches_acx_step():
     bad = torch.full((B,), 12, dtype=torch.int64, device=DEV)
     before = st_b.clone()
     assert lib.acx_step_learner(st_b.data_ptr(), None, bad.data_ptr(), rs.data_ptr(), cb.data_ptr(), None, None, None,
-                                None, None, None, 0, None, None, err.data_ptr(), None, B, L, 11, 1, stream) == 0
+                                None, None, None, 0, None, 0, None, None, err.data_ptr(), None, B, L, 11, 1,
+                                stream) == 0
     assert (err == _lib.ERR_ACTION).all() and torch.equal(before, st_b)
 
 

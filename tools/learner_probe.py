@@ -5,6 +5,7 @@ the next initial states of the round-1 curriculum).  From one snapshot of the Le
 buffers, K steps are timed (HIP events, current stream) through
   fused  -- acx_learner_step (one launch, the ranking inside the step kernel),
   four   -- acx_step_learner + acx_curriculum_assign,
+  fused_nohist -- fused without the per-env move history (hist_cap 0),
 and the same two on the fresh workload (every step_count 0: almost no env finishes).  Every
 variant must leave the same state (checksum).  Run under rocprofv3 --kernel-trace --stats to
 split the four-launch path by kernel.
@@ -24,6 +25,13 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "ac-solver-caltech_amd"))
 from bench import learner_buffers, ms_starts, restore  # noqa: E402
+
+
+class _Null:
+    """a NULL device pointer where LearnerEnv passes action_hist.data_ptr()"""
+
+    def data_ptr(self):
+        return 0
 
 
 def main():
@@ -47,19 +55,26 @@ def main():
         lenv = LearnerEnv(ms_starts(L, n_tab), B, horizon_length=H, device=dev)
         if wl == "desync":
             lenv.vec.step_count.copy_(torch.arange(B, dtype=torch.int32, device=dev) % H)
+            lenv.hist_base.copy_((-lenv.vec.step_count) % lenv.hist_cap)
         lenv.step(acts[0], obs_out=obs[1], reward_out=rew[0], done_out=done[0])
+        hist_cap, hist, hbase = lenv.hist_cap, lenv.action_hist, lenv.hist_base
         bufs = learner_buffers(lenv)
         snap = [t.clone() for t in bufs]
         torch.cuda.synchronize()
         sums = {}
         for rep in range(args.reps):
-            for mode in ("fused", "four"):
+            for mode in ("fused", "four", "fused_nohist"):
+                # fused_nohist: hist_cap 0 -- the kernel writes no move history (isolates the cost of
+                # the (hist_cap, B) byte writes, one cache line per lane when episodes are out of phase)
+                lenv.hist_cap = 0 if mode == "fused_nohist" else hist_cap
+                lenv.action_hist = _Null() if mode == "fused_nohist" else hist
+                lenv.hist_base = _Null() if mode == "fused_nohist" else hbase
                 restore(snap, bufs)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for t in range(K):
-                    lenv.step(acts[t], obs_out=obs[t + 1], reward_out=rew[t], done_out=done[t], fused=mode == "fused")
+                    lenv.step(acts[t], obs_out=obs[t + 1], reward_out=rew[t], done_out=done[t], fused=mode != "four")
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / K
