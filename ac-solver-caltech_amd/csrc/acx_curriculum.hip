@@ -141,10 +141,13 @@ using namespace acx::cur;
 extern "C" {
 
 int64_t acx_internal_curriculum_fused_offset(int64_t B);
+#define ACX_CUR_ARRIVE_STRIDE 32  // as acx_kernels.hip's CurLayout
 int64_t acx_curriculum_workspace(int64_t B) {
     if (B < 0) return 0;
     const int64_t tiles = (B + WAVE - 1) / WAVE, groups = (tiles + WAVE - 1) / WAVE;
-    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + tiles + 2 * groups);
+    // acx_learner_step's part: [0] sequence number, [1, 2] base, tile counts, group totals, and
+    // the groups' arrival words ACX_CUR_ARRIVE_STRIDE apart (acx_kernels.hip, CurLayout)
+    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + tiles + groups + groups * ACX_CUR_ARRIVE_STRIDE);
 }
 
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,

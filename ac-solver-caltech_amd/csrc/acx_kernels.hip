@@ -2107,6 +2107,12 @@ __device__ __forceinline__ void cur_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// uint64 words between two groups' arrival words, the launch's only same-address atomics (64
+// tiles add to each): 256 bytes apart, one per channel-interleave unit, the step is 6 % faster
+// than with the words packed (fresh episodes 0.1257 vs 0.1345 ms, steady state 0.159 vs 0.165,
+// profiles/r05/r05x_learner_probe_stride.json; spacing the tile count words too changed nothing).
+// acx_curriculum_workspace (acx_curriculum.hip) sizes the workspace with the same value
+#define ACX_CUR_ARRIVE_STRIDE 32
 struct CurLayout {
     int64_t tiles, groups;
     uint64_t *base, *tile, *group, *arrive;
@@ -2122,15 +2128,17 @@ struct CurLayout {
 
 // this tile's count, its group arrival, and (tile 0) the base.  Returns the arrival word before
 // this tile's add (lane 0), for cur_publish_end right after: deferring that to the tile's tail
-// (so the add's return trip overlaps the stores) made the steady-state step slower, 0.217 vs
-// 0.203 ms (r05l vs r05k bench lines), since later tiles then wait longer for the group total
+// (so the add's return trip overlaps the stores) made the step slower, fresh episodes 0.143 vs
+// 0.140 ms and steady state 0.21 vs 0.172 (same buffers, r05v), as later tiles then wait longer
+// for the group total
 __device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt) {
     if (w.lane != 0) return 0;
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     if (t == 0) cur_store(c.base, cur_word(seq, (uint32_t)*a.cur_next));
     cur_store(c.tile + t, cur_word(seq, cnt));
-    return __hip_atomic_fetch_add(c.arrive + g, (1ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_fetch_add(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, (1ull << 32) | cnt, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
 }
 // the add that completed its group publishes the group's total and clears the arrival word for
 // the next launch
@@ -2142,52 +2150,56 @@ __device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx
     const int64_t gsize = (c.tiles - g * WAVE) < WAVE ? (c.tiles - g * WAVE) : WAVE;
     if ((int64_t)(old >> 32) + 1 == gsize) {
         cur_store(c.group + g, cur_word(seq, (uint32_t)old + cnt));
-        cur_store(c.arrive + g, 0ull);
+        cur_store(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, 0ull);
     }
 }
 
 // base + the counts of every tile before this one (all_groups: + every group's total instead: the
-// last tile's next_index), or CUR_FAIL.  Wave-uniform control flow.
+// last tile's next_index), or CUR_FAIL.  Wave-uniform control flow.  A word, once seen with this
+// launch's seq, is final: each lane re-reads only the words it has not seen yet (`pend`), so the
+// polls of the waiting tiles thin out as the prefix fills in (re-reading every word on every poll
+// put ~4k waiting waves on the same few dozen lines).  Group totals are taken 4 per lane, 256 per
+// round; the base (lane 0) and the own group's earlier tile counts (a lane each) with the first.
+// (s_sleep 8 between polls instead: the same, r05v)
 __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, bool all_groups) {
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     const int64_t ng = all_groups ? c.groups : g;  // whole groups summed
-    uint32_t polls = 0;
+    auto group_bits = [&](int64_t k0) {
+        uint32_t b = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b |= (k0 + 4 * w.lane + i < ng) ? 1u << i : 0u;
+        return b;
+    };
+    uint32_t pend = group_bits(0);
+    if (w.lane == 0) pend |= 1u << 5;                            // the base
+    if (!all_groups && g * WAVE + w.lane < t) pend |= 1u << 4;  // a tile before this one in its group
+    uint32_t x = 0, polls = 0;
+    int64_t k0 = 0;
     while (true) {
-        bool ok = true;
-        uint32_t x = 0;
-        if (w.lane == 0) {
-            const uint64_t v = cur_load(c.base);
-            ok = cur_is(v, seq);
-            x = (uint32_t)v;
-        }
-        for (int64_t k0 = 0; k0 < ng; k0 += 4 * WAVE) {  // 4 group totals per lane per round
-            uint64_t v[4];
+        uint64_t v[6];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int64_t k = k0 + 4 * w.lane + i;
-                v[i] = k < ng ? cur_load(c.group + k) : cur_word(seq, 0);
-            }
+        for (int i = 0; i < 4; ++i) v[i] = (pend >> i) & 1u ? cur_load(c.group + k0 + 4 * w.lane + i) : 0ull;
+        v[4] = (pend >> 4) & 1u ? cur_load(c.tile + g * WAVE + w.lane) : 0ull;
+        v[5] = (pend >> 5) & 1u ? cur_load(c.base) : 0ull;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                ok = ok && cur_is(v[i], seq);
+        for (int i = 0; i < 6; ++i)
+            if (((pend >> i) & 1u) && cur_is(v[i], seq)) {
                 x += (uint32_t)v[i];
+                pend &= ~(1u << i);
             }
-        }
-        if (!all_groups) {  // the tiles before this one in its group
-            const int64_t k = g * WAVE + w.lane;
-            const uint64_t v = k < t ? cur_load(c.tile + k) : cur_word(seq, 0);
-            ok = ok && cur_is(v, seq);
-            x += (uint32_t)v;
-        }
-        if (__all(ok)) {
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, WAVE);
-            return x;
+        if (__all(pend == 0u)) {
+            k0 += 4 * WAVE;
+            if (k0 >= ng) break;
+            pend = group_bits(k0);
+            continue;
         }
         if (++polls > (1u << 20)) return CUR_FAIL;
         __builtin_amdgcn_s_sleep(2);
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, WAVE);
+    return x;
 }
 
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
@@ -2364,8 +2376,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             const uint64_t late = rb & ~pre;
             if (late) tile.load_rows(a.reset_state + w.r0 * twoL, late, w.R, w.lane);
             if (reset) {
+                // the tile row already holds the starting row's image (what unpack would write
+                // for a row in the domain; a row outside it is stored from its fallback): pack
+                // only checks it and sets the lengths
                 rbad = tile.pack(w.lane, p);
-                if (!rbad) tile.unpack(w.lane, p);
                 dm = 3u;
             }
             tile.flag_rows(w.lane, rbad ? FB_RESET : 0u);

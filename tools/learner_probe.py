@@ -10,7 +10,10 @@ and the same two on the fresh workload (every step_count 0: almost no env finish
 variant must leave the same state (checksum).  Run under rocprofv3 --kernel-trace --stats to
 split the four-launch path by kernel.
 
-    python tools/learner_probe.py [--K 50] [--reps 3]
+    python tools/learner_probe.py [--K 50] [--reps 3] [--libs a.so b.so ...]
+
+--libs: the fused step through each library in turn (tools/ab_build.sh builds: kernels and
+curriculum only), same buffers, interleaved, as "fused@<name>".
 """
 import argparse
 import json
@@ -39,8 +42,24 @@ def main():
     ap.add_argument("--K", type=int, default=50)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--B", type=int, default=1 << 20)
+    ap.add_argument("--libs", nargs="*", default=[])
     args = ap.parse_args()
+    import ctypes
+
+    from acx import _lib
     from acx.agents import LearnerEnv
+
+    main_lib = _lib.load()
+    libs = {"": main_lib}
+    for path in args.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        for name, (argtypes, restype) in _lib.SIGNATURES.items():
+            if hasattr(lib, name):
+                getattr(lib, name).argtypes = argtypes
+                getattr(lib, name).restype = restype
+        libs[os.path.basename(path)] = lib
+    modes = [("fused", ""), ("four", ""), ("fused_nohist", "")] if not args.libs else \
+        [("fused", k) for k in libs]
 
     dev = torch.device("cuda:0")
     L, H, B, K = 36, 200, args.B, args.K
@@ -53,6 +72,9 @@ def main():
     for wl in ("desync", "fresh"):
         n_tab = B + 2 * (K + 1) * (-(-B // H)) * args.reps * 2 + 4096
         lenv = LearnerEnv(ms_starts(L, n_tab), B, horizon_length=H, device=dev)
+        # a workspace large enough for every library's layout (acx_curriculum_workspace may differ)
+        lenv._ws = torch.zeros(max(int(lib.acx_curriculum_workspace(B)) for lib in libs.values()), dtype=torch.int32,
+                               device=dev)
         if wl == "desync":
             lenv.vec.step_count.copy_(torch.arange(B, dtype=torch.int32, device=dev) % H)
             lenv.hist_base.copy_((-lenv.vec.step_count) % lenv.hist_cap)
@@ -63,7 +85,8 @@ def main():
         torch.cuda.synchronize()
         sums = {}
         for rep in range(args.reps):
-            for mode in ("fused", "four", "fused_nohist"):
+            for mode, lk in modes:
+                _lib._lib = libs[lk]
                 # fused_nohist: hist_cap 0 -- the kernel writes no move history (isolates the cost of
                 # the (hist_cap, B) byte writes, one cache line per lane when episodes are out of phase)
                 lenv.hist_cap = 0 if mode == "fused_nohist" else hist_cap
@@ -82,7 +105,8 @@ def main():
                 ck = int(lenv.state.to(torch.int64).sum().item())
                 if sums.setdefault("ref", ck) != ck:  # every mode and rep leaves the same state
                     res[f"{wl}_mismatch"] = True
-                res.setdefault(f"{wl}_{mode}_ms", []).append(round(ms, 4))
+                _lib._lib = main_lib
+                res.setdefault(f"{wl}_{mode}{'@' + lk if lk else ''}_ms", []).append(round(ms, 4))
                 res[f"{wl}_finished_last_step"] = fin
         del lenv, bufs, snap
     print(json.dumps(res))
