@@ -1088,9 +1088,10 @@ def config2_variant(dev, H: int, timed) -> dict:
     err = torch.zeros(B2, dtype=torch.uint8, device=dev)
     ec = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    def step(a):
-        ops.step(st, a, state_out=st, reset_state=starts, step_count=cnt, horizon=H, cyclical=True, reward=rew,
-                 done=dn, truncated=tr, lengths=lens, err=err, err_count=ec)
+    # the arguments resolved once (ops.StepPlan: one ctypes call per step; ops.step's per-call
+    # checks, not the ~10 us kernel, set the eager rate at this batch)
+    step = ops.StepPlan(st, state_out=st, reset_state=starts, step_count=cnt, horizon=H, cyclical=True, reward=rew,
+                        done=dn, truncated=tr, lengths=lens, err=err, err_count=ec)
 
     for t in range(W2):
         step(acts[t])
@@ -1112,7 +1113,7 @@ def config2_variant(dev, H: int, timed) -> dict:
                         "frac": B2 * sb / (s_k / K2) / 1e9 / HBM_PEAK_GBS, "bytes_per_env_step": sb,
                         "changed_relators_per_env_step": chg, "kernel": ops.step_kernel_name(B2, L2)},
            "workload": "BASELINE configs[1]: 65536 envs, L=36, Miller-Schupp starts, uniform random actions, per-call "
-                       "acx_step in place, horizon 200, same-step autoreset; 200 launches"}
+                       "acx_step in place (ops.StepPlan), horizon 200, same-step autoreset; 200 launches"}
     gs = torch.cuda.Stream(device=dev)
     gs.wait_stream(torch.cuda.current_stream(dev))
     graph = torch.cuda.CUDAGraph()
