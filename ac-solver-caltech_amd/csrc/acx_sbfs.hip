@@ -118,6 +118,7 @@ constexpr int POS_SHIFT = 24;
 constexpr uint64_t FP_MASK = (1ull << POS_SHIFT) - 1;
 constexpr int64_t MAX_CHUNK = 1 << 19;
 constexpr int64_t MAX_ARENA = (1ll << (64 - POS_SHIFT)) - 2;  // positions the entry can name
+static int64_t g_arena_override = 0;  // tests only (acx_internal_sbfs_arena_cap): a smaller first arena
 __device__ __forceinline__ uint64_t entry_of(int64_t pos, uint64_t h) {
     return ((uint64_t)(pos + 1) << POS_SHIFT) | ((h >> 32) & FP_MASK);
 }
@@ -920,7 +921,7 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
     // the arena's first size: 12 records per expanded parent, which is ~2 per node in an AK(n)
     // search (BASELINE config 4: 1.59M parents for 10^7 nodes), plus received records at G > 1,
     // and room for one full chunk; it doubles when a chunk would not fit (grow_arena)
-    S->acap = 1 + 3 * S->lcap + 24 * pl;
+    S->acap = g_arena_override > 0 ? g_arena_override : 1 + 3 * S->lcap + 24 * pl;
     if (S->acap > MAX_ARENA) S->acap = MAX_ARENA;
     bool ok = dalloc(a.arena, (size_t)(S->acap * S->kw)) && dalloc(a.lapos, (size_t)S->lcap) &&
               dalloc(a.lgid, (size_t)S->lcap) && dalloc(a.lpar, (size_t)S->lcap) && dalloc(a.lact, (size_t)S->lcap) &&
@@ -951,6 +952,12 @@ void* acx_sbfs_create(int32_t L, int64_t local_cap, int64_t chunk_parents, int32
 }
 
 void acx_sbfs_destroy(void* h) { delete static_cast<Shard*>(h); }
+
+// tests only: the first arena of workspaces created from now on holds 2^log2_cap records
+// (0: the normal size), so a search regrows it (grow_arena) many times
+void acx_internal_sbfs_arena_cap(int32_t log2_cap) {
+    g_arena_override = log2_cap > 0 ? (int64_t)1 << log2_cap : 0;
+}
 
 int64_t acx_sbfs_max_records(void* h) {
     Shard* S = static_cast<Shard*>(h);

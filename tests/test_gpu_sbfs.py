@@ -95,6 +95,40 @@ def test_sharded_bfs_one_rank_node_order():
     assert [ok, [list(x) for x in path]] == kat["bfs_ak2"]
 
 
+def test_sharded_bfs_arena_regrowth():
+    """the key arena starting at 64 records (test hook) regrows by doubling between chunks --
+    entries name arena positions, so a reallocation must leave every probe, key compare, parent
+    expansion and lookup intact: same nodes in the same order as the device BFS, and the
+    reference's AK(2) path"""
+    import ctypes
+    from acx import _lib
+    from acx.search import _device_bfs as D
+    from acx.search import _sharded_bfs as S
+    hook = _lib.load().acx_internal_sbfs_arena_cap
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    start = _ak3(36)
+    r_d = D.device_bfs(start, 100_000, device=DEV, chunk=3000, keep_node_keys=True)
+    nd = D.LAST_STATS["nodes"]
+    dk = D.LAST_STATS["node_keys"][:nd]
+    S.release_workspaces()
+    hook(6)
+    try:
+        r_s = S.sharded_bfs(start, 100_000, device=DEV, chunk=3000, keep_node_keys=True)
+        ids, keys, n_s = S.LAST_STATS["node_ids"], S.LAST_STATS["node_keys"], S.LAST_STATS["nodes"]
+        with open(os.path.join(GOLDEN, "kat_search.json")) as f:
+            kat = json.load(f)
+        ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
+        S.release_workspaces()
+        ok, path = S.sharded_bfs(ak2, int(1e6), device=DEV)
+    finally:
+        hook(0)
+        S.release_workspaces()
+    assert r_s == r_d and n_s == nd
+    assert np.array_equal(ids[:nd], np.arange(nd)) and np.array_equal(keys[:nd], dk)
+    assert [ok, [list(x) for x in path]] == kat["bfs_ak2"]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
