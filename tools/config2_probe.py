@@ -82,7 +82,7 @@ def main():
             res[f"B{B}_{name}"] = timed(step, K, a.reps)
             if B == 65536:
                 res[f"B{B}_{name}_invalid_ids"] = timed(lambda t: step(t, bad), K, a.reps)
-        if B == 65536:
+        if B in (65536, 1 << 20):  # the bare shapes at config 2's batch and at the headline's
             cl = ceiling_lib()
             out = torch.zeros(16384, dtype=torch.int32, device=dev)
             for kind, nm in ((5, "empty"), (1, "read_tile"), (3, "rw_tile"), (2, "read_tile_pipe")):
