@@ -2074,26 +2074,6 @@ constexpr uint64_t CUR_SET = 1ull << 62;
 constexpr uint32_t CUR_FAIL = 0xffffffffu;
 constexpr uint32_t CUR_SEQ_MASK = (1u << 30) - 1u;
 
-// one lane copies a (2L) int32 row (the rare per-env row writes: a reset row the curriculum set)
-__device__ __forceinline__ void copy_row(int32_t* dst, const int32_t* src, int twoL) {
-    if ((twoL & 3) == 0) {
-        for (int k = 0; k < twoL / 4; ++k) reinterpret_cast<int4*>(dst)[k] = reinterpret_cast<const int4*>(src)[k];
-    } else {
-        for (int k = 0; k < twoL; ++k) dst[k] = src[k];
-    }
-}
-
-__device__ __forceinline__ void copy_row_f32(float* dst, const int32_t* src, int twoL) {
-    if ((twoL & 3) == 0) {
-        for (int k = 0; k < twoL / 4; ++k) {
-            const int4 v = reinterpret_cast<const int4*>(src)[k];
-            reinterpret_cast<float4*>(dst)[k] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
-        }
-    } else {
-        for (int k = 0; k < twoL; ++k) dst[k] = (float)src[k];
-    }
-}
-
 __device__ __forceinline__ uint64_t cur_word(uint32_t seq, uint32_t v) {
     return CUR_SET | ((uint64_t)(seq & CUR_SEQ_MASK) << 32) | v;
 }
@@ -2202,6 +2182,46 @@ __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx&
     return x;
 }
 
+// the rows of the tile in the wave-uniform mask `rows` <- src(q, r) (q: the row's ordinal in the
+// mask, r: its row in the tile), written to state_out, obs_f32 (as float) and, with to_reset,
+// reset_state: the whole wave copies, 16-byte chunks spread over the lanes (a lane copying its
+// own row issued 4 x 2L/4 instructions for the wave per finished env)
+template <class Src>
+__device__ __forceinline__ void copy_rows(const StepArgs& a, const WaveCtx& w, uint64_t rows, int twoL, Src src,
+                                          bool to_reset) {
+    const int n = __popcll(rows);
+    if (n == 0) return;
+    const bool full = rows == ~0ull;
+    int32_t* st = a.state_out + w.r0 * twoL;
+    float* of = a.obs_f32 ? a.obs_f32 + w.r0 * twoL : nullptr;
+    int32_t* rs = to_reset ? const_cast<int32_t*>(a.reset_state) + w.r0 * twoL : nullptr;  // learner: writable
+    auto row_of = [&](int q) {
+        if (full) return q;
+        uint64_t m = rows;
+        for (int j = 0; j < q; ++j) m &= m - 1;
+        return (int)__builtin_ctzll(m);
+    };
+    if ((twoL & 3) == 0) {
+        const int cpr = twoL >> 2;
+        for (int i = w.lane; i < n * cpr; i += WAVE) {
+            const int q = i / cpr, c = i - q * cpr, r = row_of(q);
+            const int4 v = reinterpret_cast<const int4*>(src(q, r))[c];
+            reinterpret_cast<int4*>(st + (int64_t)r * twoL)[c] = v;
+            if (rs) reinterpret_cast<int4*>(rs + (int64_t)r * twoL)[c] = v;
+            if (of) reinterpret_cast<float4*>(of + (int64_t)r * twoL)[c] = make_float4((float)v.x, (float)v.y, (float)v.z,
+                                                                                       (float)v.w);
+        }
+    } else {
+        for (int i = w.lane; i < n * twoL; i += WAVE) {
+            const int q = i / twoL, c = i - q * twoL, r = row_of(q);
+            const int32_t v = src(q, r)[c];
+            st[(int64_t)r * twoL + c] = v;
+            if (rs) rs[(int64_t)r * twoL + c] = v;
+            if (of) of[(int64_t)r * twoL + c] = (float)v;
+        }
+    }
+}
+
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
 // LIVE: the lengths-carrying step (its own kernel, so the plain step's registers stay its own)
 template <int NW, int LC, int VEC, bool LEARN, bool LIVE, int BATCH = 0>
@@ -2215,6 +2235,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     if (!wave_ctx(a.B, w)) return;
     // the launch's sequence number, read before this tile publishes (cur_publish)
     const uint32_t cseq = cur ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws)) : 0u;
+    // next_index as this launch found it (the last tile replaces it only after every tile has
+    // published, i.e. read it).  exhausted (round 1 complete): no finished env gets a state from
+    // the table, so no tile waits for its ranking; the host draws for every finished env.
+    // (Leaving a finished env's rows out of the tile's stores when the table surely lasts the
+    // launch, so that its copy needs no drain, was slower: the tile's obs store then takes its
+    // per-chunk flagged path, 0.164 vs 0.150 ms per steady-state step, r05zg.)
+    const int64_t cnext = cur ? (int64_t)__builtin_amdgcn_readfirstlane(
+                                    __hip_atomic_load(a.cur_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : 0;
+    const bool exhausted = cur && cnext >= a.n_states;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2430,8 +2460,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // with that row as it is (acx_curriculum_assign's copy; a row outside the packed domain
         // is then reported with err 3 by the next step) and curr_index = k; past the table's end
         // (round 1 complete) needs_host = 1 and the host draws.  The last tile waits for the total
-        // (the new next_index).
-        const uint32_t first = fm ? cur_prefix(a, w, cseq, false) : 0u;
+        // (the new next_index).  The copies are made by the whole wave, 16-byte chunks over the
+        // lanes (copy_rows): one lane copying its own row made the steady-state step 0.165 ms
+        // instead of 0.150 (r05zg).
+        const uint32_t first = (fm && !exhausted) ? cur_prefix(a, w, cseq, false) : 0u;
         if (w.r0 + w.R == a.B) {
             const uint32_t tot = cur_prefix(a, w, cseq, true);
             if (w.lane == 0) {
@@ -2441,23 +2473,26 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
                 cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
             }
         }
-        // the tile's own stores of these rows (other lanes, other instructions) complete first
-        if (fm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool failed = first == CUR_FAIL;  // wave-uniform
+        // finished envs with index k = first + (finished envs before it in the tile) < n_states
+        uint64_t take = 0;
+        if (fm && !exhausted && !failed) {
+            const int64_t nq = a.n_states - (int64_t)first;  // how many of the tile's finished envs get a state
+            take = fm;
+            while (take && (int64_t)__popcll(take) > nq) take &= ~(1ull << (63 - __builtin_clzll(take)));
+        }
+        if (take) {
+            // the rows were autoreset above (a failed ranking leaves them so): the tile's own
+            // stores of them complete first
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            copy_rows(a, w, take, twoL, [&](int q, int) { return a.cur_states + ((int64_t)first + q) * twoL; }, true);
+        }
         if (w.active) {
             uint8_t nh = 0;
             if (fin) {
-                const int64_t k = (int64_t)first + __popcll(fm & ((1ull << w.lane) - 1ull));
-                if (first == CUR_FAIL) {
-                    nh = 3;
-                } else if (k < a.n_states) {
-                    const int32_t* src = a.cur_states + k * twoL;
-                    copy_row(a.state_out + env * twoL, src, twoL);
-                    copy_row(const_cast<int32_t*>(a.reset_state) + env * twoL, src, twoL);  // learner: writable
-                    if (a.obs_f32) copy_row_f32(a.obs_f32 + env * twoL, src, twoL);
-                    a.curr_index[env] = (int32_t)k;
-                } else {
-                    nh = 1;
-                }
+                if (failed) nh = 3;
+                else if ((take >> w.lane) & 1ull) a.curr_index[env] = (int32_t)((int64_t)first + __popcll(fm & ((1ull << w.lane) - 1ull)));
+                else nh = 1;
             }
             a.needs_host[env] = nh;
         }
@@ -3608,6 +3643,7 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
         !workspace)
         return ACX_E_ARG;
     if (!aligned16(state) || (obs_f32 && !aligned16(obs_f32))) return ACX_E_ARG;
+    if ((L % 2) == 0 && (!aligned16(reset_state) || !aligned16(curriculum_states))) return ACX_E_ARG;  // int4 row copies
     // one launch: the step kernel ranks the finished envs itself (cur_publish / cur_prefix) in its part of the
     // workspace (acx_curriculum_workspace(B) int32 words, zeroed before the first call, 8-byte aligned)
     int32_t* ws = workspace + acx_internal_curriculum_fused_offset(B);

@@ -199,7 +199,8 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
  * past the table's end needs_host[env] = 1.  needs_host[env] = 3: the ranking gave up (an earlier
  * tile not scheduled within ~seconds, or a workspace shared by concurrent launches); the env kept
  * its own starting row and was not ranked.  done, truncated, reset_state and the curriculum
- * arguments are required; B < 2^31; workspace = acx_curriculum_workspace(B) int32 words (above).
+ * arguments are required; B < 2^31; workspace = acx_curriculum_workspace(B) int32 words (above);
+ * for even L, reset_state and curriculum_states 16-byte aligned (as state and obs_f32).
  */
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
