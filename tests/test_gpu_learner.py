@@ -65,7 +65,8 @@ def test_learner_env_matches_training_loop_restatement(L, B, N, H, T, adtype):
     assert n_host > 0 or N - B > T * B  # round 1 completed in the long cases
 
 
-@pytest.mark.parametrize("L,B,N,H", [(36, 5000, 9000, 6), (36, 4096, 4200, 3), (128, 300, 700, 4), (18, 65, 90, 2)])
+@pytest.mark.parametrize("L,B,N,H", [(36, 5000, 9000, 6), (36, 4096, 4200, 3), (128, 300, 700, 4), (18, 65, 90, 2),
+                                     (19, 333, 700, 3)])  # odd L: the curriculum copy's per-int32 path
 def test_fused_learner_step_equals_two_calls(L, B, N, H):
     """acx_learner_step (step kernel + one curriculum pass from per-wave counts) gives the same
     state, outputs, curriculum indices and host flags as acx_step_learner + acx_curriculum_assign,
