@@ -105,31 +105,62 @@ __global__ __launch_bounds__(1024) void scan_kernel(Args a, int nb) {
     }
 }
 
+// each finished env of the block takes its state; the block's copies are made by all its threads,
+// 16-byte chunks spread over them (a thread copying its own env's row element by element took
+// 24-35 us per 2^20-env step with ~B/H envs finishing)
 __global__ __launch_bounds__(TPB) void assign_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
+    __shared__ int64_t sidx[TPB];  // the block's finished envs with a state, in env order: their table row
+    __shared__ int32_t senv[TPB];  //   ... and their env index within the block
+    __shared__ uint32_t scnt;
     const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
     const bool f = finished(a, i);
     uint32_t tot;
     const uint32_t r = block_excl_scan(f ? 1u : 0u, sh, tot);
-    if (i >= a.B) return;
-    if (!f) {
-        a.needs_host[i] = 0;
-        return;
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
+    if (i < a.B) {
+        uint8_t nh = 0;
+        if (f) {
+            const int64_t idx = (int64_t)*a.base + a.bsum[blockIdx.x] + r;
+            if (idx >= a.n_states) {  // round 1 complete (training.py:329-333): the host picks
+                nh = 1;
+            } else {
+                a.curr_index[i] = (int32_t)idx;
+                // the finished envs that take a state are a prefix of the block's finished envs
+                // (idx grows with r), so r is also their position in the copy list
+                sidx[r] = idx;
+                senv[r] = (int32_t)threadIdx.x;
+                atomicAdd(&scnt, 1u);  // LDS
+            }
+        }
+        a.needs_host[i] = nh;
     }
-    const int64_t idx = (int64_t)*a.base + a.bsum[blockIdx.x] + r;
-    if (idx >= a.n_states) {  // round 1 complete (training.py:329-333): the host picks
-        a.needs_host[i] = 1;
-        return;
-    }
-    a.needs_host[i] = 0;
-    a.curr_index[i] = (int32_t)idx;
+    __syncthreads();
+    const int n = (int)scnt;
     const int twoL = 2 * a.L;
-    const int32_t* src = a.states + idx * twoL;
-    for (int k = 0; k < twoL; ++k) {
-        const int32_t v = src[k];
-        a.state[i * twoL + k] = v;
-        if (a.reset_state) a.reset_state[i * twoL + k] = v;
-        if (a.obs_f32) a.obs_f32[i * twoL + k] = (float)v;
+    const int64_t row0 = (int64_t)blockIdx.x * TPB;
+    if ((twoL & 3) == 0) {
+        const int cpr = twoL >> 2;
+        for (int t = threadIdx.x; t < n * cpr; t += TPB) {
+            const int q = t / cpr, c = t - q * cpr;
+            const int64_t e = row0 + senv[q];
+            const int4 v = reinterpret_cast<const int4*>(a.states + sidx[q] * twoL)[c];
+            reinterpret_cast<int4*>(a.state + e * twoL)[c] = v;
+            if (a.reset_state) reinterpret_cast<int4*>(a.reset_state + e * twoL)[c] = v;
+            if (a.obs_f32)
+                reinterpret_cast<float4*>(a.obs_f32 + e * twoL)[c] = make_float4((float)v.x, (float)v.y, (float)v.z,
+                                                                                 (float)v.w);
+        }
+    } else {
+        for (int t = threadIdx.x; t < n * twoL; t += TPB) {
+            const int q = t / twoL, c = t - q * twoL;
+            const int64_t e = row0 + senv[q];
+            const int32_t v = a.states[sidx[q] * twoL + c];
+            a.state[e * twoL + c] = v;
+            if (a.reset_state) a.reset_state[e * twoL + c] = v;
+            if (a.obs_f32) a.obs_f32[e * twoL + c] = (float)v;
+        }
     }
 }
 
@@ -159,6 +190,10 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
     if ((!done && !truncated) || !curriculum_states || !next_index || !curr_index || !needs_host || !state ||
         !workspace)
         return ACX_E_ARG;
+    auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+    if ((L % 2) == 0 && (!a16(curriculum_states) || !a16(state) || (reset_state && !a16(reset_state)) ||
+                         (obs_f32 && !a16(obs_f32))))
+        return ACX_E_ARG;  // the copies move 16-byte chunks
     const int nb = (int)((B + TPB - 1) / TPB);
     Args a{done, truncated, curriculum_states, n_states, next_index, curr_index, needs_host, state, reset_state,
            obs_f32, reinterpret_cast<uint32_t*>(workspace) + 1, workspace, B, L};

@@ -182,7 +182,8 @@ int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* ac
  * needs_host[env] = 1 (the reference then draws a random solved/unsolved state on the host).
  * workspace: acx_curriculum_workspace(B) int32 device words, 8-byte aligned, zeroed before the
  * first call and not written by the caller afterwards (acx_learner_step keeps its look-back state
- * there; one workspace serves both calls, but not two launches at once).
+ * there; one workspace serves both calls, but not two launches at once).  For even L the row
+ * arrays (curriculum_states, state, reset_state, obs_f32) are 16-byte aligned.
  */
 int64_t acx_curriculum_workspace(int64_t B);
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,
