@@ -2042,6 +2042,9 @@ struct StepArgs {
     // moves to one row -- coalesced -- instead of one cache line per lane
     int32_t* hist_base;
     int64_t hist_t;
+    // tests only (acx_internal_learner_ranking_fails): every ranking wait gives up at once, as one
+    // that polled 2^20 times would (needs_host = 3)
+    int cur_fail;
 };
 
 // ---------------------------------------------------------------------------------
@@ -2142,6 +2145,7 @@ __device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx
 // round; the base (lane 0) and the own group's earlier tile counts (a lane each) with the first.
 // (s_sleep 8 between polls instead: the same, r05v)
 __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, bool all_groups) {
+    if (a.cur_fail) return CUR_FAIL;
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     const int64_t ng = all_groups ? c.groups : g;  // whole groups summed
@@ -3628,6 +3632,10 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
 // acx_curriculum.hip: where acx_learner_step's part of the shared workspace starts (int32 words)
 int64_t acx_internal_curriculum_fused_offset(int64_t B);
 
+static int g_learner_fail = 0;  // tests only
+// tests only: acx_learner_step's ranking gives up at once (1) or works (0)
+void acx_internal_learner_ranking_fails(int32_t on) { g_learner_fail = on != 0; }
+
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
                      uint8_t* truncated, uint8_t* action_hist, int32_t hist_cap, int32_t* hist_base, int64_t hist_t,
@@ -3654,6 +3662,7 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
                curr_index, needs_host};
     a.hist_base = hist_base;
     a.hist_t = hist_t;
+    a.cur_fail = g_learner_fail;
     StepLaunch f{a, (hipStream_t)stream, true};
     return dispatch(L, f);
 }

@@ -269,3 +269,41 @@ def test_fused_learner_step_out_of_domain_curriculum_row():
         assert torch.equal(oa, ob) and torch.equal(ea.curr_index, eb.curr_index), t
         assert torch.equal(ea.vec.step_count, eb.vec.step_count), t
     assert errs > 0  # the copied out-of-domain rows were stepped (err 3)
+
+
+def test_fused_learner_step_ranking_failure():
+    """The one-launch step's ranking giving up (test hook: as a wait of 2^20 polls would, e.g. a
+    tile never scheduled) flags its finished envs needs_host = 3 and leaves each at its own
+    starting row with next_index unchanged; CurriculumRecord.process raises on it; the next
+    launches rank normally."""
+    import ctypes
+    from acx import _lib
+    from acx.agents import CurriculumRecord, LearnerEnv
+    L, B, N, H = 36, 2048, 6000, 2
+    init = _ms_states(L, N)
+    env = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    rec = CurriculumRecord(N, B, 0.5)
+    hook = _lib.load().acx_internal_learner_ranking_fails
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    acts = lambda: torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)  # noqa: E731
+    env.step(acts())
+    hook(1)
+    try:
+        done, trunc, _, nh = env.step(acts())  # every env truncates at H = 2
+    finally:
+        hook(0)
+    fin = (done | trunc).bool()
+    assert bool(fin.all())
+    assert bool((nh == 3).all())
+    assert torch.equal(env.state, torch.as_tensor(init[:B]).to(DEV))  # own starting rows
+    assert int(env.next_index.item()) == B and bool((env.vec.step_count == 0).all())
+    with pytest.raises(RuntimeError):
+        rec.process(env, done, trunc, nh)
+    env.step(acts())
+    done, trunc, _, nh = env.step(acts())  # all truncate again: ranked normally now
+    assert bool((nh == 0).all()) and int(env.next_index.item()) == 2 * B
+    assert torch.equal(env.curr_index, torch.arange(B, 2 * B, dtype=torch.int32, device=DEV))
+    assert torch.equal(env.state, torch.as_tensor(init[B: 2 * B]).to(DEV))
