@@ -452,25 +452,40 @@ __global__ __launch_bounds__(TPB, 8) void sbfs_insert_kernel(Args a) {  // 8 wav
 
 // (3b) this rank's survivors per parent -> mask bits (gmask, all-reduced next; mine, kept):
 // a child survives if it holds its entry and was not displaced by a smaller seq
-__global__ __launch_bounds__(TPB) void sbfs_mask_kernel(Args a) {
-    const int p = blockIdx.x * TPB + threadIdx.x;
-    if (p >= a.P) return;
+__device__ __forceinline__ uint32_t survivor_bits(const Args& a, int p) {
     uint32_t bits = 0;
 #pragma unroll
     for (int act = 0; act < 12; ++act) {
         const uint32_t s = (uint32_t)p * 12u + (uint32_t)act;
         if (a.sslot[s] != SEEN && !a.lost[s]) bits |= 1u << act;
     }
+    return bits;
+}
+__global__ __launch_bounds__(TPB) void sbfs_mask_kernel(Args a) {
+    const int p = blockIdx.x * TPB + threadIdx.x;
+    if (p >= a.P) return;
+    const uint32_t bits = survivor_bits(a, p);
     a.gmask[p] = bits;
     a.mine[p] = bits;
 }
 
-// (4a) per-block counts of all survivors and of this rank's
+// (4a) per-block counts of all survivors and of this rank's.  FOLD (one rank, no exchange: the
+// mask is this rank's own): the survivor bits are made here, the mask pass is not launched
+template <bool FOLD>
 __global__ __launch_bounds__(TPB) void sbfs_count_kernel(Args a) {
     __shared__ uint32_t sh[TPB / WAVE];
     const int p = blockIdx.x * TPB + threadIdx.x;
-    const uint32_t m = p < a.P ? a.gmask[p] : 0u;
-    const uint32_t mine = p < a.P ? a.mine[p] : 0u;
+    uint32_t m = 0, mine = 0;
+    if (p < a.P) {
+        if constexpr (FOLD) {
+            m = mine = survivor_bits(a, p);
+            a.gmask[p] = m;
+            a.mine[p] = m;
+        } else {
+            m = a.gmask[p];
+            mine = a.mine[p];
+        }
+    }
     uint32_t tot, ltot;
     block_excl_scan(__popc(m), sh, tot);
     __syncthreads();
@@ -739,6 +754,7 @@ struct Shard {
     int dev = 0, L = 0, kw = 0, cyc = 0, rank = 0, world = 1;
     int64_t lcap = 0, pmax = 0, rcap = 0, nloc = 0, lo = 0;
     int64_t acap = 0, abase = 0;  // arena records allocated / used
+    bool fold_mask = false;       // the last insert left the survivor bits to the commit's count
     int P = 0, Pr = 0;
     int64_t head = 0, nrecv = 0;
     uint64_t tsize = 0;
@@ -1080,7 +1096,10 @@ int acx_sbfs_insert(void* h, const uint64_t* recv, int64_t nrecv, int64_t end, u
         InsertLaunch il{S, st};
         by_nw(S->L, il);
     }
-    sbfs_mask_kernel<<<dim3(nblocks(S->P)), dim3(TPB), 0, st>>>(a);
+    // one rank with no exchange (end < 0): nobody reads gmask before the commit, whose count pass
+    // makes the survivor bits itself (sbfs_count_kernel<true>)
+    S->fold_mask = end < 0 && S->world == 1;
+    if (!S->fold_mask) sbfs_mask_kernel<<<dim3(nblocks(S->P)), dim3(TPB), 0, st>>>(a);
     return hipGetLastError() == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
 }
 
@@ -1098,7 +1117,9 @@ int acx_sbfs_commit(void* h, const uint32_t* gmask, int64_t n_before, int64_t ne
     a.need = need;
     a.nloc = S->nloc;
     const int nb = nblocks(S->P);
-    sbfs_count_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
+    if (S->fold_mask) sbfs_count_kernel<true><<<dim3(nb), dim3(TPB), 0, st>>>(a);
+    else sbfs_count_kernel<false><<<dim3(nb), dim3(TPB), 0, st>>>(a);
+    S->fold_mask = false;
     sbfs_scan_kernel<<<dim3(1), dim3(1024), 0, st>>>(a.bsum, a.lbsum, nb, &a.ctl->total_new, &a.ctl->local_new);
     sbfs_commit_kernel<<<dim3(nb), dim3(TPB), 0, st>>>(a);
     const int r = sync_ctl(S, st, 1);  // and re-initialise the control block for the next chunk

@@ -366,7 +366,8 @@ int64_t acx_bfs_min_trace(void* h, int32_t* out, int64_t cap);
  *   acx_sbfs_insert    probe / claim the visited set with this rank's own children and the
  *                      received records, up to seq `end` (end < 0: this rank's own first
  *                      success / move error, i.e. one rank's); survivors as bits of gmask ((P)
- *                      uint32, written by the call)
+ *                      uint32, written by the call -- or, with end < 0 at one rank, where
+ *                      nothing is exchanged, by the acx_sbfs_commit that follows)
  *   -- all_reduce (sum) of gmask over the ranks --
  *   acx_sbfs_commit    global ids, the node-budget cut and the appends; out int64[9] = nodes
  *                      appended (all ranks), cut parent (-1: none), nodes after the cut
