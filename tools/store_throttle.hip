@@ -108,8 +108,34 @@ __global__ __launch_bounds__(256) void tile_oneshot(int4* __restrict__ dst, int6
     for (int c = lane; c < WAVE * cpr; c += WAVE) st_nt(row + c, make_int4(v, (int)t, c, lane));
 }
 
+// the rollout's slices, but the block's 4 waves write their 4 adjacent tiles' slice of a step
+// together: thread t of the block stores chunks t, t + 256, ... of the block's 256-row slice, so
+// each store round covers 4 KB contiguous (as fill_oneshot's blocks do) instead of each wave
+// walking its own 18 KB.  SYNC: a block barrier between steps (the rollout's LDS tiles would
+// need one)
+template <int SYNC>
+__global__ __launch_bounds__(256) void tile_block(int4* __restrict__ dst, int64_t rows, int cpr, int K, int v) {
+    const int64_t r0 = (int64_t)blockIdx.x * 256;
+    if (r0 >= rows) return;
+    const int nch = 256 * cpr;
+    for (int t = 0; t < K; ++t) {
+        int4* row = dst + ((int64_t)t * rows + r0) * cpr;
+        for (int c = threadIdx.x; c < nch; c += 256) st_nt(row + c, make_int4(v, t, c, (int)threadIdx.x));
+        if (SYNC) __syncthreads();
+    }
+}
+
+// tile_block's slices written once each by short-lived blocks, step-major
+__global__ __launch_bounds__(256) void tile_block_oneshot(int4* __restrict__ dst, int64_t rows, int cpr, int v) {
+    const int64_t blocks_per_step = rows / 256;
+    const int64_t t = blockIdx.x / blocks_per_step, r0 = (blockIdx.x - t * blocks_per_step) * 256;
+    int4* row = dst + (t * rows + r0) * cpr;
+    for (int c = threadIdx.x; c < 256 * cpr; c += 256) st_nt(row + c, make_int4(v, (int)t, c, (int)threadIdx.x));
+}
+
 extern "C" {
 // kind: 0 fill_oneshot, 1 fill_stride, 2 tile, 3 tile_oneshot, 4 tile_grouped (n = GE: 8, 16, 32),
+// 6 tile_block (n: a barrier between steps), 7 tile_block_oneshot,
 // 5 tile with buffer stores of cache policy n (0 plain, 1 sc0, 2 nt, 16 sc1, 17 sc0 sc1, 18 sc1 nt); n: stores in flight per wave
 // (0 = unthrottled; 1, 2, 4, 8, 16); returns a hip error code
 int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin, int resident_blocks, void* stream) {
@@ -139,6 +165,11 @@ int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin
 #define G(NN) tile_grouped<NN><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7)
         switch (n) { case 8: G(8); break; case 16: G(16); break; default: G(32); }
 #undef G
+    } else if (kind == 6) {
+        if (n) tile_block<1><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
+        else tile_block<0><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
+    } else if (kind == 7) {
+        tile_block_oneshot<<<dim3((unsigned)((int64_t)K * rows / 256)), dim3(BLOCK), 0, s>>>(d, rows, cpr, 7);
     } else {
         tile_oneshot<<<dim3((unsigned)((int64_t)K * rows / 256)), dim3(BLOCK), 0, s>>>(d, rows, cpr, 7);
     }
