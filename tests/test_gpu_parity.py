@@ -727,3 +727,41 @@ def test_acenv_error_does_not_count_a_step():
     assert not t and env.count_steps == 1
     s, r, d, t, info = env.step(4)
     assert t and env.count_steps == 2
+
+
+def test_headline_rollout_every_env_vs_oracle():
+    """The driver's headline workload exactly (BASELINE configs[2]: bench.py's 2^20 Miller-Schupp
+    starts, L = 36, horizon 200, one ops.RolloutPlan launch of K = 20 steps with the full int32
+    obs trajectory), checked on EVERY env and step against the C oracle's batched ACEnv.step
+    with same-step autoreset: obs rows, rewards, done and truncated flags, final state and counts."""
+    import bench
+    from acx import ops
+    L, B, K, H = 36, 1 << 20, 20, 200
+    init = bench.ms_starts(L, B)
+    starts = torch.as_tensor(init).to(DEV)
+    state = starts.clone()
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(0)
+    acts = torch.randint(0, 12, (K, B), dtype=torch.int32, device=DEV, generator=g)
+    obs = torch.empty((K, B, 2 * L), dtype=torch.int32, device=DEV)
+    rew = torch.empty((K, B), dtype=torch.int32, device=DEV)
+    dn = torch.empty((K, B), dtype=torch.uint8, device=DEV)
+    tr = torch.empty((K, B), dtype=torch.uint8, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    ec = torch.zeros(1, dtype=torch.int32, device=DEV)
+    plan = ops.RolloutPlan(state, starts, cnt, T=K, horizon=H, cyclical=True, obs_traj=obs, reward_traj=rew,
+                           done_traj=dn, trunc_traj=tr, err=err, err_count=ec)
+    plan(acts)
+    torch.cuda.synchronize()
+    s = init.copy()
+    c = np.zeros(B, np.int32)
+    A = acts.cpu().numpy()
+    for t in range(K):
+        r, d_, t_, e, _, _ = O.env_step(s, A[t], L, H, c, reset_state=init)
+        assert not e.any()
+        assert np.array_equal(obs[t].cpu().numpy(), s), t
+        assert np.array_equal(rew[t].cpu().numpy(), r), t
+        assert np.array_equal(dn[t].cpu().numpy(), d_) and np.array_equal(tr[t].cpu().numpy(), t_), t
+    assert np.array_equal(state.cpu().numpy(), s) and np.array_equal(cnt.cpu().numpy(), c)
+    assert int(ec.item()) == 0
