@@ -765,3 +765,28 @@ def test_headline_rollout_every_env_vs_oracle():
         assert np.array_equal(dn[t].cpu().numpy(), d_) and np.array_equal(tr[t].cpu().numpy(), t_), t
     assert np.array_equal(state.cpu().numpy(), s) and np.array_equal(cnt.cpu().numpy(), c)
     assert int(ec.item()) == 0
+
+
+def test_config5_shard_every_env_vs_oracle():
+    """BASELINE configs[4]'s per-GPU shard (2^20 envs, L = 128, Miller-Schupp starts, random moves,
+    horizon 200) through VecACEnv.step -- acx_step_lengths once the rows' lengths are current --
+    on every env and step against the C oracle: states, rewards, flags and the carried lengths."""
+    import bench
+    from acx import VecACEnv
+    L, B, K, H = 128, 1 << 20, 8, 200
+    init = bench.ms_starts(L, B)
+    env = VecACEnv(init, horizon_length=H, device=DEV, track_final_obs=False)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    s = init.copy()
+    c = np.zeros(B, np.int32)
+    for t in range(K):
+        a = torch.randint(0, 12, (B,), dtype=torch.int32, device=DEV, generator=g)
+        st, rew, dn, tr, _ = env.step(a)
+        r, d_, t_, e, lens, _ = O.env_step(s, a.cpu().numpy(), L, H, c, reset_state=init)
+        assert not e.any()
+        assert np.array_equal(st.cpu().numpy(), s), t
+        assert np.array_equal(rew.cpu().numpy(), r), t
+        assert np.array_equal(dn.cpu().numpy(), d_) and np.array_equal(tr.cpu().numpy(), t_), t
+        assert np.array_equal(env.lengths.cpu().numpy(), lens), t
+    assert np.array_equal(env.step_count.cpu().numpy(), c)
