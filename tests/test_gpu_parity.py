@@ -790,3 +790,39 @@ def test_config5_shard_every_env_vs_oracle():
         assert np.array_equal(dn.cpu().numpy(), d_) and np.array_equal(tr.cpu().numpy(), t_), t
         assert np.array_equal(env.lengths.cpu().numpy(), lens), t
     assert np.array_equal(env.step_count.cpu().numpy(), c)
+
+
+def test_config2_full_horizon_every_env_vs_oracle():
+    """BASELINE configs[1] as bench.py's config2_step runs it: 65,536 Miller-Schupp starts, L = 36,
+    horizon 200, 200 per-call in-place steps through ops.StepPlan (the small-batch step kernel),
+    through one synchronised truncation -- every env and step against the C oracle."""
+    import bench
+    from acx import ops
+    L, B, K, H = 36, 65536, 200, 200
+    init = bench.ms_starts(L, B)
+    starts = torch.as_tensor(init).to(DEV)
+    st = starts.clone()
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    rew = torch.empty(B, dtype=torch.int32, device=DEV)
+    dn = torch.empty(B, dtype=torch.uint8, device=DEV)
+    tr = torch.empty(B, dtype=torch.uint8, device=DEV)
+    lens = torch.empty((B, 2), dtype=torch.int32, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    step = ops.StepPlan(st, state_out=st, reset_state=starts, step_count=cnt, horizon=H, cyclical=True, reward=rew,
+                        done=dn, truncated=tr, lengths=lens, err=err)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(0)
+    acts = torch.randint(0, 12, (K, B), dtype=torch.int32, device=DEV, generator=g)
+    A = acts.cpu().numpy()
+    s = init.copy()
+    c = np.zeros(B, np.int32)
+    n_trunc = 0
+    for t in range(K):
+        step(acts[t])
+        r, d_, t_, e, ln, _ = O.env_step(s, A[t], L, H, c, reset_state=init)
+        assert not e.any()
+        assert np.array_equal(st.cpu().numpy(), s), t
+        assert np.array_equal(rew.cpu().numpy(), r) and np.array_equal(dn.cpu().numpy(), d_), t
+        assert np.array_equal(tr.cpu().numpy(), t_) and np.array_equal(lens.cpu().numpy(), ln), t
+        n_trunc += int(t_.sum())
+    assert n_trunc > B // 2  # the horizon's synchronised truncation was stepped through
