@@ -143,7 +143,6 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
     if batch is None:
         batch = 65536 if mode == BFS else 512
     try:
-        parent_keys = np.zeros((batch, kw), dtype=np.uint64)
         pinned_in = torch.empty((batch, kw), dtype=torch.int64).pin_memory()
         pinned_out = torch.empty((batch, 12, kw), dtype=torch.int64).pin_memory()
         G = len(devs)
@@ -159,11 +158,11 @@ def run_search(mode, presentation, max_nodes_to_explore, verbose, cyclical, devi
         # kernel-only share of gpu_roundtrip_s (which adds the H2D / D2H copies and the waits)
         kev = []
         while status == 0:
-            n = lib.acx_search_next_batch(h, parent_keys.ctypes.data, batch)
+            # the engine writes the parents' keys straight into the pinned staging buffer
+            n = lib.acx_search_next_batch(h, pinned_in.data_ptr(), batch)
             if n == 0:
                 break
             g0 = time.perf_counter()
-            pinned_in[:n].numpy()[:] = parent_keys[:n].view(np.int64)
             # contiguous parent slices, one per GPU, launched asynchronously on each GPU's stream
             bounds = [n * g // G for g in range(G + 1)]
             for g, d in enumerate(devs):
