@@ -125,6 +125,27 @@ __global__ __launch_bounds__(256) void tile_block(int4* __restrict__ dst, int64_
     }
 }
 
+// tile's pattern with each wave's store sequence rotated: wave w starts its slice at chunk
+// ((w * ROT) mod 64 * 64) and wraps, so the waves writing in step do not all write the same
+// offset of their 18 KB slices at once (slices 18 KB apart give few distinct low-address
+// classes for a given offset: a channel hot spot while the waves are in step)
+__global__ __launch_bounds__(256) void tile_rot(int4* __restrict__ dst, int64_t rows, int cpr, int K, int rot, int v) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t r0 = w * WAVE;
+    if (r0 >= rows) return;
+    const int nch = WAVE * cpr;
+    const int start = (int)((w * rot) % cpr) * WAVE;  // in chunks, a whole store instruction
+    for (int t = 0; t < K; ++t) {
+        int4* row = dst + ((int64_t)t * rows + r0) * cpr;
+        for (int i = 0; i < nch; i += WAVE) {
+            int c = start + i + lane;
+            if (c >= nch) c -= nch;
+            st_nt(row + c, make_int4(v, t, c, lane));
+        }
+    }
+}
+
 // tile_block's slices written once each by short-lived blocks, step-major
 __global__ __launch_bounds__(256) void tile_block_oneshot(int4* __restrict__ dst, int64_t rows, int cpr, int v) {
     const int64_t blocks_per_step = rows / 256;
@@ -168,6 +189,8 @@ int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin
     } else if (kind == 6) {
         if (n) tile_block<1><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
         else tile_block<0><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
+    } else if (kind == 8) {
+        tile_rot<<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, n, 7);
     } else if (kind == 7) {
         tile_block_oneshot<<<dim3((unsigned)((int64_t)K * rows / 256)), dim3(BLOCK), 0, s>>>(d, rows, cpr, 7);
     } else {
