@@ -146,6 +146,23 @@ __global__ __launch_bounds__(256) void tile_rot(int4* __restrict__ dst, int64_t 
     }
 }
 
+// tile's pattern with the waves out of step: wave w writes its slices of steps t0, t0 + 1, ...
+// (mod K) with t0 = (w * 7) mod K, so the waves writing at a given moment spread over the K step
+// rows instead of all writing the same one
+__global__ __launch_bounds__(256) void tile_desync(int4* __restrict__ dst, int64_t rows, int cpr, int K, int v) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t r0 = w * WAVE;
+    if (r0 >= rows) return;
+    const int nch = WAVE * cpr;
+    const int t0 = (int)((w * 7) % K);
+    for (int i = 0; i < K; ++i) {
+        const int t = t0 + i < K ? t0 + i : t0 + i - K;
+        int4* row = dst + ((int64_t)t * rows + r0) * cpr;
+        for (int c = lane; c < nch; c += WAVE) st_nt(row + c, make_int4(v, t, c, lane));
+    }
+}
+
 // tile_block's slices written once each by short-lived blocks, step-major
 __global__ __launch_bounds__(256) void tile_block_oneshot(int4* __restrict__ dst, int64_t rows, int cpr, int v) {
     const int64_t blocks_per_step = rows / 256;
@@ -189,6 +206,8 @@ int probe_store(int kind, int n, void* buf, int64_t rows, int L, int K, int spin
     } else if (kind == 6) {
         if (n) tile_block<1><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
         else tile_block<0><<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
+    } else if (kind == 9) {
+        tile_desync<<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, 7);
     } else if (kind == 8) {
         tile_rot<<<dim3(tiles), dim3(BLOCK), 0, s>>>(d, rows, cpr, K, n, 7);
     } else if (kind == 7) {

@@ -71,6 +71,7 @@ def main():
     cases += [(f"tile_cpol{pol}", (5, pol, 0)) for pol in (0, 1, 2, 16, 17, 18)]
     cases += [("tile_block", (6, 0, 0)), ("tile_block_sync", (6, 1, 0)), ("tile_block_oneshot", (7, 0, 0))]
     cases += [(f"tile_rot{r}", (8, r, 0)) for r in (1, 5, 7)]
+    cases += [("tile_desync", (9, 0, 0))]
     ms = {c: [] for c, _ in cases}
     for rep in range(a.reps + 1):
         for name, c in cases:
