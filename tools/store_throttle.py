@@ -40,8 +40,10 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--spin", default="0,200")
     ap.add_argument("--throttle", default="0,1,2,4,8,16", type=lambda x: [int(v) for v in x.split(",")])
+    ap.add_argument("--K", type=int, default=20, help="steps per launch (trajectory rows K x B)")
+    ap.add_argument("--only", default="", help="comma-separated case names to run (default: all)")
     a = ap.parse_args()
-    K, B, L, H = 20, 1 << 20, 36, 200
+    K, B, L, H = a.K, 1 << 20, 36, 200
     dev = torch.device("cuda:0")
     P = lib()
     import acx  # noqa: F401
@@ -63,7 +65,7 @@ def main():
     resident = props.multi_processor_count * 8  # 8 blocks of 4 waves per CU = 8 waves per SIMD
     nbytes = obs.numel() * 4
     spins = [int(x) for x in a.spin.split(",")]
-    cases = [("rollout_k20", None)]
+    cases = [(f"rollout_k{K}", None)]
     cases += [("fill_oneshot", (0, 0, 0)), ("tile_oneshot", (3, 0, 0))]
     cases += [(f"fill_stride_n{n}", (1, n, 0)) for n in a.throttle]
     cases += [(f"tile_n{n}_spin{s}", (2, n, s)) for s in spins for n in a.throttle]
@@ -72,6 +74,9 @@ def main():
     cases += [("tile_block", (6, 0, 0)), ("tile_block_sync", (6, 1, 0)), ("tile_block_oneshot", (7, 0, 0))]
     cases += [(f"tile_rot{r}", (8, r, 0)) for r in (1, 5, 7)]
     cases += [("tile_desync", (9, 0, 0))]
+    if a.only:
+        keep = set(a.only.split(","))
+        cases = [(n, c) for n, c in cases if n in keep]
     ms = {c: [] for c, _ in cases}
     for rep in range(a.reps + 1):
         for name, c in cases:
@@ -91,10 +96,10 @@ def main():
             torch.cuda.synchronize()
             if rep:
                 ms[name].append(e0.elapsed_time(e1))
-    out = {"what": "tools/store_throttle.py: store patterns on one (20, 2^20, 72) int32 buffer (6.04 GB), "
+    out = {"what": f"tools/store_throttle.py: store patterns on one ({K}, 2^20, 72) int32 buffer, "
                    "interleaved, medians; TB/s = buffer bytes / time (the rollout also moves ~0.9 GB of "
                    "state / ids / rewards, not counted here)",
-           "resident_blocks": resident, "buffer_bytes": nbytes, "cases": {}}
+           "K": K, "resident_blocks": resident, "buffer_bytes": nbytes, "cases": {}}
     for name, v in ms.items():
         m = statistics.median(v)
         out["cases"][name] = {"ms": round(m, 4), "TBps": round(nbytes / m / 1e9, 3), "all_ms": [round(x, 4) for x in v]}
