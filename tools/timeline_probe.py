@@ -79,17 +79,20 @@ def main():
     ap.add_argument("--K", default="20,200")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--kinds", default="0,1,2")
+    ap.add_argument("--per-cu", default="8", help="persistent blocks per CU (4 waves each), comma-separated")
     a = ap.parse_args()
     P = lib()
     dev = torch.device("cuda:0")
     B, L = 1 << 20, 36
     out = []
-    grid = torch.cuda.get_device_properties(dev).multi_processor_count * 8  # 8 blocks of 4 waves per CU
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     ctr = torch.zeros(4, dtype=torch.int32, device=dev)
     for K in [int(k) for k in a.K.split(",")]:
         obs = torch.zeros((K, B, 2 * L), dtype=torch.int32, device=dev)
         s = torch.cuda.current_stream().cuda_stream
-        for kind in [int(k) for k in a.kinds.split(",")]:
+        runs = [(int(k), int(p)) for k in a.kinds.split(",") for p in (a.per_cu.split(",") if k != "0" else ["8"])]
+        for kind, per_cu in runs:
+            grid = ncu * per_cu  # persistent blocks of 4 waves, one per SIMD: per_cu waves per SIMD
             nb = B // 256 if kind == 0 else grid
             rec = torch.zeros((nb, 4), dtype=torch.int64, device=dev)
             steps = torch.zeros((nb, K), dtype=torch.int64, device=dev)
@@ -106,6 +109,7 @@ def main():
                 ms.append(e0.elapsed_time(e1))
             r = analyse(rec.cpu().numpy().view(np.uint64), steps.cpu().numpy().view(np.uint64), K, ms[-1], kind)
             r["event_ms_all"] = [round(m, 4) for m in ms]
+            r["blocks_per_cu"] = per_cu
             r["TBps"] = round(obs.numel() * 4 / (min(ms[1:] or ms) * 1e-3) / 1e12, 3)
             out.append(r)
             print(json.dumps(r), flush=True)
