@@ -80,11 +80,6 @@ constexpr int STAGE_UNROLL = 8;
 #ifndef ACX_OBS_SPLIT
 #define ACX_OBS_SPLIT 0
 #endif
-// the rollout as persistent waves taking 64-env tiles from a counter, this many 4-wave blocks per
-// CU (0: one block per 256 envs; A/B knob)
-#ifndef ACX_ROLLOUT_PERSIST
-#define ACX_ROLLOUT_PERSIST 0
-#endif
 // the step kernel's per-env scalar inputs (move id, step count) loaded before its tile (A/B knob)
 #ifndef ACX_EARLY_SCALARS
 #define ACX_EARLY_SCALARS 1
@@ -2569,8 +2564,11 @@ struct RolloutArgs {
 
 // OBS: 0 no trajectory, 1 int32 obs trajectory (obs_traj), 2 int8 obs trajectory (obs_traj8)
 template <int NW, int LC, int VEC, int OBS>
-__device__ __forceinline__ void rollout_tile(const RolloutArgs& a, char* smem, const WaveCtx& w) {
+__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_kernel(RolloutArgs a) {
     using Tile = TileFor<NW, LC, VEC>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    WaveCtx w;
+    if (!wave_ctx(a.B, w)) return;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2776,49 +2774,6 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs& a, char* smem, c
     tile.template store<true, ACX_NT_STATE != 0>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
                                                  w.lane, a.reset_state + w.r0 * twoL);
 }
-
-template <int NW, int LC, int VEC, int OBS>
-__global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_kernel(RolloutArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    WaveCtx w;
-    if (!wave_ctx(a.B, w)) return;
-    rollout_tile<NW, LC, VEC, OBS>(a, smem, w);
-}
-
-#if ACX_ROLLOUT_PERSIST
-// A/B only: persistent waves (ACX_ROLLOUT_PERSIST blocks per CU) that take 64-env tiles from a
-// counter, so the XCDs that write faster take more tiles and the launch ends without a tail of
-// late second-round blocks (tools/timeline_probe.py).  The last wave out resets the counter.
-__device__ unsigned g_rollout_ctr[2];
-template <int NW, int LC, int VEC, int OBS>
-__global__ __launch_bounds__(BLOCK, ACX_ROLLOUT_PERSIST) void rollout_persist_kernel(RolloutArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int64_t ntiles = (a.B + WAVE - 1) / WAVE;
-    const int lane = threadIdx.x & (WAVE - 1);
-    for (;;) {
-        unsigned tl = 0;
-        if (lane == 0) tl = atomicAdd(&g_rollout_ctr[0], 1u);
-        tl = __builtin_amdgcn_readfirstlane(tl);
-        if ((int64_t)tl >= ntiles) break;
-        WaveCtx w;
-        w.lane = lane;
-        w.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-        w.r0 = (int64_t)tl * WAVE;
-        w.R = (int)((a.B - w.r0) < WAVE ? (a.B - w.r0) : WAVE);
-        w.active = w.lane < w.R;
-        rollout_tile<NW, LC, VEC, OBS>(a, smem, w);
-        wave_sync();
-    }
-    __threadfence();
-    if (lane == 0) {
-        const unsigned n = atomicAdd(&g_rollout_ctr[1], 1u);
-        if (n == gridDim.x * (unsigned)WPB - 1u) {
-            atomicExch(&g_rollout_ctr[0], 0u);
-            atomicExch(&g_rollout_ctr[1], 0u);
-        }
-    }
-}
-#endif
 
 // Move ids (T, B) int32 -> (ceil(T/8), B) uint32, 8 consecutive steps of one env per word,
 // 4 bits each (ids outside [0,12) -> 15, ACX_ERR_ACTION).  The rollout then reads 0.5 B per
@@ -3426,18 +3381,6 @@ int launch_step(StepArgs a, hipStream_t s) {
 template <int NW, int LC, int VEC, int OBS>
 int launch_rollout(RolloutArgs a, hipStream_t s) {
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-#if ACX_ROLLOUT_PERSIST
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return ACX_E_LAUNCH;
-    }
-    const unsigned g = (unsigned)ncu * ACX_ROLLOUT_PERSIST, need = grid_for(a.B);
-    rollout_persist_kernel<NW, LC, VEC, OBS><<<dim3(g < need ? g : need), dim3(BLOCK), shm, s>>>(a);
-    return finish_launch();
-#endif
     rollout_kernel<NW, LC, VEC, OBS><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }
