@@ -10,8 +10,9 @@
 //   * the visited set -- the keys of all committed nodes live in HBM with a bucketed hash table
 //     (as in the device BFS); the expansion kernel probes it, so every child that is already a
 //     node (as of that round) comes back marked with the node's id and the host never looks it
-//     up.  Nodes the host appends are committed to the device table at the start of the next
-//     round.
+//     up.  Nodes the host appends are committed to the device table by the next round's launch,
+//     beside its expansion (one launch per round: the expansion trusts only the entries of
+//     earlier launches, and the host checks the children against the nodes committed with it).
 // The host replays the reference's order exactly: pops while the frontier's top has cached
 // children; a child the device did not know is checked only against the nodes appended since
 // its round (the in-flight conflicts), kept in a host table of the last 2^16..2^17 appended
@@ -70,10 +71,12 @@ struct DevArgs {
     int n, L, kw, cyc;
 };
 
-// lane per (parent, action): one move, the child's key, its hash, its id if already a node
+// lane per (parent, action): one move, the child's key, its hash, its id if it is a node below
+// a.lo (the nodes committed by earlier launches; greedy_round_kernel commits [lo, hi) in the same
+// launch, and those entries are skipped: their keys may still be in flight, and the host checks
+// every id >= lo itself)
 template <int NW>
-__global__ __launch_bounds__(256) void greedy_expand_kernel(DevArgs a) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void expand_lane(const DevArgs& a, int t) {
     if (t >= a.n * ACT) return;
     const int p = t / ACT, act = t - p * ACT;
     PresRegs<NW> q;
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(256) void greedy_expand_kernel(DevArgs a) {
                 }
                 if (((uint32_t)v & FP_MASK) == fp) {
                     const int64_t id = (int64_t)(v >> 24) - 1;
-                    if (keq<NW + 1>(a.nkeys + id * a.kw, kk, a.kw)) {
+                    if (id < a.lo && keq<NW + 1>(a.nkeys + id * a.kw, kk, a.kw)) {
                         known = id;
                         break;
                     }
@@ -127,8 +130,7 @@ __global__ __launch_bounds__(256) void greedy_expand_kernel(DevArgs a) {
 
 // commit the node ids [lo, hi): store their keys and enter them in the table (all distinct, new)
 template <int KWM>
-__global__ __launch_bounds__(256) void greedy_commit_kernel(DevArgs a) {
-    const int64_t id = a.lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void commit_lane(const DevArgs& a, int64_t id) {
     if (id >= a.hi) return;
     const Key<KWM> k = kload<KWM>(a.commit + (id - a.lo) * a.kw, a.kw);
 #pragma unroll
@@ -143,6 +145,23 @@ __global__ __launch_bounds__(256) void greedy_commit_kernel(DevArgs a) {
             if (atomicCAS((unsigned long long*)(bk + j), 0ull, (unsigned long long)my) == 0ull) return;
         b = (b + 1) & a.bmask;
     }
+}
+
+template <int KWM>
+__global__ __launch_bounds__(256) void greedy_commit_kernel(DevArgs a) {
+    commit_lane<KWM>(a, a.lo + (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+
+// one round in one launch: blocks [0, cblocks) commit the nodes [lo, hi) appended since the last
+// round, the others expand the round's parents against the nodes committed before (ids < lo).
+// The two halves touch disjoint key-store rows; a probe that meets a concurrent table insert
+// sees the slot empty or holding an id >= lo (skipped), and either way reaches every older entry.
+template <int NW>
+__global__ __launch_bounds__(256) void greedy_round_kernel(DevArgs a, int cblocks) {
+    if ((int)blockIdx.x < cblocks)
+        commit_lane<NW + 1>(a, a.lo + (int64_t)blockIdx.x * 256 + threadIdx.x);
+    else
+        expand_lane<NW>(a, ((int)blockIdx.x - cblocks) * 256 + threadIdx.x);
 }
 
 // host restatement of bfs::khash (the kernels' hash): the host tables index by it
@@ -183,7 +202,7 @@ struct Engine {
     int64_t gen_lo[2] = {0, 0};
     int cur = 0;
     uint64_t gmask = 0;
-    std::vector<int64_t> n_at_round;  // node count when round r's kernel probed the device table
+    std::vector<int64_t> n_at_round;  // round r: its kernel knew the ids below this; the host checks the rest
     int64_t committed = 0;            // ids < committed are in the device table
     int round = 0;
     // result (greedy.py:86-121)
@@ -680,12 +699,13 @@ struct Engine {
     }
 };
 
-struct ExpandLaunch {
+struct RoundLaunch {
     Engine* E;
     template <int NW>
     void go() {
         const int n = E->d.n * ACT;
-        greedy_expand_kernel<NW><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, E->stream>>>(E->d);
+        const int cb = (int)((E->d.hi - E->d.lo + 255) / 256);
+        greedy_round_kernel<NW><<<dim3((unsigned)(cb + (n + 255) / 256)), dim3(256), 0, E->stream>>>(E->d, cb);
     }
 };
 struct CommitLaunch {
@@ -707,33 +727,34 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
     const int64_t n_nodes = (int64_t)parent.size();
     if (n_nodes > dcap && !grow(std::min<int64_t>(cap, std::max<int64_t>(2 * dcap, n_nodes)))) return ACX_E_LAUNCH;
     // staging in: the batch's parent keys, then the keys of the nodes appended since the last
-    // round (committed to the device visited set before the expansion probes it)
+    // round.  The last commit_cap of those are committed by the round's own launch, beside the
+    // expansion (greedy_round_kernel), which therefore knows only the ids below them: the host
+    // checks the children against every node from there on (n_at_round)
     for (int i = 0; i < n; ++i) memcpy(h_in + (size_t)i * kw, &keys[(size_t)batch[i] * kw], 8 * kw);
     int64_t lo = committed;
-    while (true) {
-        const int64_t hi = std::min(n_nodes, lo + commit_cap);
-        uint64_t* cst = h_in + (size_t)n * kw;
-        if (hi > lo) memcpy(cst, &keys[(size_t)lo * kw], (size_t)(hi - lo) * kw * 8);
-        if (hi > lo) {
-            d.commit = hd_in + (size_t)n * kw;
-            d.lo = lo;
-            d.hi = hi;
-            commit_launch();
-        }
-        lo = hi;
-        if (lo >= n_nodes) break;
+    d.commit = hd_in + (size_t)n * kw;
+    while (n_nodes - lo > commit_cap) {  // a backlog beyond one launch's staging: commit ahead
+        memcpy(h_in + (size_t)n * kw, &keys[(size_t)lo * kw], (size_t)commit_cap * kw * 8);
+        d.lo = lo;
+        d.hi = lo + commit_cap;
+        commit_launch();
+        lo += commit_cap;
         if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return ACX_E_LAUNCH;  // h_in is reused
     }
+    if (n_nodes > lo) memcpy(h_in + (size_t)n * kw, &keys[(size_t)lo * kw], (size_t)(n_nodes - lo) * kw * 8);
+    d.lo = lo;
+    d.hi = n_nodes;
     committed = n_nodes;
-    n_at_round.push_back(n_nodes);
-    if (n == 0) return hipGetLastError() == hipSuccess ? wait() : ACX_E_LAUNCH;
+    n_at_round.push_back(lo);
     d.n = n;
     d.parents = hd_in;
     d.ckeys = hd_out;
     d.chash = hd_out + (size_t)n * ACT * kw;
     d.cknown = reinterpret_cast<int64_t*>(d.chash + (size_t)n * ACT);
-    ExpandLaunch el{this};
-    bfs::by_nw(L, el);
+    if (n == 0 && n_nodes == lo) return ACX_OK;
+    RoundLaunch rl{this};
+    bfs::by_nw(L, rl);
+    if (n == 0) return hipGetLastError() == hipSuccess ? wait() : ACX_E_LAUNCH;
     const int64_t tw = now_ns();
     if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return ACX_E_LAUNCH;
     const int64_t tc = now_ns();
