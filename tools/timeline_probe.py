@@ -71,7 +71,7 @@ def analyse(rec, steps, K, ev_ms, kind):
     return res
 
 
-KINDS = ["block_per_tile", "persistent_dynamic", "persistent_static"]
+KINDS = ["block_per_tile", "persistent_dynamic", "persistent_static", "block_per_tile_xcc_weighted", "block_per_ticket"]
 
 
 def main():
@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--kinds", default="0,1,2")
     ap.add_argument("--per-cu", default="8", help="persistent blocks per CU (4 waves each), comma-separated")
+    ap.add_argument("--odd-pct", default="100,78", help="kind 3: an odd XCC's tiles as a percentage of an even one's")
+    ap.add_argument("--over", default="100,125", help="kind 4: blocks launched as a percentage of the tiles")
     a = ap.parse_args()
     P = lib()
     dev = torch.device("cuda:0")
@@ -90,10 +92,11 @@ def main():
     for K in [int(k) for k in a.K.split(",")]:
         obs = torch.zeros((K, B, 2 * L), dtype=torch.int32, device=dev)
         s = torch.cuda.current_stream().cuda_stream
-        runs = [(int(k), int(p)) for k in a.kinds.split(",") for p in (a.per_cu.split(",") if k != "0" else ["8"])]
+        runs = [(int(k), int(p)) for k in a.kinds.split(",")
+                for p in ({"0": ["8"], "3": a.odd_pct.split(","), "4": a.over.split(",")}.get(k) or a.per_cu.split(","))]
         for kind, per_cu in runs:
-            grid = ncu * per_cu  # persistent blocks of 4 waves, one per SIMD: per_cu waves per SIMD
-            nb = B // 256 if kind == 0 else grid
+            grid = ncu * per_cu if kind in (1, 2) else per_cu  # persistent: per_cu waves per SIMD; kind 3: pct
+            nb = B // 256 if kind in (0, 3, 4) else grid
             rec = torch.zeros((nb, 4), dtype=torch.int64, device=dev)
             steps = torch.zeros((nb, K), dtype=torch.int64, device=dev)
             ms = []
@@ -109,7 +112,9 @@ def main():
                 ms.append(e0.elapsed_time(e1))
             r = analyse(rec.cpu().numpy().view(np.uint64), steps.cpu().numpy().view(np.uint64), K, ms[-1], kind)
             r["event_ms_all"] = [round(m, 4) for m in ms]
-            r["blocks_per_cu"] = per_cu
+            r["blocks_per_cu" if kind in (1, 2) else "param"] = per_cu
+            if kind == 4:
+                assert int(ctr[0].item()) == 0 and int(ctr[1].item()) == 0, "ticket counters not reset"
             r["TBps"] = round(obs.numel() * 4 / (min(ms[1:] or ms) * 1e-3) / 1e12, 3)
             out.append(r)
             print(json.dumps(r), flush=True)
