@@ -80,11 +80,6 @@ constexpr int STAGE_UNROLL = 8;
 #ifndef ACX_OBS_SPLIT
 #define ACX_OBS_SPLIT 0
 #endif
-// A/B knob: the rollout's 256-env blocks dealt unevenly to the XCDs, an odd XCC taking this
-// percentage of an even one's (0: one block per 256 envs, dealt round-robin by the dispatcher)
-#ifndef ACX_XCC_ODD_PCT
-#define ACX_XCC_ODD_PCT 0
-#endif
 // the step kernel's per-env scalar inputs (move id, step count) loaded before its tile (A/B knob)
 #ifndef ACX_EARLY_SCALARS
 #define ACX_EARLY_SCALARS 1
@@ -2565,7 +2560,6 @@ struct RolloutArgs {
     int64_t B;
     int T, L, horizon, cyclical;
     int8_t* obs_traj8;  // acx_rollout_obs8: the trajectory as int8 letters (obs_traj unused)
-    int xe, xo;         // A/B (ACX_XCC_ODD_PCT): 256-env blocks dealt per even / odd XCC (0: one per block)
 };
 
 // OBS: 0 no trajectory, 1 int32 obs trajectory (obs_traj), 2 int8 obs trajectory (obs_traj8)
@@ -2574,21 +2568,6 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     using Tile = TileFor<NW, LC, VEC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
-#if ACX_XCC_ODD_PCT
-    if (a.xe) {
-        // block b runs on XCC b % 8 (the dispatcher's round-robin); XCC x takes a contiguous range
-        // of xe (even x) or xo (odd x) 256-env blocks, the blocks beyond its quota exit
-        const int x = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
-        if (j >= ((x & 1) ? a.xo : a.xe)) return;
-        const int64_t blk = (int64_t)((x + 1) / 2) * a.xe + (int64_t)(x / 2) * a.xo + j;
-        w.lane = threadIdx.x & (WAVE - 1);
-        w.wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-        w.r0 = (blk * WPB + w.wid) * WAVE;
-        if (w.r0 >= a.B) return;
-        w.R = (int)((a.B - w.r0) < WAVE ? (a.B - w.r0) : WAVE);
-        w.active = w.lane < w.R;
-    } else
-#endif
     if (!wave_ctx(a.B, w)) return;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
@@ -3402,17 +3381,6 @@ int launch_step(StepArgs a, hipStream_t s) {
 template <int NW, int LC, int VEC, int OBS>
 int launch_rollout(RolloutArgs a, hipStream_t s) {
     const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
-#if ACX_XCC_ODD_PCT
-    const int64_t tiles = grid_for(a.B);
-    if (tiles >= 64) {
-        // 4 xe + 4 xo >= tiles, xo = xe * pct / 100
-        a.xe = (int)((tiles * 100 + 4 * (100 + ACX_XCC_ODD_PCT) - 1) / (4 * (100 + ACX_XCC_ODD_PCT)));
-        a.xo = (int)((tiles - 4 * (int64_t)a.xe + 3) / 4);
-        if (a.xo < 0) a.xo = 0;
-        rollout_kernel<NW, LC, VEC, OBS><<<dim3((unsigned)(8 * a.xe)), dim3(BLOCK), shm, s>>>(a);
-        return finish_launch();
-    }
-#endif
     rollout_kernel<NW, LC, VEC, OBS><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
     return finish_launch();
 }
