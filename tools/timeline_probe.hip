@@ -156,6 +156,46 @@ __global__ __launch_bounds__(256) void tile_ticket(int4* __restrict__ dst, int64
     }
 }
 
+// One block per tile (kind 0), but a wave's issue priority falls with its progress (s_setprio
+// 3 at the start, 0 in its last quarter of steps): the arbiter serves the waves that are behind
+// first instead of the oldest, so a SIMD's waves advance together
+__device__ __forceinline__ void set_prio(int q) {
+    switch (q) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+__global__ __launch_bounds__(256) void tile_fair(int4* __restrict__ dst, int64_t rows, int cpr, int K, int mode,
+                                                 uint64_t* __restrict__ rec, uint64_t* __restrict__ steps) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wid) * WAVE;
+    const int nch = WAVE * cpr;
+    if (r0 < rows) {
+        for (int t = 0; t < K; ++t) {
+            // mode 1: by progress quarter; mode 2: young waves first (3 for the whole wave's life
+            // after its first step, so a new wave overtakes the old ones); mode 3: plain 0..3 by
+            // block index (a fixed random-ish order)
+            if (mode == 1) set_prio((4 * t) / K);
+            else if (mode == 2) set_prio(t == 0 ? 3 : 0);
+            else set_prio((int)(blockIdx.x * 7 % 4));
+            if (wid == 0 && lane == 0) steps[(int64_t)blockIdx.x * K + t] = __builtin_amdgcn_s_memrealtime();
+            int4* row = dst + ((int64_t)t * rows + r0) * cpr;
+            for (int c = lane; c < nch; c += WAVE) st_nt(row + c, make_int4(7, t, c, lane));
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        rec[4 * blockIdx.x + 0] = t_start;
+        rec[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        rec[4 * blockIdx.x + 2] = xcc_id();
+        rec[4 * blockIdx.x + 3] = 0;
+    }
+}
+
 // kind 0: one block per tile (the rollout's launch); 1: persistent blocks, dynamic tiles;
 // 2: persistent blocks, static tiles; 3: one block per tile, odd XCCs dealt grid/100 % of an even
 // XCC's tiles (grid = that percentage here).  grid: persistent blocks (rec / steps sized for the larger)
@@ -167,6 +207,9 @@ extern "C" int timeline_tile(int kind, void* buf, int64_t rows, int L, int K, in
     if (kind == 0) {
         tile_timed<<<dim3((unsigned)(rows / 256)), dim3(256), 0, s>>>((int4*)buf, rows, cpr, K, (uint64_t*)rec,
                                                                        (uint64_t*)steps);
+    } else if (kind == 5) {
+        tile_fair<<<dim3((unsigned)(rows / 256)), dim3(256), 0, s>>>((int4*)buf, rows, cpr, K, grid, (uint64_t*)rec,
+                                                                     (uint64_t*)steps);
     } else if (kind == 4) {
         const unsigned tiles = (unsigned)(rows / 256);
         tile_ticket<<<dim3((unsigned)((uint64_t)tiles * grid / 100)), dim3(256), 0, s>>>(

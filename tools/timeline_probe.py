@@ -71,7 +71,8 @@ def analyse(rec, steps, K, ev_ms, kind):
     return res
 
 
-KINDS = ["block_per_tile", "persistent_dynamic", "persistent_static", "block_per_tile_xcc_weighted", "block_per_ticket"]
+KINDS = ["block_per_tile", "persistent_dynamic", "persistent_static", "block_per_tile_xcc_weighted", "block_per_ticket",
+         "block_per_tile_prio"]
 
 
 def main():
@@ -82,6 +83,7 @@ def main():
     ap.add_argument("--per-cu", default="8", help="persistent blocks per CU (4 waves each), comma-separated")
     ap.add_argument("--odd-pct", default="100,78", help="kind 3: an odd XCC's tiles as a percentage of an even one's")
     ap.add_argument("--over", default="100,125", help="kind 4: blocks launched as a percentage of the tiles")
+    ap.add_argument("--prio", default="1,2,3", help="kind 5: priority modes (1 by progress, 2 young first, 3 fixed)")
     a = ap.parse_args()
     P = lib()
     dev = torch.device("cuda:0")
@@ -93,10 +95,10 @@ def main():
         obs = torch.zeros((K, B, 2 * L), dtype=torch.int32, device=dev)
         s = torch.cuda.current_stream().cuda_stream
         runs = [(int(k), int(p)) for k in a.kinds.split(",")
-                for p in ({"0": ["8"], "3": a.odd_pct.split(","), "4": a.over.split(",")}.get(k) or a.per_cu.split(","))]
+                for p in ({"0": ["8"], "3": a.odd_pct.split(","), "4": a.over.split(","), "5": a.prio.split(",")}.get(k) or a.per_cu.split(","))]
         for kind, per_cu in runs:
-            grid = ncu * per_cu if kind in (1, 2) else per_cu  # persistent: per_cu waves per SIMD; kind 3: pct
-            nb = B // 256 if kind in (0, 3, 4) else grid
+            grid = ncu * per_cu if kind in (1, 2) else per_cu  # persistent: per_cu waves per SIMD; else the kind's parameter
+            nb = B // 256 if kind in (0, 3, 4, 5) else grid
             rec = torch.zeros((nb, 4), dtype=torch.int64, device=dev)
             steps = torch.zeros((nb, K), dtype=torch.int64, device=dev)
             ms = []
