@@ -362,6 +362,35 @@ struct Engine {
             pos += nbits;
         };
         constexpr uint64_t PAD20 = 0x492492492492492ull >> 0;  // 20 x 010 (60 bits): padding letters
+        if (L <= 40) {
+            // a relator's 2L code bits are taken in one 128-bit shift and mapped 4 letters per
+            // table lookup into two 60-bit parts (letters 0..19, 20..L-1); the padding letters'
+            // fields replaced by 010s with one mask per part -- a few appends instead of one per
+            // 4 letters (the general path below, which this reproduces bit for bit)
+            using u128 = unsigned __int128;
+            for (int h = 0; h < 2; ++h) {
+                const int n = len_field(k, h);
+                const int b0 = 2 * h * L, w = b0 >> 6, o = b0 & 63;
+                u128 codes = ((u128)k[w] | ((u128)(w + 1 < kw ? k[w + 1] : 0ull) << 64)) >> o;
+                if (o + 2 * L > 128 && w + 2 < kw) codes |= (u128)k[w + 2] << (128 - o);
+                auto part = [&](int f, int cnt) -> uint64_t {  // letters [f, f + cnt), cnt <= 20
+                    const int groups = (cnt + 3) / 4;
+                    uint64_t v = 0;
+                    for (int g = 0; g < groups; ++g) v = (v << 12) | tbl[(uint32_t)(codes >> (2 * f + 8 * g)) & 0xffu];
+                    v >>= 3 * (4 * groups - cnt);  // the letters past the part in its last group
+                    const int live = n - f < 0 ? 0 : (n - f > cnt ? cnt : n - f);
+                    if (live < cnt) {
+                        const uint64_t mask = (1ull << (3 * (cnt - live))) - 1;
+                        v = (v & ~mask) | (PAD20 & mask);
+                    }
+                    return v;
+                };
+                const int c0 = L < 20 ? L : 20;
+                put(part(0, c0), 3 * c0);
+                if (L > 20) put(part(20, L - 20), 3 * (L - 20));
+            }
+            return;
+        }
         for (int h = 0; h < 2; ++h) {
             const int n = len_field(k, h);
             int i = 0;
