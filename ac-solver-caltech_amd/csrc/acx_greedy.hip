@@ -179,6 +179,7 @@ static inline int64_t now_ns() {
 struct Engine {
     int L = 0, kw = 0, pk = 0, cyc = 0, dev = 0;
     int64_t max_nodes = 0, cap = 0;
+    bool prio_generic = false;  // tests only (acx_internal_greedy_prio_key): the per-group priority key
     int64_t dcap = 0;  // nodes the device key store / visited set hold now (grown by doubling)
     uint64_t tsize = 0;
     int batch_cap = DEFAULT_BATCH;
@@ -362,7 +363,7 @@ struct Engine {
             pos += nbits;
         };
         constexpr uint64_t PAD20 = 0x492492492492492ull >> 0;  // 20 x 010 (60 bits): padding letters
-        if (L <= 40) {
+        if (L <= 40 && !prio_generic) {
             // a relator's 2L code bits are taken in one 128-bit shift and mapped 4 letters per
             // table lookup into two 60-bit parts (letters 0..19, 20..L-1); the padding letters'
             // fields replaced by 010s with one mask per part -- a few appends instead of one per
@@ -847,6 +848,20 @@ void acx_internal_greedy_age(int32_t log2_age) { g_age_override = log2_age > 0 ?
 // tests only: searches started afterwards begin with a 2^log2_cap-node device store (0: INIT_DCAP),
 // so the store's regrowth mid-search is exercised at test sizes
 void acx_internal_greedy_init_cap(int32_t log2_cap) { g_dcap_override = log2_cap > 0 ? (int64_t)1 << log2_cap : 0; }
+// tests only (host code, no GPU): the heap priority key of a packed key at L (out: the key's
+// words, (40 + 6L + 63) / 64 of them), through the fast path (generic = 0, L <= 40) or the
+// per-group one; returns the number of words, -1 on bad arguments
+int32_t acx_internal_greedy_prio_key(int32_t L, const uint64_t* key, int32_t total, int32_t depth, uint64_t* out,
+                                     int32_t generic) {
+    if (L < 1 || L > ACX_MAX_L || !key || !out) return -1;
+    Engine e;
+    e.L = L;
+    e.kw = acx_key_words(L);
+    e.pk = (HDR + 6 * L + 63) / 64;
+    e.prio_generic = generic != 0;
+    e.prio_key(key, total, depth, out);
+    return e.pk;
+}
 
 // 0 running, 1 success, 2 failed, 3 move error; budget_hit, min_length, nodes (len(tree_nodes))
 int32_t acx_greedy_status(void* h, int32_t* budget_hit, int32_t* min_length, int64_t* n_nodes) {

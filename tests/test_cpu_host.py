@@ -181,6 +181,38 @@ def test_key_packing_roundtrip():
             assert np.array_equal(_unpack_key_host(E._pack_key(s, L), L), s)
 
 
+def test_greedy_priority_key():
+    """The device greedy's heap key (csrc/acx_greedy.hip prio_key, host code): total (9 bits) |
+    path length (31) | every letter + 2 in 3 bits, MSB first, so that word order is the order of
+    the reference's heap tuples (total, path length, state tuple), greedy.py:55-64,104-113.  The
+    fast path (L <= 40) and the per-group one against that definition, on random presentations."""
+    import ctypes
+    lib = _lib.load()
+    hook = lib.acx_internal_greedy_prio_key
+    hook.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                     ctypes.c_int32]
+    hook.restype = ctypes.c_int32
+    rng = np.random.default_rng(1)
+    for L in list(range(1, 43)) + [64, 128]:
+        pk = (40 + 6 * L + 63) // 64
+        for _ in range(40):
+            s = np.zeros(2 * L, np.int64)
+            for h in range(2):
+                n = int(rng.integers(0, L + 1))
+                s[h * L : h * L + n] = rng.choice([1, -1, 2, -2], size=n)
+            tot, dep = int(rng.integers(0, 512)), int(rng.integers(0, 1 << 31))
+            v = (tot << 31) | dep
+            for x in s:
+                v = (v << 3) | int(x + 2)
+            v <<= 64 * pk - (40 + 6 * L)
+            want = [(v >> (64 * (pk - 1 - i))) & ((1 << 64) - 1) for i in range(pk)]
+            key = np.ascontiguousarray(E._pack_key(s, L), dtype=np.uint64)
+            for generic in (0, 1):
+                out = np.zeros(pk + 1, np.uint64)
+                assert hook(L, key.ctypes.data, tot, dep, out.ctypes.data, generic) == pk
+                assert [int(w) for w in out[:pk]] == want, (L, generic, s.tolist())
+
+
 def test_search_engine_name_is_validated():
     """A misspelt engine raises instead of silently running another engine."""
     ak2 = np.array([1, 1, -2, -2, -2, 0, 0, 1, 2, 1, -2, -1, -2, 0])
