@@ -26,7 +26,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from .. import _lib
+from .. import _lib, ops
 from ..envs.ac_env import VecACEnv
 
 
@@ -95,7 +95,7 @@ class LearnerEnv:
             a64 = action.to(torch.int64)
         v = self.vec
         v._lengths_ok = False  # the learner step does not write the vector env's lengths
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = ops._stream(dev)
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         if fused:
             st = lib.acx_learner_step(

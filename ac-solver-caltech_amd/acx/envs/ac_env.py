@@ -336,7 +336,7 @@ class VecACEnv:
                 or actions.shape != (self.num_envs,)):
             actions = actions.to(self.device, torch.int32).contiguous().reshape(self.num_envs)
         s_in, s_out, rs, cnt, rew, dn, tr, ln, fo, err, ec = self._step_args()
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = ops._stream(self.device)
         if self.autoreset_mode == "next_step":
             rec = self.record_actions
             st = self._lib.acx_step_next(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln,

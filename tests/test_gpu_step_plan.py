@@ -72,3 +72,34 @@ def test_step_plan_argument_errors():
     with pytest.raises(ValueError):
         ops.StepPlan(st, state_out=starts.clone(), lengths=torch.zeros((B, 2), dtype=torch.int32, device=DEV),
                      lengths_in=True)
+
+
+def test_stream_handle_is_the_current_stream():
+    """ops._stream (the raw current-stream getter every launch uses) names the stream torch
+    considers current on the device -- the default one and one entered with torch.cuda.stream --
+    and a StepPlan call inside a side stream runs there (its result is ready once that stream is
+    synchronised, whatever the default stream does)."""
+    from acx import ops
+    assert ops._stream(DEV) == torch.cuda.current_stream(DEV).cuda_stream
+    assert ops._stream(torch.device("cuda")) == torch.cuda.current_stream().cuda_stream
+    side = torch.cuda.Stream(device=DEV)
+    with torch.cuda.stream(side):
+        assert ops._stream(DEV) == side.cuda_stream
+    assert ops._stream(DEV) == torch.cuda.current_stream(DEV).cuda_stream
+    L, B = 36, 4096
+    starts = torch.as_tensor(_ms_states(L, B)).to(DEV)
+    a = _bufs(B, L, starts)
+    b = _bufs(B, L, starts)
+    act = torch.randint(0, 12, (B,), dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    pa = ops.StepPlan(a["state"], reset_state=starts, step_count=a["cnt"], horizon=200, reward=a["rew"])
+    pb = ops.StepPlan(b["state"], reset_state=starts, step_count=b["cnt"], horizon=200, reward=b["rew"])
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        for _ in range(5):
+            pa(act)
+    for _ in range(5):
+        pb(act)
+    side.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(a["state"], b["state"]) and torch.equal(a["rew"], b["rew"])
