@@ -362,6 +362,7 @@ class StepPlan:
                 (err_count, "err_count", _INT32, (1,))):
             _check(t, name, dt, shape, dev)
         self.B, self.L, self.device, self.state_out = B, L, dev, state_out
+        self._didx = dev.index if dev.index is not None else torch.cuda.current_device()
         self._ashape = torch.Size((B,))
         self._keep = (state_in, state_out, reset_state, step_count, reward, done, truncated, lengths, final_obs, err,
                       err_count)
@@ -381,13 +382,14 @@ class StepPlan:
 
     def __call__(self, action: torch.Tensor) -> torch.Tensor:
         """One env step with `action` ((B,) int32, contiguous, on the plan's device)."""
-        if (action.shape != self._ashape or action.dtype != _INT32 or action.device != self.device
+        if (action.shape != self._ashape or action.dtype != _INT32 or action.get_device() != self._didx
                 or not action.is_contiguous()):
             raise ValueError(f"action must be a contiguous int32 tensor of shape {tuple(self._ashape)} on "
                              f"{self.device}, got {action.dtype} {tuple(action.shape)} on {action.device}")
         if self.B:
-            s = _stream(self.device)
-            _lib.check(self._fn(*self._head, action.data_ptr(), *self._tail, s), self._name)
+            rc = self._fn(*self._head, action.data_ptr(), *self._tail, _stream(self.device))
+            if rc:
+                _lib.check(rc, self._name)
         return self.state_out
 
 
