@@ -71,28 +71,15 @@ __device__ __forceinline__ int4 widen4(uint32_t p) {
 
 
 constexpr int STAGE_UNROLL = 8;
-// the step kernel's CodeTile (L = 128) full-tile loads software-pipelined across batches (A/B knob)
-#ifndef ACX_PIPE_LOAD
-#define ACX_PIPE_LOAD 1
-#endif
-// the rollout's int32 observation store split in two halves: step t's second half is issued at
-// the top of step t + 1, ahead of that step's move (FastTile only; A/B knob)
-#ifndef ACX_OBS_SPLIT
-#define ACX_OBS_SPLIT 0
-#endif
-// the step kernel's per-env scalar inputs (move id, step count) loaded before its tile (A/B knob)
-#ifndef ACX_EARLY_SCALARS
-#define ACX_EARLY_SCALARS 1
-#endif
-// Non-temporal (streaming) stores for the rollout's write-once trajectory outputs: the
-// obs trajectory with them is 1.4 % faster (B = 2^20, L = 36, T = 200: 10.08 vs 10.22 ms,
-// tools/ab_libs.py); for reward/done/truncated they cost 0.4 %, so those stay plain.
-#ifndef ACX_NT_OBS
-#define ACX_NT_OBS 1
-#endif
-#ifndef ACX_NT_SCALARS
-#define ACX_NT_SCALARS 0
-#endif
+// Cache-policy choices, each settled by an interleaved A/B on one buffer set (the measurements
+// are cited where each is used; the losing variants live in commit history, not here):
+//   * the rollout's write-once trajectory: non-temporal / sc1 stores (1.4 % faster at T = 200);
+//     its reward/done/truncated stay plain (non-temporal cost 0.4 %);
+//   * the in-place step's write-back of changed relators: non-temporal (L = 36) or an sc1
+//     buffer store (L = 128); whole output rows stay plain;
+//   * tile loads: non-temporal for the L = 128 step and the rollout's state in, plain for the
+//     L = 36 step; expand12's parent loads and key stores non-temporal.
+constexpr bool NT_OBS = true;
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 template <bool NT>
@@ -149,64 +136,37 @@ __device__ __forceinline__ void pack4_codes(uint32_t d, uint32_t& c8, uint32_t& 
     nz4 = __builtin_amdgcn_udot4(nz, 0x08040201u, 0u, false);
 }
 
-// the step kernel's L = 128 tile load: chunks converted by chunk_i8 into a lane-fixed slot
-// address, rows flagged from one wave-wide bad mask at the end (A/B knob: 0 = the per-letter
-// to_i8 conversion and a per-chunk flag store)
-// Non-temporal stores for the in-place step's write-back of changed relators (`ACX_NT_WRITEBACK`):
-// nothing reads those lines again inside the launch, and plain stores kept them in L2 beside the
-// tile loads (same buffers: L = 128 0.2727 -> 0.2581 ms, lengths-carrying 0.2302 -> 0.2102, L = 36
-// 0.0742 -> 0.0697; profiles/r04/r04z_ab_nt*.json).  Whole output rows (`ACX_NT_STATE`: the
-// out-of-place step, the rollout's final state, canonicalized rows, expanded children) stay plain:
-// non-temporal made the rollout slower (K = 20 int32 1.332 -> 1.351 ms, int8 0.447 -> 0.477; its
-// next launch reads that state) and expand12's children no faster (0.778 -> 0.772 ms).
-#ifndef ACX_NT_WRITEBACK
-#define ACX_NT_WRITEBACK 1
-#endif
-#ifndef ACX_NT_STATE
-#define ACX_NT_STATE 0
-#endif
-// The L = 128 in-place step's write-back (CodeTile) through a buffer store with this cache policy
-// (-1: the global store of ACX_NT_WRITEBACK).  sc1 (16), same buffers: lengths-carrying 0.1993 ->
+// Non-temporal stores for the in-place step's write-back of changed relators: nothing reads
+// those lines again inside the launch, and plain stores kept them in L2 beside the tile loads
+// (same buffers: L = 128 0.2727 -> 0.2581 ms, lengths-carrying 0.2302 -> 0.2102, L = 36
+// 0.0742 -> 0.0697; profiles/r04/r04z_ab_nt*.json).  Whole output rows (the out-of-place step,
+// the rollout's final state, canonicalized rows, expanded children) stay plain: non-temporal
+// made the rollout slower (K = 20 int32 1.332 -> 1.351 ms, int8 0.447 -> 0.477; its next launch
+// reads that state) and expand12's children no faster (0.778 -> 0.772 ms).
+constexpr bool NT_WRITEBACK = true;
+constexpr bool NT_STATE = false;
+// Buffer-instruction cache policies (gfx950 cpol bits: sc0 1, nt 2, sc1 16).
+// The L = 128 in-place step's write-back (CodeTile): sc1, same buffers: lengths-carrying 0.1993 ->
 // 0.1791 ms, acx_step 0.2423 -> 0.2182 against nt; nt + sc1 0.1989 (profiles/r04/r04s_ab_wb_cpol.json).
-// sc1 / sc0 sc1 on the tile LOADS instead of nt: 0.2327 (r04s_ab_ld_cpol.json), so those stay nt.
-#ifndef ACX_WB_CPOL
-#define ACX_WB_CPOL 16
-#endif
-// (FastTile, e.g. L = 36, keeps the global non-temporal write-back: sc1 measured 0.0757 vs nt
-// 0.0698 ms per 2^20-env step, profiles/r04/r04s_ab_wb36_cpol.json; that A/B knob was removed in
-// round 5 -- DESIGN.md "Buffer descriptors")
-// (the rollout's int8 trajectory keeps global non-temporal stores: K = 20 0.4626 ms vs sc1 buffer
-// stores 0.4862, plain 0.494, profiles/r04/r04s_ab_obs8_cpol.json; that knob was removed in round 5)
-// The rollout's int32 trajectory stores (full tiles) through a buffer store with this cache policy
-// (gfx950 cpol bits: sc0 1, nt 2, sc1 16; -1: the global non-temporal store of ACX_NT_OBS).  sc1
-// (the line is not kept in the XCD's L2): same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059
-// and 1.3241 -> 1.3027 ms against nt, plain 1.2267 / 1.3195; K = 200 within 0.3 %
-// (profiles/r04/r04s_ab_obs_cpol*.json; the bare store pattern, r04s_cpol.json, orders them alike)
-#ifndef ACX_OBS_CPOL
-#define ACX_OBS_CPOL 16
-#endif
+// FastTile (L = 36) keeps the global non-temporal write-back: sc1 measured 0.0757 vs nt 0.0698 ms
+// per 2^20-env step (r04s_ab_wb36_cpol.json).
+constexpr int WB_CPOL = 16;
+// The rollout's int32 trajectory stores (full tiles): sc1 (the line is not kept in the XCD's L2):
+// same buffers, K = 20 on Samsung boxes 1.2377 -> 1.2059 and 1.3241 -> 1.3027 ms against nt,
+// plain 1.2267 / 1.3195; K = 200 within 0.3 % (profiles/r04/r04s_ab_obs_cpol*.json).  The int8
+// trajectory keeps global non-temporal stores: K = 20 0.4626 ms vs sc1 0.4862, plain 0.494
+// (r04s_ab_obs8_cpol.json).
+constexpr int OBS_CPOL = 16;
 // expand12's parent loads and packed-key stores non-temporal (keys as 16-B stores): same buffers,
 // 4M parents (profiles/r04/r04z_ab_keys.json): 0.4246 ms (0.71 of 8 TB/s) -> 0.380 ms (0.79) with
 // both; the loads alone 0.4085, the stores alone 0.5101 (slower); the children kernel unchanged
-#ifndef ACX_NT_EXPAND_LOADS
-#define ACX_NT_EXPAND_LOADS 1
-#endif
-#ifndef ACX_NT_KEYS
-#define ACX_NT_KEYS 1
-#endif
-// A/B knob: the step kernel's per-env outputs (reward, done, truncated, step count, lengths, err)
-// with non-temporal stores
-#ifndef ACX_NT_STEP_SCALARS
-#define ACX_NT_STEP_SCALARS 0
-#endif
+constexpr bool NT_EXPAND_LOADS = true;
+constexpr bool NT_KEYS = true;
 // Non-temporal tile loads (NTL): the state rows are read once per launch.  Taken where it
 // measured faster (same buffers, profiles/r04/r04z_ab_ld*.json): the L = 128 step (CodeTile:
 // 0.2587 -> 0.2432 ms, lengths-carrying 0.2105 -> 0.1991) and the rollout's state in (int8
 // trajectory 0.4635 -> 0.4402 ms, int32 1.3235 -> 1.3131); not the L = 36 step, whose write-back
 // of relators that are not sector-aligned (288-B rows) then went 0.0699 -> 0.0944 ms.
-#ifndef ACX_NT_STEP_LOADS36
-#define ACX_NT_STEP_LOADS36 0  // FastTile (L % 4 == 0, not CodeTile) step loads: A/B knob
-#endif
 template <bool NT>
 __device__ __forceinline__ int4 ld_tile(const int4* p) {
     if constexpr (NT) {
@@ -216,17 +176,7 @@ __device__ __forceinline__ int4 ld_tile(const int4* p) {
         return *p;
     }
 }
-#ifndef ACX_LD_CPOL
-#define ACX_LD_CPOL 2  // A/B knob: the cache policy of the non-temporal buffer tile loads (nt = 2)
-#endif
-constexpr int tile_cpol(bool nt) { return nt ? ACX_LD_CPOL : 0; }  // buffer-load cache policy (gfx94x/950 bits)
-// A/B knob: extra LDS bytes per step-kernel block (occupancy probes; 0 in the product)
-#ifndef ACX_STEP_LDS_PAD
-#define ACX_STEP_LDS_PAD 0
-#endif
-#ifndef ACX_FAST_CONVERT
-#define ACX_FAST_CONVERT 1
-#endif
+constexpr int tile_cpol(bool nt) { return nt ? 2 : 0; }  // buffer-load cache policy: nt (gfx94x/950 bits)
 // 16 bytes of a row (4 int32 letters) -> the dword of their low bytes (2 v_perm_b32 + or);
 // bad = a letter outside {-2..2} (max / min of the four).  A bad chunk's bytes are arbitrary:
 // its row is flagged and never decoded from the tile.
@@ -388,13 +338,7 @@ struct FastTile {
                     if (u0 + u >= CPR) continue;
                     bool bad = false;
                     uint32_t p = 0;
-#if ACX_FAST_CONVERT
                     if (lv[u]) p = chunk_i8(v[u], bad);
-#else
-                    if (lv[u])
-                        p = to_i8(v[u].x, bad) | (to_i8(v[u].y, bad) << 8) | (to_i8(v[u].z, bad) << 16) |
-                            (to_i8(v[u].w, bad) << 24);
-#endif
                     lds[lds_index(ln, u0 + u)] = p;
                     if (bad) flags[(ln + (u0 + u) * WAVE) / CPR] = 1;
                     any_bad |= bad;
@@ -419,7 +363,6 @@ struct FastTile {
         }
         tile_bad = __any(any_bad);
         wave_sync();
-#if ACX_FAST_CONVERT
         if (tile_bad) {
             // rare (wave-uniform): chunk_i8 left arbitrary bytes in the flagged rows; their image
             // is rebuilt with to_i8 (an out-of-domain letter -> 0x7f), so the letter counts the
@@ -435,7 +378,6 @@ struct FastTile {
             }
             wave_sync();
         }
-#endif
     }
 
     // all BLOCK threads load R rows into this tile (the block's one): consecutive threads on
@@ -452,7 +394,7 @@ struct FastTile {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = (int)threadIdx.x + u * BLOCK;
-            if (c < nc) v[u] = ld_tile<ACX_NT_EXPAND_LOADS != 0>(src + c);
+            if (c < nc) v[u] = ld_tile<NT_EXPAND_LOADS>(src + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -556,8 +498,7 @@ struct FastTile {
     // tile's spare lanes re-store its last chunk, same data to the same address), so the
     // compiler's waitcnt pass can count them (rollout_kernel's one-step-ahead action load).
     // [UB, UE): a range of the lane's chunk slots only (the rollout's split obs store)
-    static constexpr bool SPLIT_OK = true;
-    static constexpr bool NT_STEP_LOADS = ACX_NT_STEP_LOADS36 != 0;  // see ld_tile
+    static constexpr bool NT_STEP_LOADS = false;  // see ld_tile
     template <bool NT, int UB = 0, int UE = CPR>
     __device__ __forceinline__ void store_rows(int32_t* g, int R, int lane) const {
         int ln = lane;
@@ -565,8 +506,7 @@ struct FastTile {
         int4* dst = reinterpret_cast<int4*>(g);
         const int nc = R * CPR;
         if (R == WAVE) {
-#if ACX_OBS_CPOL >= 0
-            if constexpr (NT) {  // the trajectory store with an explicit cache policy (A/B knob)
+            if constexpr (NT) {  // the trajectory store with an explicit cache policy (OBS_CPOL)
                 const uint64_t b = reinterpret_cast<uint64_t>(g);
                 const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
                 const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
@@ -584,12 +524,11 @@ struct FastTile {
                             const int4 v = widen4(p[u]);
                             const v4i_t x = {v.x, v.y, v.z, v.w};
                             __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (u0 + u) * WAVE) * 16u, 0,
-                                                                   ACX_OBS_CPOL);
+                                                                   OBS_CPOL);
                         }
                 }
                 return;
             }
-#endif
             store_flat<NT, false, true, UB, UE>(dst + ln, ln, nc);
             return;
         }
@@ -969,7 +908,6 @@ struct CodeTile {
     bool tile_bad = false;
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
-    static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
@@ -1043,7 +981,6 @@ struct CodeTile {
         const int nc = R * CPR;
         const int4* src = reinterpret_cast<const int4*>(g) + ln;
         bool any_bad = false;
-#if ACX_FAST_CONVERT
         if constexpr (CPR == WAVE) {
             if (PIPE && R == WAVE) {
                 // full tile, one row per wave-instruction (row u, lane ln = its chunk ln):
@@ -1139,7 +1076,6 @@ struct CodeTile {
                 return;
             }
         }
-#endif
         if (PIPE && R == WAVE) {
             // full tile (wave-uniform): software-pipelined, batch b + 1's loads are issued before
             // batch b is converted, so LOAD_BATCH..2*LOAD_BATCH loads stay in flight through the
@@ -1230,7 +1166,7 @@ struct CodeTile {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = (int)threadIdx.x + u * BLOCK;
-            if (c < nc) v[u] = ld_tile<ACX_NT_EXPAND_LOADS != 0>(src + c);
+            if (c < nc) v[u] = ld_tile<NT_EXPAND_LOADS>(src + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1552,19 +1488,16 @@ struct CodeTile {
             }
             return;
         }
-#if ACX_FAST_CONVERT
         if constexpr (CPR == WAVE) {
             // one row per wave-instruction (row r, lane ln = its chunk ln): the lane's fixed slot
             // address, row r's dirty bits and live counts read from lane r's registers (scalars)
             const uint16_t* mine = reinterpret_cast<const uint16_t*>(lds) + ln;
             const int hs = ln >= HALF ? 1 : 0;
-#if ACX_WB_CPOL >= 0
             const uint64_t gb = reinterpret_cast<uint64_t>(g);
             const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)gb);
             const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32));
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<void*>(((uint64_t)ghi << 32) | glo), (short)0, WAVE * CPR * 16, 0x00020000);
-#endif
             for (int r0 = 0; r0 < R; r0 += STAGE_UNROLL) {
                 uint32_t p[STAGE_UNROLL];
                 bool wr[STAGE_UNROLL];
@@ -1581,19 +1514,13 @@ struct CodeTile {
                 for (int u = 0; u < STAGE_UNROLL; ++u) {
                     if (!wr[u]) continue;
                     const uint32_t nz4 = (p[u] >> 8) & 0xfu;
-#if ACX_WB_CPOL >= 0
                     const int4 v = widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4)));
                     const v4i_t x = {v.x, v.y, v.z, v.w};
-                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (r0 + u) * WAVE) * 16u, 0, ACX_WB_CPOL);
-#else
-                    out16<NT, false>(dst + ln + (r0 + u) * WAVE,
-                                     widen4(codes_to_i8x4(p[u] & 0xffu, 8u * __builtin_popcount(nz4))));
-#endif
+                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(ln + (r0 + u) * WAVE) * 16u, 0, WB_CPOL);
                 }
             }
             return;
         }
-#endif
         for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
             uint32_t p[STAGE_UNROLL];
             bool wr[STAGE_UNROLL];
@@ -1658,7 +1585,6 @@ struct CodeTile {
 
 template <int NW, int LC, int VEC>
 struct GenericTile {
-    static constexpr bool SPLIT_OK = false;  // the rollout's split obs store: FastTile only
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
@@ -2231,8 +2157,7 @@ __device__ __forceinline__ void copy_rows(const StepArgs& a, const WaveCtx& w, u
 template <int NW, int LC, int VEC, bool LEARN, bool LIVE, int BATCH = 0>
 __device__ __forceinline__ void step_body(const StepArgs& a) {
     using Tile = TileFor<NW, LC, VEC>;
-    constexpr bool NT_SC = ACX_NT_STEP_SCALARS != 0;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+        extern __shared__ __attribute__((aligned(16))) char smem[];
     WaveCtx w;
     // acx_learner_step: the curriculum fused in (cur_publish / cur_prefix)
     const bool cur = LEARN && a.cur_ws != nullptr;  // kernel argument: uniform
@@ -2256,7 +2181,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // the env's move id and step count: issued ahead of the tile so their latency hides under it
     int act_in = 0, cnt_in = 0;
     const bool pend = w.active && a.pending && a.pending[env] != 0;  // next-step autoreset: reset now
-#if ACX_EARLY_SCALARS
     if (w.active) {
         if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
             const int64_t v = a.action64[env];
@@ -2266,7 +2190,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         cnt_in = a.step_count ? a.step_count[env] : 0;
     }
-#endif
     int hb = 0;  // the move-history ring's row of this env's episode move 0
     if (LEARN && w.active && a.hist_base) hb = a.hist_base[env];
     if constexpr (LIVE) {
@@ -2277,9 +2200,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         tile.set_lim(w.lane, n_in0, n_in1);
         wave_sync();
-        tile.template load<ACX_PIPE_LOAD != 0, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
+        tile.template load<true, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     } else {
-        tile.template load<ACX_PIPE_LOAD != 0, false, Tile::NT_STEP_LOADS, BATCH>(a.state_in + w.r0 * twoL, w.R, w.lane);
+        tile.template load<true, false, Tile::NT_STEP_LOADS, BATCH>(a.state_in + w.r0 * twoL, w.R, w.lane);
     }
 
     // Truncations are known before the move (step_count + 1 >= horizon, unless the move fails):
@@ -2287,7 +2210,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // before this step's stores -- loaded after the move instead, behind those stores, they were
     // a second dependent round trip that doubled the life of every wave holding one (a learner
     // step with episodes out of phase, ~B/H truncations per step: +44 us on a 124 us step)
-    constexpr bool PREF = !LIVE && Tile::PREFETCH_OK && ACX_EARLY_SCALARS != 0;
+    constexpr bool PREF = !LIVE && Tile::PREFETCH_OK;
     uint64_t pre = 0;  // wave-uniform: the rows fetched
     int4 pv = {0, 0, 0, 0};
     if constexpr (PREF) {
@@ -2310,15 +2233,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     int32_t rwd = 0;
     if (w.active) {
         act = act_in;
-#if !ACX_EARLY_SCALARS
-        if (LEARN && a.action64) {  // policy samples (int64); out of range -> ACX_ERR_ACTION
-            const int64_t v = a.action64[env];
-            act = (v >= 0 && v < 12) ? (int)v : -1;
-        } else {
-            act = a.action[env];
-        }
-        cnt_in = a.step_count ? a.step_count[env] : 0;
-#endif
         cnt0 = cnt_in;
         cnt = a.step_count ? cnt0 + 1 : 0;
         const bool bad = tile.template pack<LIVE>(w.lane, p);
@@ -2363,9 +2277,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             }
             a.action_hist[(int64_t)row * a.B + env] = (uint8_t)act;
         }
-        if (a.reward) st_scalar<NT_SC, int32_t>(a.reward + env, rwd);
-        if (a.done) st_scalar<NT_SC, uint8_t>(a.done + env, (uint8_t)triv);
-        if (a.truncated) st_scalar<NT_SC, uint8_t>(a.truncated + env, (uint8_t)trunc);
+        if (a.reward) st_scalar<false, int32_t>(a.reward + env, rwd);
+        if (a.done) st_scalar<false, uint8_t>(a.done + env, (uint8_t)triv);
+        if (a.truncated) st_scalar<false, uint8_t>(a.truncated + env, (uint8_t)trunc);
         if constexpr (LEARN) {
             if (a.reward_f32) a.reward_f32[env] = (float)rwd;
             if (a.done_f32) a.done_f32[env] = triv ? 1.0f : 0.0f;
@@ -2422,14 +2336,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (reset) cnt = 0;
     }
     if (w.active) {
-        if (a.step_count) st_scalar<NT_SC, int32_t>(a.step_count + env, cnt);
+        if (a.step_count) st_scalar<false, int32_t>(a.step_count + env, cnt);
         if (a.lengths_out) {
             // lengths-carrying step: an out-of-domain row is read whole on the next call (L, L)
             const bool whole = LIVE && e == ACX_ERR_DOMAIN;
-            st_scalar<NT_SC, int32_t>(a.lengths_out + 2 * env, whole ? L : p.n0);
-            st_scalar<NT_SC, int32_t>(a.lengths_out + 2 * env + 1, whole ? L : p.n1);
+            st_scalar<false, int32_t>(a.lengths_out + 2 * env, whole ? L : p.n0);
+            st_scalar<false, int32_t>(a.lengths_out + 2 * env + 1, whole ? L : p.n1);
         }
-        if (a.err) st_scalar<NT_SC, uint8_t>(a.err + env, (uint8_t)e);
+        if (a.err) st_scalar<false, uint8_t>(a.err + env, (uint8_t)e);
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
     }
     if (a.in_place) {
@@ -2441,19 +2355,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         wave_sync();
         if (__ballot(dm != 0u)) {
             if constexpr (LIVE)
-                tile.template store_dirty<ACX_NT_WRITEBACK != 0, true>(a.state_out + w.r0 * twoL, w.R, w.lane,
+                tile.template store_dirty<NT_WRITEBACK, true>(a.state_out + w.r0 * twoL, w.R, w.lane,
                                                        a.reset_state + w.r0 * twoL);
             else
-                tile.template store_dirty<ACX_NT_WRITEBACK != 0>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
+                tile.template store_dirty<NT_WRITEBACK>(a.state_out + w.r0 * twoL, w.R, w.lane, a.reset_state + w.r0 * twoL);
         }
     } else {
         wave_sync();
-        tile.template store<true, ACX_NT_STATE != 0>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL,
+        tile.template store<true, NT_STATE>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL,
                                                      twoL, w.lane,
                                   a.reset_state + w.r0 * twoL);
     }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
-        tile.template store<true, ACX_NT_OBS != 0, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
+        tile.template store<true, NT_OBS, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
                                                a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
     if (cur) {
         // The curriculum's tail (training.py:329-336, 349-352).  A finished env was reset to its own
@@ -2512,18 +2426,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 // round trip instead of CPR / LOAD_BATCH of them) with the VGPR budget two waves per SIMD leave.
 // FastTile instantiations (compile-time L % 4 == 0, L < 64: the L = 36 configs); launch_step
 // takes it for B <= SMALL_STEP_MAX_B
-// A/B knobs: ACX_SMALL_STEP=0 keeps every batch on step_kernel; ACX_SMALL_BATCH loads in flight
-// per batch (0: the whole row, LC / 2)
-#ifndef ACX_SMALL_STEP
-#define ACX_SMALL_STEP 1
-#endif
-#ifndef ACX_SMALL_BATCH
-#define ACX_SMALL_BATCH 0
-#endif
-constexpr int64_t SMALL_STEP_MAX_B = ACX_SMALL_STEP ? (int64_t)2 * 4 * 256 * WAVE : -1;  // <= 2 waves per SIMD on 256 CUs
+constexpr int64_t SMALL_STEP_MAX_B = (int64_t)2 * 4 * 256 * WAVE;  // <= 2 waves per SIMD on 256 CUs
 template <int NW, int LC, int VEC>
 __global__ __launch_bounds__(BLOCK, 2) void step_small_kernel(StepArgs a) {
-    step_body<NW, LC, VEC, false, false, (ACX_SMALL_BATCH > 0 ? ACX_SMALL_BATCH : LC / 2)>(a);
+    step_body<NW, LC, VEC, false, false, LC / 2>(a);
 }
 template <int NW, int LC, int VEC>
 constexpr bool small_step_ok() {
@@ -2536,13 +2442,6 @@ constexpr bool small_step_ok() {
 template <int NW, int LC, int VEC>
 __global__ __launch_bounds__(BLOCK, LC == 128 ? 4 : Occupancy<LC>::waves_per_simd) void step_lengths_kernel(StepArgs a) {
     step_body<NW, LC, VEC, false, true>(a);
-}
-
-// the first half of a FastTile row's chunk slots, rounded to whole store batches
-template <class Tile>
-constexpr int split_half_chunks() {
-    if constexpr (Tile::SPLIT_OK) return (Tile::CPR / 2 + STAGE_UNROLL - 1) / STAGE_UNROLL * STAGE_UNROLL;
-    else return 0;
 }
 
 struct RolloutArgs {
@@ -2603,20 +2502,6 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     __builtin_amdgcn_s_waitcnt(0);
     const int32_t* act_tile = a.actions + w.r0;  // wave-uniform
 
-    // split obs store (ACX_OBS_SPLIT): the trajectory row offset of the step whose second half
-    // is still to be stored, -1 if none (wave-uniform)
-    constexpr bool SPLIT = ACX_OBS_SPLIT != 0 && OBS == 1 && Tile::SPLIT_OK;
-    constexpr int HALF_CH = split_half_chunks<Tile>();
-    int64_t pend_ti = -1;
-    auto flush_half = [&](int lane) {
-        if constexpr (SPLIT) {
-            if (pend_ti >= 0)
-                tile.template store_rows<ACX_NT_OBS != 0, HALF_CH, Tile::CPR>(a.obs_traj + (pend_ti + w.r0) * twoL,
-                                                                          w.R, lane);
-            pend_ti = -1;
-        }
-    };
-
     // One env step of the wave: move, reward/done/truncated, autoreset, obs rows.
     auto step = [&](int t, uint32_t id) {
         const int64_t ti = (int64_t)t * a.B;
@@ -2628,8 +2513,6 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         const int lane = (int)__lane_id();
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        // the previous step's deferred half, from the LDS image before this step changes it
-        flush_half(lane);
         bool reset = false;
         bool both = false;  // the LDS image needs both relators (general move: both reduced)
         bool h1 = false;    // the moved relator (ac_moves.py:167-179: i = (id + 1) & 1)
@@ -2654,9 +2537,9 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
             const bool triv = ok && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
             cnt += ok ? 1 : 0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
             const bool trunc = ok && cnt >= a.horizon;
-            if (a.reward_traj) st_scalar<ACX_NT_SCALARS != 0, int32_t>(a.reward_traj + ti + w.r0 + ln, triv ? max_reward : -(p.n0 + p.n1));
-            if (a.done_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.done_traj + ti + w.r0 + ln, (uint8_t)triv);
-            if (a.trunc_traj) st_scalar<ACX_NT_SCALARS != 0, uint8_t>(a.trunc_traj + ti + w.r0 + ln, (uint8_t)trunc);
+            if (a.reward_traj) st_scalar<false, int32_t>(a.reward_traj + ti + w.r0 + ln, triv ? max_reward : -(p.n0 + p.n1));
+            if (a.done_traj) st_scalar<false, uint8_t>(a.done_traj + ti + w.r0 + ln, (uint8_t)triv);
+            if (a.trunc_traj) st_scalar<false, uint8_t>(a.trunc_traj + ti + w.r0 + ln, (uint8_t)trunc);
             reset = triv || trunc;
             if (reset) cnt = 0;
         }
@@ -2701,13 +2584,10 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
                 return;
             }
             wave_sync();
-            if constexpr (SPLIT) {
-                tile.template store_rows<ACX_NT_OBS != 0, 0, HALF_CH>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
-                pend_ti = ti;
-            } else if constexpr (OBS == 1) {
-                tile.template store_rows<ACX_NT_OBS != 0>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
+            if constexpr (OBS == 1) {
+                tile.template store_rows<NT_OBS>(a.obs_traj + (ti + w.r0) * twoL, w.R, lane);
             } else {
-                tile.template store_rows_i8<ACX_NT_OBS != 0>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, lane);
+                tile.template store_rows_i8<NT_OBS>(a.obs_traj8 + (ti + w.r0) * twoL, w.R, lane);
             }
             wave_sync();
         }
@@ -2762,7 +2642,6 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
         for (int k = 0; k < QW; ++k) q[k] = (q[k] >> 4) | (k + 1 < QW ? q[k + 1] << 28 : 0u);
         step(t, id);
     }
-    flush_half(w.lane);
     if (w.active) {
         if (!bad) tile.unpack(w.lane, p);
         a.step_count[env] = cnt;
@@ -2771,7 +2650,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void rollout_
     }
     // out-of-domain rows: their input row (untouched in HBM), or the starting row they reset to
     tile.restore_flags(w.lane, (w.active && bad) ? (bad_reset ? FB_RESET : FB_IN) : 0u);
-    tile.template store<true, ACX_NT_STATE != 0>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
+    tile.template store<true, NT_STATE>(a.state + w.r0 * twoL, twoL, w.R, a.state + w.r0 * twoL, twoL,
                                                  w.lane, a.reset_state + w.r0 * twoL);
 }
 
@@ -2894,7 +2773,7 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void expand12
         }
         if (a.children) {
             wave_sync();
-            tile.template store<true, ACX_NT_STATE != 0>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
+            tile.template store<true, NT_STATE>(a.children + (w.r0 * 12 + act) * twoL, (int64_t)12 * twoL, w.R,
                                       a.parents + w.r0 * twoL, twoL, w.lane);
             wave_sync();
         }
@@ -3011,7 +2890,7 @@ __global__ __launch_bounds__(BLOCK) void expand12_keys_kernel(ExpandArgs a) {
     }
     __syncthreads();
     uint64_t* dst = a.child_key + r0 * 12 * kw;
-    if constexpr (ACX_NT_KEYS != 0) {
+    if constexpr (NT_KEYS) {
         // 16-B non-temporal stores (dst is 16-B aligned: r0 is a multiple of 64), odd tail word apart
         const int nw = R * 12 * kw;
         for (int i = threadIdx.x; 2 * i + 1 < nw; i += BLOCK) {
@@ -3099,7 +2978,7 @@ __global__ __launch_bounds__(BLOCK) void expand12_children_kernel(ExpandArgs a) 
             if (!bad) tile.unpack(lane, q);
         }
         wave_sync();
-        tile.template store<true, ACX_NT_STATE != 0>(a.children + (r0 * 12 + act) * twoL, (int64_t)12 * twoL, R,
+        tile.template store<true, NT_STATE>(a.children + (r0 * 12 + act) * twoL, (int64_t)12 * twoL, R,
                                   a.parents + r0 * twoL, twoL, lane);
         wave_sync();
     }
@@ -3279,7 +3158,7 @@ __global__ __launch_bounds__(BLOCK) void canon_kernel(CanonArgs a) {
     }
     tile.flag_rows(w.lane, bad ? FB_IN : 0u);  // incl. a zero inside a relator (not flagged by the load)
     wave_sync();
-    tile.template store<true, ACX_NT_STATE != 0>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL,
+    tile.template store<true, NT_STATE>(a.state_out + w.r0 * twoL, twoL, w.R, a.state_in + w.r0 * twoL, twoL,
                                                  w.lane);
 }
 
@@ -3364,7 +3243,7 @@ static inline unsigned grid_for(int64_t rows) {
 // while the main object declares them `extern template` below.
 template <int NW, int LC, int VEC, bool LEARN>
 int launch_step(StepArgs a, hipStream_t s) {
-    const size_t shm = smem_bytes<NW, LC, VEC>(a.L) + ACX_STEP_LDS_PAD;
+    const size_t shm = smem_bytes<NW, LC, VEC>(a.L);
     if (!LEARN && a.live) {
         step_lengths_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
         return finish_launch();
