@@ -11,6 +11,8 @@ import re, sys
 out = sys.argv[1]
 s = open(out + '/acx36.s').read()
 for k in re.findall(r'^(_ZN3acx\w+):', s, re.M):
+    if '.name:           ' + k not in s:  # an out-of-line device function, not a kernel
+        continue
     i = s.index(k + ':'); j = s.index('.Lfunc_end', i)
     short = re.sub(r'_ZN3acx\d+(\w+?)_kernel.*', r'\1', k)
     open(f'{out}/{short}.s', 'w').write(s[i:j])

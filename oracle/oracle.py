@@ -15,6 +15,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+# tests/test_sanitizers.py runs the oracle's own tests against the ASan + UBSan build
+# (liboracle_asan.so) by naming it here
+LIB_PATH = os.environ.get("ACX_ORACLE_LIB", LIB_PATH)
 
 ERR_OK, ERR_INVALID, ERR_EMPTY_CONJ, ERR_DOMAIN, ERR_BAD_ACTION, ERR_OTHER = 0, 1, 2, 3, 4, 9
 
@@ -22,6 +25,8 @@ _lib = None
 
 
 def build(force: bool = False) -> str:
+    if os.path.basename(LIB_PATH) != "liboracle.so":
+        return LIB_PATH  # a sanitizer build, made by its caller
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
         os.path.join(HERE, "acx_oracle.c")
     ):
