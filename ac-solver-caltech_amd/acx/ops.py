@@ -68,9 +68,9 @@ LIVE_TILE_L = (36, 128)
 # horizon); at L = 36 the two tie (0.0793 vs 0.0799 ms per 2^20-env step in-process, 4 % the
 # other way in a bench line: 288-B rows leave little to save against the per-chunk live test)
 LENGTHS_STEP_L = (128,)
-# acx_step at a compile-time L = 36 tile with B <= this many envs runs the small-batch instance
-# (step_small_kernel: <= 2 waves per SIMD, the whole tile's loads in flight at once); csrc
-# acx_kernels.hip SMALL_STEP_MAX_B
+# acx_step at a compile-time L = 36 tile with B <= this many envs runs the small-batch kernel
+# (step_pair_kernel: two lanes per env, one per relator, so config 2's 65,536 envs are two waves
+# per SIMD instead of one); csrc acx_kernels.hip SMALL_STEP_MAX_B
 SMALL_STEP_MAX_B = 2 * 4 * 256 * 64
 
 
@@ -79,7 +79,7 @@ def step_kernel_name(B: int, L: int) -> str:
     nw = 1 if L <= 16 else 2 if L <= 32 else 3 if L <= 48 else 4 if L <= 64 else 8
     lc = L if L in (36, 128) else 0
     if lc == 36 and B <= SMALL_STEP_MAX_B:
-        return f"acx::step_small_kernel<{nw},{lc},4>"
+        return f"acx::step_pair_kernel<{nw},{lc},4>"
     return f"acx::step_kernel<{nw},{lc},4,false>"
 
 

@@ -2421,19 +2421,315 @@ template <int NW, int LC, int VEC, bool LEARN>
 __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_kernel(StepArgs a) {
     step_body<NW, LC, VEC, LEARN, false>(a);
 }
-// Small batches (BASELINE configs[1]: 65,536 envs = 1,024 waves, one per SIMD): no other wave
-// hides a wave's load -> move -> store chain, so the whole tile's loads are issued at once (one
-// round trip instead of CPR / LOAD_BATCH of them) with the VGPR budget two waves per SIMD leave.
-// FastTile instantiations (compile-time L % 4 == 0, L < 64: the L = 36 configs); launch_step
-// takes it for B <= SMALL_STEP_MAX_B
-constexpr int64_t SMALL_STEP_MAX_B = (int64_t)2 * 4 * 256 * WAVE;  // <= 2 waves per SIMD on 256 CUs
-template <int NW, int LC, int VEC>
-__global__ __launch_bounds__(BLOCK, 2) void step_small_kernel(StepArgs a) {
-    step_body<NW, LC, VEC, false, false, LC / 2>(a);
-}
+// ---------------------------------------------------------------------------------
+// Small batches: two lanes per env (BASELINE configs[1]: 65,536 envs at L = 36).
+//
+// With one lane per env, 65,536 envs are 1,024 waves -- one per SIMD: nothing hides a wave's
+// load -> pack -> move -> unpack -> store chain, and a lone wave issues a VALU instruction every
+// 4 cycles instead of every 2 (MI355X_MICROARCH.md, "vector-instruction ISSUE cost").
+// step_pair_kernel gives each env two lanes of a 32-env tile, lane 2e + h holding relator h of
+// env e, so the same batch is 2,048 waves and the per-relator work is split between the lanes:
+//   * the tile (32 rows, 18 16-byte chunks each) is read with 9 coalesced loads per lane into an
+//     int8 image in LDS; relator q of the tile (q = 2e + h) is chunks [9q, 9q + 9) -- lane q's;
+//   * lane q packs ITS relator into bit planes (pl::, one 64-bit word per plane at L <= 64) and
+//     takes its partner's planes and length with four DPP quad-permutes (quad_perm [1,0,3,2]);
+//   * both lanes run the env's move (acx_planes.h: the junction cancellation count and the
+//     cyclic peel are the first set bit of a mismatch mask, the splice is shifts of the planes);
+//   * lane q re-images only its relator and compares it with the loaded image: the per-relator
+//     "changed" bits, the rows' fallback codes and the error flags are wave ballots -- one bit per
+//     relator, bit q <-> chunks [9q, 9q + 9) -- so the coalesced in-place write-back tests chunk c
+//     against bit c / 9 of a 64-bit scalar mask, no per-row flag bytes.
+// Results are those of step_body<..., LEARN = false, LIVE = false> (the same pack, move,
+// image and error contract; tests/test_gpu_*: every acx_step test at L = 36 and B <= 131,072 runs
+// here); only the instruction schedule differs.  launch_step takes it for B <= SMALL_STEP_MAX_B.
+// ---------------------------------------------------------------------------------
+constexpr int64_t SMALL_STEP_MAX_B = (int64_t)2 * 4 * 256 * WAVE;  // <= 4 pair-waves per SIMD on 256 CUs
 template <int NW, int LC, int VEC>
 constexpr bool small_step_ok() {
-    return std::is_same<TileFor<NW, LC, VEC>, FastTile<NW, LC>>::value;
+    return std::is_same<TileFor<NW, LC, VEC>, FastTile<NW, LC>>::value && LC <= 64;
+}
+
+// partner lane's value (lane ^ 1): DPP quad_perm [1,0,3,2], full-rate VALU, no LDS
+__device__ __forceinline__ uint32_t pair_xchg(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t pair_xchg64(uint64_t v) {
+    return (uint64_t)pair_xchg((uint32_t)v) | ((uint64_t)pair_xchg((uint32_t)(v >> 32)) << 32);
+}
+
+template <int LC>
+struct PairLayout {
+    static constexpr int CPR = LC / 2;          // 16-byte chunks per row
+    static constexpr int HALF = CPR / 2;        // chunks (= image dwords) per relator
+    static constexpr int ENVS = WAVE / 2;       // envs per wave
+    static constexpr int NCH = ENVS * CPR;      // chunks per full tile
+    static constexpr int U = NCH / WAVE;        // chunk loads per lane (full tile)
+    static_assert(LC % 4 == 0 && LC <= 64 && HALF * 2 == CPR && U * WAVE == NCH, "pair tile layout");
+    static constexpr size_t wave_bytes = (size_t)NCH * 4 + WAVE;  // int8 image + one flag byte per relator
+};
+
+// relator image (HALF dwords of int8 letters, zero padding) -> its planes and length; true if
+// outside the domain (a zero inside the relator): FastTile::pack on one relator
+template <int HALF>
+__device__ __forceinline__ bool pair_pack(const uint32_t* src, Planes<1>& w, int& n) {
+    uint64_t s = 0, y = 0, nz = 0;
+#pragma unroll
+    for (int k = 0; k < HALF; k += 2) {
+        const uint32_t d0 = src[k];
+        const uint32_t d1 = k + 1 < HALF ? src[k + 1] : 0u;
+        uint32_t s8, y8, z8;
+        pl::i8x8_to_bytes(d0, d1, s8, y8, z8);
+        s |= (uint64_t)s8 << (4 * k);
+        y |= (uint64_t)y8 << (4 * k);
+        nz |= (uint64_t)z8 << (4 * k);
+    }
+    w.s[0] = s;
+    w.y[0] = y;
+    n = __builtin_popcountll(nz);
+    return nz != pl::bmask<1>(n).b[0];  // zeros only as right padding <=> mask == low n bits
+}
+
+// planes -> the relator's int8 image in dst; returns true if it differs from what dst held
+template <int HALF>
+__device__ __forceinline__ bool pair_image(uint32_t* dst, const Planes<1>& w, int n) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+        const uint32_t d = pl::nibbles_to_i8x4(pl::nib<1>(w.s, k), pl::nib<1>(w.y, k), clamp_bits(8 * n - 32 * k));
+        x |= dst[k] ^ d;
+        dst[k] = d;
+    }
+    return x != 0u;
+}
+
+// a relator's int32 letters (HALF chunks from src) -> its int8 image in dst; true if a letter is
+// outside {-2..2} (the image then holds 0x7f there, as FastTile::load_rows)
+template <int HALF>
+__device__ __forceinline__ bool pair_load_relator(uint32_t* dst, const int32_t* src) {
+    int4 v[HALF];
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) v[k] = reinterpret_cast<const int4*>(src)[k];
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < HALF; ++k)
+        dst[k] = to_i8(v[k].x, bad) | (to_i8(v[k].y, bad) << 8) | (to_i8(v[k].z, bad) << 16) | (to_i8(v[k].w, bad) << 24);
+    return bad;
+}
+
+template <int NW, int LC, int VEC>
+__global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
+    using PT = PairLayout<LC>;
+    constexpr int L = LC, twoL = 2 * LC, CPR = PT::CPR, HALF = PT::HALF, ENVS = PT::ENVS;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t r0 = ((int64_t)blockIdx.x * WPB + wid) * ENVS;  // wave-uniform
+    if (r0 >= a.B) return;
+    const int R = (int)((a.B - r0) < ENVS ? (a.B - r0) : ENVS);
+    const int er = lane >> 1, h = lane & 1;  // env (tile row) and relator of this lane
+    const bool active = er < R;
+    const int64_t env = r0 + er;
+    uint32_t* img = reinterpret_cast<uint32_t*>(smem + wid * PT::wave_bytes);
+    uint8_t* rflag = reinterpret_cast<uint8_t*>(img + PT::NCH);  // per relator: a bad chunk at load (rare path)
+    uint32_t* mine = img + lane * HALF;                          // this lane's relator image
+
+    // scalars first: their latency hides under the tile's loads (both lanes of an env read the
+    // same words; the second is a cache hit)
+    int act = 0, cnt0 = 0;
+    bool pend = false;
+    if (active) {
+        act = a.action[env];
+        cnt0 = a.step_count ? a.step_count[env] : 0;
+        pend = a.pending && a.pending[env] != 0;  // next-step autoreset: reset now
+    }
+    // the tile: chunk c = lane + 64u of the tile's rows (coalesced), relator c / HALF
+    bool flagged = false;  // this lane's relator has a chunk with a letter outside {-2..2}
+    {
+        const int4* src = reinterpret_cast<const int4*>(a.state_in + r0 * twoL) + lane;
+        uint32_t badm = 0;  // bit u: chunk lane + 64u
+        if (R == ENVS) {  // full tile (wave-uniform): every load in flight at once
+            int4 v[PT::U];
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u) v[u] = src[u * WAVE];
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u) {
+                bool bad;
+                img[lane + u * WAVE] = chunk_i8(v[u], bad);
+                badm |= (uint32_t)bad << u;
+            }
+        } else {
+            const int nc = R * CPR;
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u) {
+                const int c = lane + u * WAVE;
+                if (c < nc) {
+                    bool bad;
+                    img[c] = chunk_i8(src[u * WAVE], bad);
+                    badm |= (uint32_t)bad << u;
+                }
+            }
+        }
+        if (__any(badm != 0u)) {
+            // rare (wave-uniform): the flagged relators are found through LDS, and chunk_i8's
+            // arbitrary bytes in them re-imaged letter by letter (an out-of-domain letter ->
+            // 0x7f), so the letter counts the contract reports for the row (reward, lengths) are
+            // those of the input row
+            rflag[lane] = 0;
+            wave_sync();
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u)
+                if ((badm >> u) & 1u) rflag[(lane + u * WAVE) / HALF] = 1;
+            wave_sync();
+            flagged = rflag[lane] != 0;
+            if (active && flagged) pair_load_relator<HALF>(mine, a.state_in + env * twoL + h * L);
+        }
+        wave_sync();
+    }
+
+    // this lane's relator -> planes; the partner's by DPP
+    Planes<1> w;
+    int n;
+    bool bad = pair_pack<HALF>(mine, w, n) || flagged;
+    PlaneRegs<1> p;
+    {
+        Planes<1> wp;
+        wp.s[0] = pair_xchg64(w.s[0]);
+        wp.y[0] = pair_xchg64(w.y[0]);
+        const uint32_t np = pair_xchg((uint32_t)n | (bad ? 0x100u : 0u));
+        bad = bad || (np & 0x100u) != 0u;
+        p.w0 = h ? wp : w;
+        p.w1 = h ? w : wp;
+        p.n0 = h ? (int)(np & 0xffu) : n;
+        p.n1 = h ? n : (int)(np & 0xffu);
+    }
+
+    // the env's move, computed by both of its lanes (step_body's contract)
+    int cnt = 0, e = ACX_ERR_NONE;
+    bool keep = false, triv = false, trunc = false, fin = false, reset = false;
+    int32_t rwd = 0;
+    if (active) {
+        cnt = a.step_count ? cnt0 + 1 : 0;
+        const bool cyc = a.cyclical != 0;
+        if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
+        else if (bad) e = ACX_ERR_DOMAIN;
+        else if (pl::is_clean<1>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<1>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+        else {
+            const pl::MoveOut<1> mo = pl::ac_move_call<1>(p, act, L, cyc);
+            p = mo.p;
+            e = mo.e;
+        }
+        keep = e != ACX_ERR_NONE;
+        if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
+        triv = !pend && !keep && pl::is_trivial<1>(p.w0, p.n0, p.w1, p.n1);
+        trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
+        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        fin = triv || trunc;
+        reset = a.pending ? pend : (fin && a.reset_state && !keep);
+    }
+    // this lane's relator re-imaged (a failed env keeps its loaded image)
+    bool chg = false;
+    if (active && !keep) chg = pair_image<HALF>(mine, h ? p.w1 : p.w0, h ? p.n1 : p.n0);
+    // same-step autoreset (or a pending env's reset): the lane loads its relator of the starting
+    // row into the image (FastTile::load_rows' result; an out-of-domain starting row is taken as it
+    // is and stored from reset_state, FB_RESET)
+    bool rbad = false;
+    if (active && reset) {
+        if (h == 0 && a.final_obs) {  // final_obs <- the post-move state (rare)
+            int32_t* fo = a.final_obs + env * twoL;
+#pragma unroll 1
+            for (int hh = 0; hh < 2; ++hh) {
+                const Planes<1>& ww = hh ? p.w1 : p.w0;
+                const int nn = hh ? p.n1 : p.n0;
+#pragma unroll 1
+                for (int k = 0; k < L; ++k) {
+                    const uint32_t code = pl::pletter<1>(ww, k);
+                    fo[hh * L + k] = k < nn ? (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu) : 0;
+                }
+            }
+        }
+        rbad = pair_load_relator<HALF>(mine, a.reset_state + env * twoL + h * L);
+        Planes<1> rw;
+        int rn;
+        rbad = pair_pack<HALF>(mine, rw, rn) || rbad;
+        if (h) p.n1 = rn;
+        else p.n0 = rn;
+        chg = true;  // dm = 3: the whole row is written
+    }
+    // the partner's starting-row length and domain flag (every lane takes part in the DPP)
+    {
+        const uint32_t x = pair_xchg((uint32_t)(h ? p.n1 : p.n0) | (rbad ? 0x100u : 0u));
+        if (reset) {
+            rbad = rbad || (x & 0x100u) != 0u;
+            if (h) p.n0 = (int)(x & 0xffu);
+            else p.n1 = (int)(x & 0xffu);
+        }
+    }
+    if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
+    if (reset) cnt = 0;
+    // per-env outputs: lane 0 of the pair the env's scalars, lane 1 the lengths
+    if (active) {
+        if (h == 0) {
+            if (a.reward) a.reward[env] = rwd;
+            if (a.done) a.done[env] = (uint8_t)triv;
+            if (a.truncated) a.truncated[env] = (uint8_t)trunc;
+            if (a.pending) a.pending[env] = fin ? 1 : 0;
+            if (a.step_count) a.step_count[env] = cnt;
+            if (a.err) a.err[env] = (uint8_t)e;
+            if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
+        } else if (a.lengths_out) {
+            a.lengths_out[2 * env] = p.n0;
+            a.lengths_out[2 * env + 1] = p.n1;
+        }
+    }
+
+    // the state store.  Relator masks, bit q = relator q of the tile (chunks [9q, 9q + 9)):
+    //   fb_in    rows stored from their input row (out of domain, not reset: FB_IN)
+    //   fb_rst   rows stored from their starting row (reset to an out-of-domain row: FB_RESET)
+    //   dirty    relators that differ from state_in (in place: the only chunks written)
+    const uint64_t fb_rst = __ballot(active && reset && rbad);
+    const uint64_t fb_in = __ballot(active && !reset && e == ACX_ERR_DOMAIN);
+    const uint64_t dirty = __ballot(active && chg);
+    wave_sync();
+    const int nc = R * CPR;
+    int4* dst = reinterpret_cast<int4*>(a.state_out + r0 * twoL);
+    const int4* fin_row = reinterpret_cast<const int4*>(a.state_in + r0 * twoL);
+    const int4* frs_row = reinterpret_cast<const int4*>(a.reset_state ? a.reset_state + r0 * twoL : a.state_in);
+    if (a.in_place) {
+        if (dirty == 0ull) return;
+        // dirty and fb_in never share a relator (a failed env is not dirty)
+        if (fb_rst == 0ull && R == ENVS) {
+            // the common case (wave-uniform): every image dword read first (one LDS wait, not one
+            // per chunk), then the dirty chunks stored
+            uint32_t v[PT::U];
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u) v[u] = img[lane + u * WAVE];
+#pragma unroll
+            for (int u = 0; u < PT::U; ++u) {
+                const int c = lane + u * WAVE;
+                if ((dirty >> (c / HALF)) & 1ull) out16<NT_WRITEBACK, false>(dst + c, widen4(v[u]));
+            }
+            return;
+        }
+#pragma unroll
+        for (int u = 0; u < PT::U; ++u) {
+            const int c = lane + u * WAVE;
+            if (c >= nc) continue;
+            const int q = c / HALF;
+            if (!((dirty >> q) & 1ull)) continue;
+            if ((fb_rst >> q) & 1ull) dst[c] = frs_row[c];
+            else out16<NT_WRITEBACK, false>(dst + c, widen4(img[c]));
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PT::U; ++u) {
+            const int c = lane + u * WAVE;
+            if (c >= nc) continue;
+            const int q = c / HALF;
+            if ((fb_rst >> q) & 1ull) dst[c] = frs_row[c];
+            else if ((fb_in >> q) & 1ull) dst[c] = fin_row[c];
+            else dst[c] = widen4(img[c]);
+        }
+    }
 }
 
 // acx_step_lengths (in place, lengths in and out).  At L = 128 the tile's LDS allows 4 waves per
@@ -3250,7 +3546,9 @@ int launch_step(StepArgs a, hipStream_t s) {
     }
     if constexpr (!LEARN && small_step_ok<NW, LC, VEC>()) {
         if (a.B <= SMALL_STEP_MAX_B) {
-            step_small_kernel<NW, LC, VEC><<<dim3(grid_for(a.B)), dim3(BLOCK), shm, s>>>(a);
+            constexpr int per_block = WPB * PairLayout<LC>::ENVS;
+            step_pair_kernel<NW, LC, VEC><<<dim3((unsigned)((a.B + per_block - 1) / per_block)), dim3(BLOCK),
+                                            WPB * PairLayout<LC>::wave_bytes, s>>>(a);
             return finish_launch();
         }
     }

@@ -767,6 +767,53 @@ def test_headline_rollout_every_env_vs_oracle():
     assert int(ec.item()) == 0
 
 
+def test_packed_rollout_full_horizon_every_env_vs_oracle():
+    """The packed-move-id rollout path at full size: BASELINE configs[2]'s own
+    horizon -- 2^20 Miller-Schupp starts, L = 36, ONE ops.RolloutPlan launch of K = 200 steps with
+    the int32 obs trajectory, so the move ids go through acx_pack_actions (ops.packs_actions: an
+    int32 trajectory longer than 32 steps).  Against the C oracle's batched ACEnv.step with
+    same-step autoreset (training.py:221-356's collection loop): every env's reward / done /
+    truncated at every step, the final state and step count of every env (step 200 truncates and
+    resets every env whose episode never ended), and the obs rows of a 4,096-env sample at every step."""
+    import bench
+    from acx import ops
+    L, B, K, H = 36, 1 << 20, 200, 200
+    assert ops.packs_actions(K, torch.zeros(1, dtype=torch.int32))
+    init = bench.ms_starts(L, B)
+    starts = torch.as_tensor(init).to(DEV)
+    state = starts.clone()
+    cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(6)
+    acts = torch.randint(0, 12, (K, B), dtype=torch.int32, device=DEV, generator=g)
+    obs = torch.empty((K, B, 2 * L), dtype=torch.int32, device=DEV)  # 60 GB of HBM
+    rew = torch.empty((K, B), dtype=torch.int32, device=DEV)
+    dn = torch.empty((K, B), dtype=torch.uint8, device=DEV)
+    tr = torch.empty((K, B), dtype=torch.uint8, device=DEV)
+    err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    ec = torch.zeros(1, dtype=torch.int32, device=DEV)
+    plan = ops.RolloutPlan(state, starts, cnt, T=K, horizon=H, cyclical=True, obs_traj=obs, reward_traj=rew,
+                           done_traj=dn, trunc_traj=tr, err=err, err_count=ec)
+    plan(acts)
+    torch.cuda.synchronize()
+    sample = torch.as_tensor(np.random.default_rng(6).choice(B, 4096, replace=False)).to(DEV)
+    obs_s = obs[:, sample].cpu().numpy()
+    del obs
+    sample = sample.cpu().numpy()
+    R, D, T, A = rew.cpu().numpy(), dn.cpu().numpy(), tr.cpu().numpy(), acts.cpu().numpy()
+    s = init.copy()
+    c = np.zeros(B, np.int32)
+    for t in range(K):
+        r, d_, t_, e, _, _ = O.env_step(s, A[t], L, H, c, reset_state=init)
+        assert not e.any()
+        assert np.array_equal(R[t], r), t
+        assert np.array_equal(D[t], d_) and np.array_equal(T[t], t_), t
+        assert np.array_equal(obs_s[t], s[sample]), t
+    assert T[K - 1].sum() > B // 2  # the horizon ends on the last step for every env that never finished
+    assert np.array_equal(state.cpu().numpy(), s) and np.array_equal(cnt.cpu().numpy(), c)
+    assert int(ec.item()) == 0
+
+
 def test_config5_shard_every_env_vs_oracle():
     """BASELINE configs[4]'s per-GPU shard (2^20 envs, L = 128, Miller-Schupp starts, random moves,
     horizon 200) through VecACEnv.step -- acx_step_lengths once the rows' lengths are current --

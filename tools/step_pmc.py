@@ -3,7 +3,7 @@
 Miller-Schupp starts, uniform moves, horizon 200 -- W + K calls each, at L = 128 then L = 36.
 
     rocprofv3 --pmc SQ_WAVE_CYCLES ... -d gpurun_out/pmc -o pmc -- python3 tools/step_pmc.py
-    ... -- python3 tools/step_pmc.py --L 36 --B 65536 --K 50   (config 2's launch: step_small_kernel)
+    ... -- python3 tools/step_pmc.py --L 36 --B 65536 --K 50   (config 2's launch: step_pair_kernel)
 """
 import argparse
 import os
