@@ -33,6 +33,7 @@ SIGNATURES = {
     "acx_step_record": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_step_next": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_curriculum_workspace": ([_I64], ctypes.c_int64),
+    "acx_learner_failure_word": ([_I64], ctypes.c_int64),
     "acx_curriculum_assign": ([_P, _P, _P, _I64] + [_P] * 7 + [_I64, _I32, _P], ctypes.c_int),
     "acx_learner_step": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 4 + [_I64] + [_P] * 4 + [_I64, _I32, _I32, _I32, _P],
                          ctypes.c_int),

@@ -66,6 +66,9 @@ class CurriculumRecord:
         env.episode_actions_many (one copy for all of them); envs the device placed (round 1) take env.curr_index[i]; envs it
         flagged are drawn here and placed with env.place (obs_out: the step's observation row
         buffer, as for LearnerEnv.place).  Returns [(env, state index)] for every restart."""
+        if hasattr(env, "failed") and env.failed():
+            raise RuntimeError("LearnerEnv: a curriculum ranking gave up (acx_learner_step's sticky failure word: "
+                               "needs_host 3 or a stale next_index); call env.reset_workspace() before stepping on")
         d = np.asarray(done.cpu() if hasattr(done, "cpu") else done).astype(bool)
         t = np.asarray(truncated.cpu() if hasattr(truncated, "cpu") else truncated).astype(bool)
         fin = np.nonzero(d | t)[0]
@@ -81,8 +84,8 @@ class CurriculumRecord:
         out = []
         hv = np.asarray(needs_host.cpu() if hasattr(needs_host, "cpu") else needs_host)
         if (hv == 3).any():
-            raise RuntimeError("LearnerEnv: the device could not rank the finished envs (needs_host 3: a curriculum "
-                               "workspace shared by concurrent launches)")
+            raise RuntimeError("LearnerEnv: the device could not rank the finished envs (needs_host 3: a ranking wait "
+                               "gave up); call env.reset_workspace() before stepping on")
         for i in fin.tolist():
             if d[i]:
                 self.on_done(i, acts[i])

@@ -15,8 +15,9 @@ launch, the curriculum's ranking fused into the step -- per step:
     take the next unprocessed initial state in env order.  Once every initial state has been
     used the reference draws random solved/unsolved states with Python `random` (:337-346);
     those envs are flagged in `needs_host` and placed by `place()`.  needs_host 3: the device
-    could not rank the env (a workspace shared by concurrent launches) -- CurriculumRecord.process
-    raises.
+    could not rank the env (a ranking wait gave up) -- CurriculumRecord.process raises, as it does
+    on the workspace's sticky failure word (`failed()`); `reset_workspace()` recovers.  One
+    LearnerEnv's steps must not run concurrently (they share the workspace; unsupported).
 """
 
 from __future__ import annotations
@@ -59,6 +60,21 @@ class LearnerEnv:
         self.done = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros(num_envs, dtype=torch.uint8, device=dev)
         self._ws = torch.zeros(int(_lib.load().acx_curriculum_workspace(num_envs)), dtype=torch.int32, device=dev)
+        self._fail_word = int(_lib.load().acx_learner_failure_word(num_envs))
+
+    def failed(self) -> bool:
+        """True once a ranking of acx_learner_step gave up (acx.h: needs_host 3, or the last tile's
+        total never arrived and next_index is stale); every later step ranks nothing until
+        reset_workspace().  One small device-to-host copy."""
+        return bool(self._ws[self._fail_word: self._fail_word + 2].any().item())
+
+    def reset_workspace(self) -> None:
+        """After a failed ranking: re-zero the curriculum workspace and restore next_index in round 1
+        (every finished env the device did rank holds its state in curr_index, acx.h)."""
+        self._ws.zero_()
+        if int(self.next_index.item()) < self.n_states:
+            nxt = max(int(self.next_index.item()), int(self.curr_index.max().item()) + 1)
+            self.next_index.fill_(min(nxt, self.n_states))
 
     @property
     def state(self) -> torch.Tensor:

@@ -254,8 +254,8 @@ struct Engine {
         L = L_;
         kw = acx_key_words(L);
         pk = (HDR + 6 * L + 63) / 64;
-        frontier.init(pk);
-        unexpanded.init(pk);
+        frontier.init(pk, &pkeys);
+        unexpanded.init(pk, &pkeys);
         cyc = cyc_;
         max_nodes = max_nodes_;
         cap = max_nodes + 12;
@@ -407,51 +407,49 @@ struct Engine {
         }
     }
 
-    struct Heap {  // 4-ary min-heap of node ids on their packed keys (pk words, inline)
+    // the nodes' heap keys (pk words per node id, prio_key), written once when a node is appended
+    std::vector<uint64_t> pkeys;
+
+    // 4-ary min-heap of node ids ordered by their heap keys.  An entry is the key's first word
+    // (total | path length | the first 24 letter bits: nearly always decides) and the id, 16 bytes;
+    // the rest of the key is read from pkeys only on a tie of first words.  (Round 5's entries
+    // held the whole key inline, 8 + 8 * pk bytes, copied at every level of a sift.)
+    struct Heap {
+        struct Ent {
+            uint64_t k0;
+            int64_t id;
+        };
         int pk = 0;
-        std::vector<uint64_t> k;
-        std::vector<int64_t> id;
-        bool less(const uint64_t* x, const uint64_t* y) const {
-            if (x[0] != y[0]) return x[0] < y[0];  // total | depth | 24 letter bits: nearly always decides
+        const std::vector<uint64_t>* keys = nullptr;  // Engine::pkeys
+        std::vector<Ent> e;
+        bool less(const Ent& x, const Ent& y) const {
+            if (x.k0 != y.k0) return x.k0 < y.k0;
+            const uint64_t* a = keys->data() + (size_t)x.id * pk;
+            const uint64_t* b = keys->data() + (size_t)y.id * pk;
             for (int i = 1; i < pk; ++i)
-                if (x[i] != y[i]) return x[i] < y[i];
+                if (a[i] != b[i]) return a[i] < b[i];
             return false;
         }
-        bool empty() const { return id.empty(); }
-        void reserve(size_t n) {
-            id.reserve(n);
-            k.reserve(n * pk);
-        }
-        size_t size() const { return id.size(); }
-        int64_t top() const { return id[0]; }
-        void push(const uint64_t* key, int64_t v) {
-            size_t i = id.size();
-            id.push_back(v);
-            k.resize(k.size() + pk);
-            uint64_t tmp[32];
-            memcpy(tmp, key, 8 * pk);
+        bool empty() const { return e.empty(); }
+        size_t size() const { return e.size(); }
+        int64_t top() const { return e[0].id; }
+        void push(uint64_t k0, int64_t v) {
+            size_t i = e.size();
+            e.push_back(Ent{k0, v});
+            const Ent x{k0, v};
             while (i > 0) {
                 const size_t par = (i - 1) / 4;
-                if (!less(tmp, &k[par * pk])) break;
-                memcpy(&k[i * pk], &k[par * pk], 8 * pk);
-                id[i] = id[par];
+                if (!less(x, e[par])) break;
+                e[i] = e[par];
                 i = par;
             }
-            memcpy(&k[i * pk], tmp, 8 * pk);
-            id[i] = v;
+            e[i] = x;
         }
         void pop() {
-            const size_t n = id.size() - 1;
-            if (n == 0) {
-                id.clear();
-                k.clear();
-                return;
-            }
-            uint64_t tmp[32];
-            memcpy(tmp, &k[n * pk], 8 * pk);
-            const int64_t v = id[n];
-            id.pop_back();
-            k.resize(n * pk);
+            const size_t n = e.size() - 1;
+            const Ent x = e[n];
+            e.pop_back();
+            if (n == 0) return;
             size_t i = 0;
             while (true) {
                 const size_t c0 = 4 * i + 1;
@@ -459,44 +457,40 @@ struct Engine {
                 size_t best = c0;
                 const size_t ce = c0 + 4 < n ? c0 + 4 : n;
                 for (size_t c = c0 + 1; c < ce; ++c)
-                    if (less(&k[c * pk], &k[best * pk])) best = c;
-                if (!less(&k[best * pk], tmp)) break;
-                memcpy(&k[i * pk], &k[best * pk], 8 * pk);
-                id[i] = id[best];
+                    if (less(e[c], e[best])) best = c;
+                if (!less(e[best], x)) break;
+                e[i] = e[best];
                 i = best;
             }
-            memcpy(&k[i * pk], tmp, 8 * pk);
-            id[i] = v;
+            e[i] = x;
         }
-        const uint64_t* top_key() const { return k.data(); }
     };
     // one heap per total (the priority key's top 9 bits): a pop sifts through the nodes of the
     // smallest total only, not the whole frontier (10^6 nodes: ~10 cold levels per pop); the order
     // is the single heap's, since the total is the key's most significant field
     struct BucketHeap {
         static constexpr int NB = 512;
-        int pk = 0;
         int minb = NB;  // the smallest non-empty bucket (NB: none)
         size_t n = 0;
         std::vector<Heap> b;
-        void init(int pk_) {
-            pk = pk_;
+        void init(int pk, const std::vector<uint64_t>* keys) {
             b.assign(NB, Heap{});
-            for (Heap& h : b) h.pk = pk;
+            for (Heap& h : b) {
+                h.pk = pk;
+                h.keys = keys;
+            }
             minb = NB;
             n = 0;
         }
-        static int bucket_of(const uint64_t* key) { return (int)(key[0] >> 55); }
         bool empty() const { return n == 0; }
         size_t size() const { return n; }
-        void push(const uint64_t* key, int64_t v) {
-            const int i = bucket_of(key);
-            b[(size_t)i].push(key, v);
+        void push(uint64_t k0, int64_t v) {
+            const int i = (int)(k0 >> 55);
+            b[(size_t)i].push(k0, v);
             if (i < minb) minb = i;
             ++n;
         }
         int64_t top() const { return b[(size_t)minb].top(); }
-        const uint64_t* top_key() const { return b[(size_t)minb].top_key(); }
         void pop() {
             b[(size_t)minb].pop();
             --n;
@@ -549,10 +543,11 @@ struct Engine {
         depth.push_back(dep);
         cache_slot.push_back(-1);
         recent_insert(id, h);
-        uint64_t pkey[32];
+        pkeys.resize(pkeys.size() + pk);
+        uint64_t* pkey = &pkeys[(size_t)id * pk];
         prio_key(k, tot, dep, pkey);
-        frontier.push(pkey, id);
-        unexpanded.push(pkey, id);
+        frontier.push(pkey[0], id);
+        unexpanded.push(pkey[0], id);
         return id;
     }
 
@@ -623,11 +618,7 @@ struct Engine {
     }
 
     // the smallest frontier nodes without usable cached children (greedy expands them next)
-    void push_unexpanded(int64_t id) {
-        uint64_t pkey[32];
-        prio_key(&keys[(size_t)id * kw], total[id], depth[id], pkey);
-        unexpanded.push(pkey, id);
-    }
+    void push_unexpanded(int64_t id) { unexpanded.push(pkeys[(size_t)id * pk], id); }
 
     // the smallest frontier nodes without usable cached children (greedy expands them next)
     void select(std::vector<int64_t>& out) {
@@ -681,10 +672,11 @@ struct Engine {
         cur = 0;
         gen_lo[0] = gen_lo[1] = 0;
         recent_insert(0, host_hash(root, kw));
-        uint64_t pkey[32];
-        prio_key(root, tot0, 0, pkey);
-        frontier.push(pkey, 0);
-        unexpanded.push(pkey, 0);
+        pkeys.assign(pk, 0ull);
+        pkeys.reserve(nres * pk);
+        prio_key(root, tot0, 0, pkeys.data());
+        frontier.push(pkeys[0], 0);
+        unexpanded.push(pkeys[0], 0);
         std::vector<int64_t> batch;
         while (status == 0) {
             const int64_t t0 = now_ns();
@@ -712,7 +704,7 @@ struct Engine {
                     if (cache_slot[id] >= 0) {  // expanded before the last AGE appends: expand again
                         ++st_stop_aged;
                         drop_cache(id);
-                        unexpanded.push(frontier.top_key(), id);
+                        push_unexpanded(id);
                     } else if (id >= n_sel) {
                         ++st_stop_new;
                     } else {

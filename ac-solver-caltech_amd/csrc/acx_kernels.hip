@@ -1968,8 +1968,8 @@ struct StepArgs {
     // moves to one row -- coalesced -- instead of one cache line per lane
     int32_t* hist_base;
     int64_t hist_t;
-    // tests only (acx_internal_learner_ranking_fails): every ranking wait gives up at once, as one
-    // that polled 2^20 times would (needs_host = 3)
+    // tests only (acx_internal_learner_ranking_fails): ranking waits give up at once, as one that
+    // polled 2^20 times would (1: every wait, needs_host = 3; 2: only the last tile's total)
     int cur_fail;
 };
 
@@ -1994,10 +1994,17 @@ struct StepArgs {
 //     and reads as not there.  Every wave reads the sequence number before it publishes, so once
 //     every group is complete no wave of the launch reads it again and the last tile may advance it;
 //   * HIP promises no dispatch order: a tile that polls too long (2^20 polls, ~seconds -- an
-//     earlier tile never scheduled, or a workspace shared by concurrent launches) gives up and flags
-//     its finished envs needs_host = 3 (CurriculumRecord.process raises), so the launch always ends.
-// cur_ws (uint64 words): [0] sequence number, [1] base, [2] reserved, [3, 3 + T) tile counts,
-// [3 + T, 3 + T + G) group totals, [3 + T + G, 3 + T + 2G) group arrival words (T tiles, G groups).
+//     earlier tile never scheduled) gives up and flags its finished envs needs_host = 3
+//     (CurriculumRecord.process raises), so the launch always ends.  Any give-up -- a tile's
+//     prefix, or the last tile's total, after which next_index is stale -- also sets the sticky
+//     word [2]: every later launch then ranks nothing (its finished envs get needs_host = 3) until
+//     the host re-zeroes the workspace (LearnerEnv.reset_workspace, which also restores
+//     next_index from curr_index), since a give-up can leave a group's arrival word incomplete;
+//     CurriculumRecord.process raises on the word.  Concurrent launches on one workspace are not
+//     supported (they would overwrite each other's words; nothing detects it).
+// cur_ws (uint64 words): [0] sequence number, [1] base, [2] sticky failure word, [3, 3 + T) tile
+// counts, [3 + T, 3 + T + G) group totals, [3 + T + G, 3 + T + 2G) group arrival words (T tiles,
+// G groups).
 // ---------------------------------------------------------------------------------
 constexpr uint64_t CUR_SET = 1ull << 62;
 constexpr uint32_t CUR_FAIL = 0xffffffffu;
@@ -2040,15 +2047,24 @@ struct CurLayout {
 // (so the add's return trip overlaps the stores) made the step slower, fresh episodes 0.143 vs
 // 0.140 ms and steady state 0.21 vs 0.172 (same buffers, r05v), as later tiles then wait longer
 // for the group total
-__device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt) {
+// cnext: next_index as this wave read it, before publishing -- the last tile overwrites it once
+// every tile has published, so the read must complete first: the published word takes an opaque
+// dependency on it, both words being relaxed agent-scope atomics
+__device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
+                                                int64_t cnext) {
     if (w.lane != 0) return 0;
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     if (t == 0) cur_store(c.base, cur_word(seq, (uint32_t)*a.cur_next));
-    cur_store(c.tile + t, cur_word(seq, cnt));
+    uint64_t word = cur_word(seq, cnt);
+    asm volatile("" : "+v"(word) : "s"((uint32_t)cnext));
+    cur_store(c.tile + t, word);
     return __hip_atomic_fetch_add(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, (1ull << 32) | cnt, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
 }
+// the sticky failure word (cur_ws[2], see above)
+__device__ __forceinline__ void cur_set_failed(const StepArgs& a) { cur_store(a.cur_ws + 2, 1ull); }
+
 // the add that completed its group publishes the group's total and clears the arrival word for
 // the next launch
 __device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
@@ -2071,7 +2087,7 @@ __device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx
 // round; the base (lane 0) and the own group's earlier tile counts (a lane each) with the first.
 // (s_sleep 8 between polls instead: the same, r05v)
 __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, bool all_groups) {
-    if (a.cur_fail) return CUR_FAIL;
+    if (a.cur_fail == 1 || (a.cur_fail == 2 && all_groups)) return CUR_FAIL;  // test hook
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     const int64_t ng = all_groups ? c.groups : g;  // whole groups summed
@@ -2174,6 +2190,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
                                     __hip_atomic_load(a.cur_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                               : 0;
     const bool exhausted = cur && cnext >= a.n_states;
+    // a give-up in an earlier launch (cur_set_failed) left the workspace unusable until the host
+    // re-zeroes it: this launch ranks nothing
+    const bool broken = cur && __builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws + 2)) != 0;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2295,7 +2314,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     if (cur) {
         fm = __ballot(fin);
         const uint32_t cnt = (uint32_t)__popcll(fm);
-        cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt));
+        if (!broken) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
     }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
@@ -2381,17 +2400,23 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // (the new next_index).  The copies are made by the whole wave, 16-byte chunks over the
         // lanes (copy_rows): one lane copying its own row made the steady-state step 0.165 ms
         // instead of 0.150 (r05zg).
-        const uint32_t first = (fm && !exhausted) ? cur_prefix(a, w, cseq, false) : 0u;
-        if (w.r0 + w.R == a.B) {
+        const uint32_t first = broken ? CUR_FAIL : (fm && !exhausted) ? cur_prefix(a, w, cseq, false) : 0u;
+        if (!broken && w.r0 + w.R == a.B) {
             const uint32_t tot = cur_prefix(a, w, cseq, true);
             if (w.lane == 0) {
                 // every group is complete: no wave of this launch reads next_index or the sequence
-                // number again -- advance both for the next one
-                if (tot != CUR_FAIL) *a.cur_next = (int32_t)((int64_t)tot < a.n_states ? (int64_t)tot : a.n_states);
-                cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
+                // number again -- advance both for the next one.  A total that never arrived leaves
+                // next_index stale: the workspace is marked failed (the host restores both)
+                if (tot != CUR_FAIL) {
+                    *a.cur_next = (int32_t)((int64_t)tot < a.n_states ? (int64_t)tot : a.n_states);
+                    cur_store(a.cur_ws, (uint64_t)((cseq + 1u) & CUR_SEQ_MASK));
+                } else {
+                    cur_set_failed(a);
+                }
             }
         }
         const bool failed = first == CUR_FAIL;  // wave-uniform
+        if (failed && !broken && w.lane == 0) cur_set_failed(a);
         // finished envs with index k = first + (finished envs before it in the tile) < n_states
         uint64_t take = 0;
         if (fm && !exhausted && !failed) {
@@ -3809,9 +3834,12 @@ int acx_step_record(const int32_t* state_in, int32_t* state_out, const int32_t* 
 // acx_curriculum.hip: where acx_learner_step's part of the shared workspace starts (int32 words)
 int64_t acx_internal_curriculum_fused_offset(int64_t B);
 
+int64_t acx_learner_failure_word(int64_t B) { return acx_internal_curriculum_fused_offset(B) + 4; }  // cur_ws[2]
+
 static int g_learner_fail = 0;  // tests only
-// tests only: acx_learner_step's ranking gives up at once (1) or works (0)
-void acx_internal_learner_ranking_fails(int32_t on) { g_learner_fail = on != 0; }
+// tests only: acx_learner_step's ranking polls give up at once: 1 every one, 2 only the last tile's
+// total (next_index), 0 none
+void acx_internal_learner_ranking_fails(int32_t on) { g_learner_fail = on; }
 
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,

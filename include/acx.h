@@ -182,7 +182,8 @@ int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* ac
  * needs_host[env] = 1 (the reference then draws a random solved/unsolved state on the host).
  * workspace: acx_curriculum_workspace(B) int32 device words, 8-byte aligned, zeroed before the
  * first call and not written by the caller afterwards (acx_learner_step keeps its look-back state
- * there; one workspace serves both calls, but not two launches at once).  For even L the row
+ * there; one workspace serves both calls; concurrent launches on one workspace are unsupported --
+ * their results are undefined and nothing detects them).  For even L the row
  * arrays (curriculum_states, state, reset_state, obs_f32) are 16-byte aligned.
  */
 int64_t acx_curriculum_workspace(int64_t B);
@@ -198,10 +199,14 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
  * workspace) and, after a tile's own stores, a finished env with index k < n_states takes initial
  * state k -- its state, obs_f32 and reset_state rows become that row as it is, curr_index[env] = k;
  * past the table's end needs_host[env] = 1.  needs_host[env] = 3: the ranking gave up (an earlier
- * tile not scheduled within ~seconds, or a workspace shared by concurrent launches); the env kept
- * its own starting row and was not ranked.  done, truncated, reset_state and the curriculum
- * arguments are required; B < 2^31; workspace = acx_curriculum_workspace(B) int32 words (above);
- * for even L, reset_state and curriculum_states 16-byte aligned (as state and obs_f32).
+ * tile not scheduled within ~seconds); the env kept its own starting row and was not ranked.  Any
+ * give-up -- a tile's ranking, or the last tile's total, after which *next_index is stale -- also
+ * sets the workspace's sticky failure word (acx_learner_failure_word); from then on every launch
+ * ranks nothing (finished envs: needs_host 3) until the caller re-zeroes the workspace and
+ * restores *next_index (max(curr_index) + 1 in round 1: every finished env that was ranked holds
+ * its state).  done, truncated, reset_state and the curriculum arguments are required; B < 2^31;
+ * workspace = acx_curriculum_workspace(B) int32 words (above); for even L, reset_state and
+ * curriculum_states 16-byte aligned (as state and obs_f32).
  */
 int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* action_i64, int32_t* reset_state,
                      int32_t* step_count, float* obs_f32, float* reward_f32, float* done_f32, uint8_t* done,
@@ -209,6 +214,9 @@ int acx_learner_step(int32_t* state, const int32_t* action, const int64_t* actio
                      int32_t* episode_len, uint8_t* err, int32_t* err_count, const int32_t* curriculum_states,
                      int64_t n_states, int32_t* next_index, int32_t* curr_index, uint8_t* needs_host,
                      int32_t* workspace, int64_t B, int32_t L, int32_t horizon, int32_t cyclical, void* stream);
+/* the int32 index, in a workspace of acx_curriculum_workspace(B) words, of acx_learner_step's
+ * sticky failure word (a uint64: 0 while every ranking has completed) */
+int64_t acx_learner_failure_word(int64_t B);
 
 /*
  * T fused env steps (PPO rollout collection).  state (B,2L) and step_count (B) are

@@ -110,21 +110,38 @@ def test_rollout_refuses_per_env_state_it_cannot_keep():
         r.rollout(acts[:2])
 
 
-def test_reset_takes_starting_states_unvalidated():
+@pytest.mark.parametrize("L", [36, 128])
+def test_reset_takes_starting_states_unvalidated(L):
     """reset(options={"starting_states": rows}) copies the rows as the reference's ACEnv.reset
     does (ac_env.py:113-129, no validation); an out-of-domain row is then held as it is and
-    reported with err 3 by every step, its exact values kept."""
+    reported with err 3 by every step, its exact values kept.  At L = 128 VecACEnv.step
+    takes the lengths-carrying kernel (acx_step_lengths, LIVE loads from _row_extent), at L = 36
+    acx_step.  An out-of-domain row that only an autoreset brings in (env 20's
+    starting row, its episode truncated at the horizon) is taken the same way: the env's row becomes
+    that row's exact values, err 3, count 0, and stays so."""
     from acx.envs.ac_env import VecACEnv
-    B, L = 128, 36
-    env = VecACEnv(_starts(L, B), horizon_length=50, device=DEV)
+    B, H = 128, 3
+    env = VecACEnv(_starts(L, B), horizon_length=H, device=DEV)
     rows = _starts(L, B)
+    rows[::3] = rows[1]  # no trivial starts: env 20's episode runs to the horizon
     assert rows[5, 2] != 0
     rows[5, 1] = 0  # a zero inside relator 0 (its letters continue after it)
     rows[9, L] = 7  # a letter outside the packed domain
     env.reset(options={"starting_states": rows})
     assert torch.equal(env.state.cpu(), torch.as_tensor(rows))
-    env.step(torch.zeros(B, dtype=torch.int32, device=DEV))
-    err = env.err.cpu().numpy()
-    assert err[5] == 3 and err[9] == 3 and (np.delete(err, [5, 9]) == 0).all()
-    st = env.state.cpu().numpy()
-    assert np.array_equal(st[5], rows[5]) and np.array_equal(st[9], rows[9])
+    bad20 = rows[20].copy()
+    bad20[L + 2] = -9  # env 20's starting row, out of the domain; its current row is not
+    env.reset_state[20].copy_(torch.as_tensor(bad20))
+    g = torch.Generator(device=DEV)
+    g.manual_seed(L)
+    for t in range(H + 2):
+        env.step(torch.randint(0, 12, (B,), dtype=torch.int32, device=DEV, generator=g))
+        err = env.err.cpu().numpy()
+        st = env.state.cpu().numpy()
+        assert err[5] == 3 and err[9] == 3, t
+        assert np.array_equal(st[5], rows[5]) and np.array_equal(st[9], rows[9]), t
+        if t < H - 1:
+            assert err[20] == 0, t
+        else:  # step H truncates env 20: autoreset to its out-of-domain starting row
+            assert err[20] == 3 and np.array_equal(st[20], bad20), t
+            assert int(env.step_count[20].item()) == 0, t

@@ -274,8 +274,8 @@ def test_fused_learner_step_out_of_domain_curriculum_row():
 def test_fused_learner_step_ranking_failure():
     """The one-launch step's ranking giving up (test hook: as a wait of 2^20 polls would, e.g. a
     tile never scheduled) flags its finished envs needs_host = 3 and leaves each at its own
-    starting row with next_index unchanged; CurriculumRecord.process raises on it; the next
-    launches rank normally."""
+    starting row with next_index unchanged and the sticky failure word set; CurriculumRecord.process
+    raises on it; after LearnerEnv.reset_workspace() the launches rank normally."""
     import ctypes
     from acx import _lib
     from acx.agents import CurriculumRecord, LearnerEnv
@@ -300,10 +300,59 @@ def test_fused_learner_step_ranking_failure():
     assert bool((nh == 3).all())
     assert torch.equal(env.state, torch.as_tensor(init[:B]).to(DEV))  # own starting rows
     assert int(env.next_index.item()) == B and bool((env.vec.step_count == 0).all())
+    assert env.failed()
     with pytest.raises(RuntimeError):
         rec.process(env, done, trunc, nh)
+    env.reset_workspace()
+    assert not env.failed() and int(env.next_index.item()) == B
     env.step(acts())
     done, trunc, _, nh = env.step(acts())  # all truncate again: ranked normally now
     assert bool((nh == 0).all()) and int(env.next_index.item()) == 2 * B
     assert torch.equal(env.curr_index, torch.arange(B, 2 * B, dtype=torch.int32, device=DEV))
     assert torch.equal(env.state, torch.as_tensor(init[B: 2 * B]).to(DEV))
+
+
+def test_fused_learner_step_last_total_failure():
+    """only the last tile's wait for the batch total gives up (test hook 2).  Every
+    tile still ranks its finished envs (they take states B..2B-1), but next_index is stale: the
+    launch sets the sticky failure word, CurriculumRecord.process raises, and later launches rank
+    nothing (needs_host 3, envs at their own starting rows) until LearnerEnv.reset_workspace()
+    re-zeroes the workspace and restores next_index from curr_index; then ranking resumes with
+    state 2B, so no initial state is handed out twice."""
+    import ctypes
+    from acx import _lib
+    from acx.agents import CurriculumRecord, LearnerEnv
+    L, B, N, H = 36, 2048, 9000, 2
+    init = _ms_states(L, N)
+    env = LearnerEnv(init, B, horizon_length=H, device=DEV)
+    rec = CurriculumRecord(N, B, 0.5)
+    hook = _lib.load().acx_internal_learner_ranking_fails
+    hook.argtypes = [ctypes.c_int32]
+    hook.restype = None
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    acts = lambda: torch.randint(0, 12, (B,), dtype=torch.int64, device=DEV, generator=g)  # noqa: E731
+    env.step(acts())
+    hook(2)
+    try:
+        done, trunc, _, nh = env.step(acts())  # every env truncates at H = 2
+    finally:
+        hook(0)
+    assert bool((done | trunc).bool().all()) and bool((nh == 0).all())
+    assert torch.equal(env.curr_index, torch.arange(B, 2 * B, dtype=torch.int32, device=DEV))
+    assert torch.equal(env.state, torch.as_tensor(init[B: 2 * B]).to(DEV))
+    assert int(env.next_index.item()) == B  # stale: the total never arrived
+    assert env.failed()
+    with pytest.raises(RuntimeError):
+        rec.process(env, done, trunc, nh)
+    env.step(acts())
+    done, trunc, _, nh = env.step(acts())  # truncate again: nothing is ranked now
+    assert bool((nh == 3).all()) and int(env.next_index.item()) == B
+    assert torch.equal(env.state, torch.as_tensor(init[B: 2 * B]).to(DEV))
+    env.reset_workspace()
+    assert not env.failed() and int(env.next_index.item()) == 2 * B
+    env.step(acts())
+    done, trunc, _, nh = env.step(acts())
+    assert bool((nh == 0).all()) and int(env.next_index.item()) == 3 * B
+    assert torch.equal(env.curr_index, torch.arange(2 * B, 3 * B, dtype=torch.int32, device=DEV))
+    assert torch.equal(env.state, torch.as_tensor(init[2 * B: 3 * B]).to(DEV))

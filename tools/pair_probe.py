@@ -49,7 +49,7 @@ def patched_source():
            "if (lane == 0 && a.final_obs) { uint64_t* P_ = reinterpret_cast<uint64_t*>(a.final_obs) + "
            f"((int64_t)blockIdx.x * WPB + wid) * {NST}; for (int i_ = 0; i_ < {NST}; ++i_) P_[i_] = PT_[i_]; }} }}")
     st = body.index("    // the state store.  Relator masks")
-    tail = body[st:].replace("return;", end + " return;")
+    tail = body[st:].replace("return;", "{ " + end + " return; }")
     body = body[:st] + tail[:-2] + "    " + end + "\n}\n"
     ins("        if (h == 0 && a.final_obs) {", "        if (false) {  // final_obs carries the probe buffer\n")
     body = body.replace("        if (false) {  // final_obs carries the probe buffer\n        if (h == 0 && a.final_obs) {",
