@@ -939,9 +939,15 @@ struct CodeTile {
         lim[2 * lane + 1] = (uint8_t)live_chunks(n1);
         limv = (uint32_t)live_chunks(n0) | ((uint32_t)live_chunks(n1) << 8);
     }
-    // see FastTile::widen_lim
+    // see FastTile::widen_lim; rounded up to whole 64-byte sectors (4 chunks; relators start on a
+    // sector at L % 32 == 0): the chunks past the letters in the last sector hold zero padding in
+    // HBM and in the tile, and a partly written sector was a read-modify-write in HBM
     __device__ __forceinline__ void widen_lim(int lane, int n0, int n1) {
-        const int a = max((int)(limv & 0xffu), live_chunks(n0)), b = max((int)(limv >> 8), live_chunks(n1));
+        int a = max((int)(limv & 0xffu), live_chunks(n0)), b = max((int)(limv >> 8), live_chunks(n1));
+        if constexpr (L % 32 == 0) {
+            a = min(HALF, (a + 3) & ~3);
+            b = min(HALF, (b + 3) & ~3);
+        }
         lim[2 * lane] = (uint8_t)a;
         lim[2 * lane + 1] = (uint8_t)b;
         limv = (uint32_t)a | ((uint32_t)b << 8);
@@ -2611,82 +2617,102 @@ __global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
         wave_sync();
     }
 
-    // this lane's relator -> planes; the partner's by DPP
+    // this lane's relator -> planes and its reversal; the partner's by DPP
+    const bool cyc = a.cyclical != 0;
     Planes<1> w;
     int n;
     bool bad = pair_pack<HALF>(mine, w, n) || flagged;
-    PlaneRegs<1> p;
+    const Planes<1> rw = pl::prev<1>(w, n);
+    bool clean = pl::relator_clean<1>(w, n, cyc);
+    Planes<1> pw, prw;
+    int pn;
     {
-        Planes<1> wp;
-        wp.s[0] = pair_xchg64(w.s[0]);
-        wp.y[0] = pair_xchg64(w.y[0]);
-        const uint32_t np = pair_xchg((uint32_t)n | (bad ? 0x100u : 0u));
-        bad = bad || (np & 0x100u) != 0u;
-        p.w0 = h ? wp : w;
-        p.w1 = h ? w : wp;
-        p.n0 = h ? (int)(np & 0xffu) : n;
-        p.n1 = h ? n : (int)(np & 0xffu);
+        pw.s[0] = pair_xchg64(w.s[0]);
+        pw.y[0] = pair_xchg64(w.y[0]);
+        prw.s[0] = pair_xchg64(rw.s[0]);
+        prw.y[0] = pair_xchg64(rw.y[0]);
+        const uint32_t x = pair_xchg((uint32_t)n | (bad ? 0x100u : 0u) | (clean ? 0x200u : 0u));
+        pn = (int)(x & 0xffu);
+        bad = bad || (x & 0x100u) != 0u;
+        clean = clean && (x & 0x200u) != 0u;
     }
 
-    // the env's move, computed by both of its lanes (step_body's contract)
-    int cnt = 0, e = ACX_ERR_NONE;
+    // the env's move: on a clean env (both relators reduced) each lane runs its relator's part of
+    // it (pl::pair_move_clean: the target lane moves, its partner keeps its relator); otherwise
+    // (an unreduced start: rare) both lanes run the general move on the whole env
+    int e = ACX_ERR_NONE;
+    bool general = false;
+    if (active) {
+        if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
+        else if (bad) e = ACX_ERR_DOMAIN;
+        else if (clean) e = pl::pair_move_clean(w, n, rw, pw, pn, prw, h, act, L, cyc);
+        else general = true;
+    }
+    if (general) {
+        PlaneRegs<1> q;
+        q.w0 = h ? pw : w;
+        q.w1 = h ? w : pw;
+        q.n0 = h ? pn : n;
+        q.n1 = h ? n : pn;
+        const pl::MoveOut<1> mo = pl::ac_move_call<1>(q, act, L, cyc);
+        e = mo.e;
+        w = h ? mo.p.w1 : mo.p.w0;
+        n = h ? mo.p.n1 : mo.p.n0;
+    }
+    // the env's code is its target lane's (ac_moves.py:167-179: relator (id + 1) & 1; every other
+    // outcome is the same on both lanes); the partner's new length and letter-0 y bit
+    bool xy = false;  // the relators' first letters: one x^{+-1} and one y^{+-1}
+    {
+        const uint32_t x = pair_xchg((uint32_t)e | ((uint32_t)n << 8) | ((uint32_t)(w.y[0] & 1u) << 16));
+        if (h != ((act + 1) & 1)) e = (int)(x & 0xffu);
+        pn = (int)((x >> 8) & 0xffu);
+        xy = ((x >> 16) & 1u) != (uint32_t)(w.y[0] & 1u);
+    }
+    const int n0 = h ? pn : n, n1 = h ? n : pn;
+    int cnt = 0;
     bool keep = false, triv = false, trunc = false, fin = false, reset = false;
     int32_t rwd = 0;
     if (active) {
         cnt = a.step_count ? cnt0 + 1 : 0;
-        const bool cyc = a.cyclical != 0;
-        if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
-        else if (bad) e = ACX_ERR_DOMAIN;
-        else if (pl::is_clean<1>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<1>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
-        else {
-            const pl::MoveOut<1> mo = pl::ac_move_call<1>(p, act, L, cyc);
-            p = mo.p;
-            e = mo.e;
-        }
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
-        triv = !pend && !keep && pl::is_trivial<1>(p.w0, p.n0, p.w1, p.n1);
+        // strict triviality (pl::is_trivial): both relators one letter, one x and one y
+        triv = !pend && !keep && n0 == 1 && n1 == 1 && xy;
         trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
-        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(n0 + n1);
         fin = triv || trunc;
         reset = a.pending ? pend : (fin && a.reset_state && !keep);
     }
     // this lane's relator re-imaged (a failed env keeps its loaded image)
     bool chg = false;
-    if (active && !keep) chg = pair_image<HALF>(mine, h ? p.w1 : p.w0, h ? p.n1 : p.n0);
+    if (active && !keep) chg = pair_image<HALF>(mine, w, n);
     // same-step autoreset (or a pending env's reset): the lane loads its relator of the starting
     // row into the image (FastTile::load_rows' result; an out-of-domain starting row is taken as it
     // is and stored from reset_state, FB_RESET)
     bool rbad = false;
+    int rn = n;
     if (active && reset) {
-        if (h == 0 && a.final_obs) {  // final_obs <- the post-move state (rare)
-            int32_t* fo = a.final_obs + env * twoL;
+        if (a.final_obs) {  // final_obs <- the post-move state (rare): each lane its relator
+            int32_t* fo = a.final_obs + env * twoL + h * L;
 #pragma unroll 1
-            for (int hh = 0; hh < 2; ++hh) {
-                const Planes<1>& ww = hh ? p.w1 : p.w0;
-                const int nn = hh ? p.n1 : p.n0;
-#pragma unroll 1
-                for (int k = 0; k < L; ++k) {
-                    const uint32_t code = pl::pletter<1>(ww, k);
-                    fo[hh * L + k] = k < nn ? (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu) : 0;
-                }
+            for (int k = 0; k < L; ++k) {
+                const uint32_t code = pl::pletter<1>(w, k);
+                fo[k] = k < n ? (int32_t)(int8_t)((0xFE02FF01u >> (code << 3)) & 0xffu) : 0;
             }
         }
         rbad = pair_load_relator<HALF>(mine, a.reset_state + env * twoL + h * L);
-        Planes<1> rw;
-        int rn;
-        rbad = pair_pack<HALF>(mine, rw, rn) || rbad;
-        if (h) p.n1 = rn;
-        else p.n0 = rn;
+        Planes<1> rw2;
+        rbad = pair_pack<HALF>(mine, rw2, rn) || rbad;
         chg = true;  // dm = 3: the whole row is written
     }
     // the partner's starting-row length and domain flag (every lane takes part in the DPP)
+    int ln0 = n0, ln1 = n1;  // lengths_out
     {
-        const uint32_t x = pair_xchg((uint32_t)(h ? p.n1 : p.n0) | (rbad ? 0x100u : 0u));
+        const uint32_t x = pair_xchg((uint32_t)rn | (rbad ? 0x100u : 0u));
         if (reset) {
             rbad = rbad || (x & 0x100u) != 0u;
-            if (h) p.n0 = (int)(x & 0xffu);
-            else p.n1 = (int)(x & 0xffu);
+            ln0 = h ? (int)(x & 0xffu) : rn;
+            ln1 = h ? rn : (int)(x & 0xffu);
         }
     }
     if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
@@ -2702,8 +2728,8 @@ __global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
             if (a.err) a.err[env] = (uint8_t)e;
             if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
         } else if (a.lengths_out) {
-            a.lengths_out[2 * env] = p.n0;
-            a.lengths_out[2 * env + 1] = p.n1;
+            a.lengths_out[2 * env] = ln0;
+            a.lengths_out[2 * env + 1] = ln1;
         }
     }
 

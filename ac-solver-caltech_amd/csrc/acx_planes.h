@@ -410,6 +410,77 @@ ACX_HD __forceinline__ int ac_move_clean(Planes<PW>& w0, int& n0, Planes<PW>& w1
     return ACX_ERR_NONE;
 }
 
+// ac_move_clean split over the two lanes of an env (acx_kernels.hip step_pair_kernel, one lane per
+// relator, PW = 1).  The lane holds relator h (w, n) and its reversal rw = prev(w, n); from its
+// partner it has the other relator (pw, pn) and that one's reversal (prw).  On the lane of the
+// move's target relator (ac_moves.py:167-179: i = (id + 1) & 1) it returns ac_move_clean's
+// ACX_ERR_* code and the relator becomes its result; on the other lane it returns ACX_ERR_NONE
+// (ACX_ERR_ACTION for a bad id) and leaves the relator as it is -- a clean move changes only its
+// target -- so the caller takes the env's code from the target lane.  Same results as
+// ac_move_clean:
+//   r_i <- r_i r_j^{+-1}: the junction cancellation count is the first mismatch of prev(r_i) and
+//     r_j^{+-1} (ac_moves.py:56-60), r_j^-1 = the partner's reversal with every letter inverted;
+//     the result's reversal, for the cyclic peel (utils.py:223-232), is spliced from the two
+//     reversals -- reverse(a b) = reverse(b) reverse(a) -- so each lane reverses only its own
+//     relator (ac_move_clean reverses r_i, r_j and the result);
+//   conjugation (ac_moves.py:79-156) reads only r_i.
+ACX_HD __forceinline__ int pair_move_clean(Planes<1>& w, int& n, const Planes<1>& rw, const Planes<1>& pw, int pn,
+                                           const Planes<1>& prw, int h, int action, int L, bool cyc) {
+    if ((unsigned)action >= 12u) return ACX_ERR_ACTION;
+    if ((((action + 1) & 1) != 0) != (h == 1)) return ACX_ERR_NONE;  // not the target relator
+    if (action < 4) {
+        const bool inv = (action == 1) || (action == 2);
+        const int nA = n, nJ = pn;
+        const uint64_t mJ = bmask<1>(nJ).b[0];
+        // Bw = r_j^{+-1} and its reversal (the reversal of r_j^-1 is r_j with its letters inverted)
+        Planes<1> Bw, rB;
+        Bw.y[0] = inv ? prw.y[0] : pw.y[0];
+        Bw.s[0] = inv ? (prw.s[0] ^ mJ) : pw.s[0];
+        rB.y[0] = inv ? pw.y[0] : prw.y[0];
+        rB.s[0] = inv ? (pw.s[0] ^ mJ) : prw.s[0];
+        const int mn = nA < nJ ? nA : nJ;
+        int acc = bfirst<1>(noncancel<1>(rw, Bw));
+        acc = acc < mn ? acc : mn;
+        int nn = nA + nJ - 2 * acc;
+        if (nn > L) return ACX_ERR_NONE;      // gated: no-op
+        if (nn == 0) return ACX_ERR_INVALID;  // r_i emptied (utils.py:264-266)
+        Planes<1> A = por<1>(pkeep<1>(w, nA - acc), pshl<1>(pshr<1>(Bw, acc), nA - acc));
+        if (cyc) {
+            const Planes<1> rA = por<1>(pkeep<1>(rB, nJ - acc), pshl<1>(pshr<1>(rw, acc), nJ - acc));
+            int p = bfirst<1>(noncancel<1>(A, rA));
+            p = p < (nn >> 1) ? p : (nn >> 1);  // a reduced word never peels past its middle
+            if (p > 0) {
+                A = pkeep<1>(pshr<1>(A, p), nn - 2 * p);
+                nn -= 2 * p;
+            }
+        }
+        w = A;
+        n = nn;
+        return ACX_ERR_NONE;
+    }
+    // conjugation r_i <- g r_i g^-1 (ac_move_clean's branch on the lane's own relator)
+    const uint32_t g = (CONJ_G >> (2 * (action - 4))) & 3u;
+    const uint32_t first = pletter<1>(w, 0);
+    const uint32_t last = pletter<1>(w, n - 1);
+    const bool sc = first == (g ^ 1u);
+    const bool ec = last == g;
+    if (cyc) {
+        if (sc == ec) return ACX_ERR_NONE;  // no cancellation: reduces back to r_i
+        if (sc) w = por<1>(pshr<1>(w, 1), psingle<1>(first, n - 1));  // g^-1 v -> v g^-1
+        else w = por<1>(pkeep<1>(pshl<1>(w, 1), n), psingle<1>(last, 0));  // v g -> g v
+        return ACX_ERR_NONE;
+    }
+    const int nn = n + 2 - 2 * ((int)sc + (int)ec);
+    if (nn > L) return ACX_ERR_NONE;
+    const Planes<1> mid = pkeep<1>(pshr<1>(w, (int)sc), n - (int)sc - (int)ec);
+    Planes<1> nw = pshl<1>(mid, 1 - (int)sc);
+    if (!sc) nw = por<1>(nw, psingle<1>(g, 0));
+    if (!ec) nw = por<1>(nw, psingle<1>(g ^ 1u, nn - 1));
+    w = nw;
+    n = nn;
+    return ACX_ERR_NONE;
+}
+
 // strict triviality (ac_env.py:99, utils.py:57-87): both relators one letter, one x and one y
 template <int PW>
 ACX_HD __forceinline__ bool is_trivial(const Planes<PW>& w0, int n0, const Planes<PW>& w1, int n1) {

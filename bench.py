@@ -413,8 +413,11 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
         if lens is not None:
             c_old = (n_before.clamp(0, L) + 3) // 4
             c_new = (lens.clamp(0, L) + 3) // 4
+            c_wr = torch.maximum(c_old, c_new)
+            if L % 32 == 0:  # relators start on a 64-B sector: the kernel writes whole sectors (CodeTile::widen_lim)
+                c_wr = torch.clamp((c_wr + 3) // 4 * 4, max=L // 4)
             rd += float(c_old.sum().item()) * 16
-            wr += float((torch.maximum(c_old, c_new) * ch).sum().item()) * 16
+            wr += float((c_wr * ch).sum().item()) * 16
             srd += float(sectors(c_old).sum().item()) * 64
             swr += float(sectors(torch.maximum(c_old, c_new) * ch).sum().item()) * 64
         if finished is not None:

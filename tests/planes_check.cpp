@@ -62,6 +62,28 @@ static int fail(const char* what, int L, int a, int cyc, const int32_t* in, cons
     return 1;
 }
 
+// step_pair_kernel's split of ac_move_clean (PW = 1, pl::pair_move_clean): lane h holds relator h,
+// its own reversal and the partner's relator and reversal; the env's code is the target lane's,
+// the other lane's relator must stay as it was.  false: the split broke that contract
+static bool pair_clean(const PlaneRegs<1>& p, int a, int L, bool cyc, PlaneRegs<1>& out, int& e) {
+    const Planes<1> w[2] = {p.w0, p.w1};
+    const int n[2] = {p.n0, p.n1};
+    const Planes<1> rv[2] = {pl::prev<1>(p.w0, p.n0), pl::prev<1>(p.w1, p.n1)};
+    Planes<1> nw[2] = {w[0], w[1]};
+    int nn[2] = {n[0], n[1]}, eh[2];
+    for (int h = 0; h < 2; ++h) eh[h] = pl::pair_move_clean(nw[h], nn[h], rv[h], w[1 - h], n[1 - h], rv[1 - h], h, a, L, cyc);
+    const bool bad_id = a < 0 || a >= 12;
+    const int t = bad_id ? 0 : ((a + 1) & 1);
+    e = eh[t];
+    if (nw[1 - t].s[0] != w[1 - t].s[0] || nw[1 - t].y[0] != w[1 - t].y[0] || nn[1 - t] != n[1 - t]) return false;
+    if (eh[1 - t] != (bad_id ? ACX_ERR_ACTION : ACX_ERR_NONE)) return false;
+    out.w0 = nw[0];
+    out.n0 = nn[0];
+    out.w1 = nw[1];
+    out.n1 = nn[1];
+    return true;
+}
+
 template <int PW>
 static int run(int L, int cases, std::mt19937_64& rng) {
     std::vector<int32_t> in(2 * L), out(2 * L), got(2 * L);
@@ -88,11 +110,23 @@ static int run(int L, int cases, std::mt19937_64& rng) {
                 const int b = (int)(rng() % 12);
                 std::vector<int32_t> base(got), o2(2 * L), g2(2 * L);
                 const int e1 = acx_oracle_move(base.data(), L, b, cyc, o2.data(), lens);
+                PlaneRegs<PW> q0 = q;
                 const int e2 = pl::ac_move_clean<PW>(q.w0, q.n0, q.w1, q.n1, b, L, cyc != 0);
                 from_planes<PW>(q, L, g2.data());
                 const int32_t* w2 = e1 ? base.data() : o2.data();
                 if (e1 != e2 || memcmp(w2, g2.data(), 8 * L) != 0)
                     return fail("ac_move_clean", L, b, cyc, base.data(), w2, g2.data(), e1, e2);
+                if constexpr (PW == 1) {
+                    PlaneRegs<1> r;
+                    int e3;
+                    const int bb = (int)(rng() % 14) - 1;  // the bad ids too
+                    const int e4 = acx_oracle_move(base.data(), L, bb, cyc, o2.data(), lens);
+                    if (!pair_clean(q0, bb, L, cyc != 0, r, e3)) return fail("pair contract", L, bb, cyc, base.data(), base.data(), base.data(), 0, -1);
+                    from_planes<1>(r, L, g2.data());
+                    const int32_t* w4 = e4 ? base.data() : o2.data();
+                    if (e4 != e3 || memcmp(w4, g2.data(), 8 * L) != 0)
+                        return fail("pair_move_clean", L, bb, cyc, base.data(), w4, g2.data(), e4, e3);
+                }
             } else if (ew == 0 && cyc == 0) {
                 // a successful move's output is reduced: freely (always) -- never unclean unless
                 // a relator is empty, which the move rejects
@@ -141,6 +175,15 @@ static int run(int L, int cases, std::mt19937_64& rng) {
             if (!pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, true)) break;
             const int a = (int)(rng() % 12);
             const int ew = acx_oracle_move(in.data(), L, a, 1, out.data(), lens);
+            if constexpr (PW == 1) {
+                PlaneRegs<1> r;
+                int e3;
+                std::vector<int32_t> g3(2 * L);
+                if (!pair_clean(p, a, L, true, r, e3)) return fail("pair walk contract", L, a, 1, in.data(), in.data(), in.data(), 0, -1);
+                from_planes<1>(r, L, g3.data());
+                const int32_t* w3 = ew ? in.data() : out.data();
+                if (ew != e3 || memcmp(w3, g3.data(), 8 * L) != 0) return fail("pair walk", L, a, 1, in.data(), w3, g3.data(), ew, e3);
+            }
             const int eg = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, a, L, true);
             from_planes<PW>(p, L, got.data());
             const int32_t* want = ew ? in.data() : out.data();

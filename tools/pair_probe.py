@@ -42,7 +42,7 @@ def patched_source():
     stamp = "__builtin_amdgcn_s_memrealtime()"
     ins("    const int64_t env = r0 + er;\n", f"    uint64_t PT_[{NST}] = {{}};\n    PT_[0] = {stamp};\n", before=False)
     ins("        if (__any(badm != 0u)) {", f"        PT_[1] = {stamp};\n")
-    ins("    // the env's move, computed by both of its lanes", f"    PT_[2] = {stamp};\n")
+    ins("    // the env's move: on a clean env", f"    PT_[2] = {stamp};\n")
     ins("    // this lane's relator re-imaged (a failed env keeps its loaded image)", f"    PT_[3] = {stamp};\n")
     ins("    // the state store.  Relator masks", f"    PT_[4] = {stamp};\n")
     end = (f"{{ PT_[5] = {stamp}; __builtin_amdgcn_s_waitcnt(0); PT_[6] = {stamp}; "
@@ -51,9 +51,9 @@ def patched_source():
     st = body.index("    // the state store.  Relator masks")
     tail = body[st:].replace("return;", "{ " + end + " return; }")
     body = body[:st] + tail[:-2] + "    " + end + "\n}\n"
-    ins("        if (h == 0 && a.final_obs) {", "        if (false) {  // final_obs carries the probe buffer\n")
-    body = body.replace("        if (false) {  // final_obs carries the probe buffer\n        if (h == 0 && a.final_obs) {",
-                        "        if (false) {  // final_obs carries the probe buffer")
+    anchor = "        if (a.final_obs) {  // final_obs <- the post-move state (rare)"
+    assert body.count(anchor) == 1
+    body = body.replace(anchor, "        if (false) {  // final_obs carries the probe buffer")
     return s[:k0] + body + s[k1:]
 
 
