@@ -395,7 +395,7 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
 
     snap = [t.clone() for t in tensors]
     B = state.shape[0]
-    chg = rd = wr = fin = srd = swr = 0.0
+    chg = rd = wr = fin = srd = swr = lrd = 0.0
     if lens is not None:
         # byte offset of each relator in the (B, 2L) int32 state: the 64-B sectors its chunks touch
         rel0 = ((torch.arange(B, device=state.device, dtype=torch.int64) * 2 * L)[:, None]
@@ -420,13 +420,17 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
             wr += float((c_wr * ch).sum().item()) * 16
             srd += float(sectors(c_old).sum().item()) * 64
             swr += float(sectors(torch.maximum(c_old, c_new) * ch).sum().item()) * 64
+            # HBM reads whole 128-B lines (tools/line_probe.py: a read of 16, 32 or 64 B of a line
+            # takes the whole line's time and one 128-B request); relators start on a line at
+            # L % 32 == 0
+            lrd += float(((c_old + 7) // 8).sum().item()) * 128
         if finished is not None:
             fin += float((finished[0] | finished[1]).sum().item())
         del before, n_before
     restore(snap, tensors)
     d = max(1, n) * B
     return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d,
-            "sector_read": srd / d, "sector_written": swr / d}
+            "sector_read": srd / d, "sector_written": swr / d, "line_read": lrd / d}
 
 
 def learner_buffers(lenv) -> list:
@@ -816,7 +820,8 @@ def run_rank(args):
             # inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.  The
             # live bytes follow the walk's lengths, which grow through a horizon and drop at the
             # synchronised resets, so a sample of other steps would not do.
-            rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, err_count), K, L, lens=lens2)
+            rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, err_count), K, L, lens=lens2,
+                             finished=(dn1, tr1))
             rd, wr = rp["live_read"], rp["live_written"]
             sb_len = rd + wr + 16 + 27
             wall_len, s_len, wall_len_local = timed(go_steps2)
@@ -831,13 +836,18 @@ def run_rank(args):
                              "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
                              "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
                              "sector_bytes_per_env_step": rp["sector_read"] + rp["sector_written"] + 16 + 27,
+                             # the same walk at the memory's read granularity: live chunks read in whole
+                             # 128-B lines, plus the starting row each reset env loads whole
+                             "line_bytes_per_env_step": rp["line_read"] + wr + 16 + 27 + rp["finished"] * 8 * L,
+                             "resets_per_env_step": rp["finished"],
                              "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
                                            "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
-                                           "summed over exactly the timed steps; HBM moves whole 64-B sectors, so a "
-                                           "relator's last live chunk brings its sector's dead ones (sector_bytes: the "
-                                           "same walk rounded to the 64-B sectors touched; PMC of config 5's command "
-                                           "1.134x the live bytes, writes within 3 %, profiles/r05/"
-                                           "r05_step128_step_variants.json)"},
+                                           "summed over exactly the timed steps (a changed relator's written chunks "
+                                           "rounded up to whole 64-B sectors at L = 128, as the kernel writes them); "
+                                           "HBM reads whole 128-B lines, so a relator's last live chunk brings its "
+                                           "line's dead ones (line_bytes: the same walk at that granularity, plus "
+                                           "the starting rows of resets; tools/line_probe.py calibrates it, "
+                                           "profiles/r06/r06i_line_probe.json; sector_bytes: 64-B sectors)"},
                 "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
             }
             if not same:  # a lengths-path regression must not publish a headline
