@@ -258,6 +258,12 @@ class VecACEnv:
         # them (rollout, direct writes by a learner), and the next step uses acx_step, which rewrites them
         self.lengths = _row_extent(self.state, L).contiguous()
         self._lengths_ok = True
+        # per row: the previous lengths-carrying step left both relators reduced (bit 0 freely, bit 1
+        # cyclically; 0 unknown) -- acx_step_lengths_reduced then leaves a conjugation's other
+        # relator unread.  _reduced_ok is False after a step by any other kernel (which does not
+        # write the flags); the next lengths-carrying step zeroes them first
+        self.reduced = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self._reduced_ok = True
         # the lengths-carrying step where it measured faster (ops.LENGTHS_STEP_L, L = 128)
         self._live_tile = L in ops.LENGTHS_STEP_L
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
@@ -299,6 +305,8 @@ class VecACEnv:
         # (reset_state may also have been rewritten on the device, e.g. by the learner's curriculum)
         self.lengths.copy_(_row_extent(self.state, self.max_relator_length))
         self._lengths_ok = True
+        self.reduced.zero_()
+        self._reduced_ok = True
         self.step_count.zero_()
         if self.autoreset_mode == "next_step":
             self.pending.zero_()
@@ -315,6 +323,7 @@ class VecACEnv:
         self.reset_state[i].copy_(t)
         self.state[i].copy_(t)
         self.lengths[i].copy_(_row_extent(t, self.max_relator_length)[0])
+        self.reduced[i] = 0
         self.step_count[i] = 0
         if self.autoreset_mode == "next_step":
             self.pending[i] = 0
@@ -337,6 +346,8 @@ class VecACEnv:
             actions = actions.to(self.device, torch.int32).contiguous().reshape(self.num_envs)
         s_in, s_out, rs, cnt, rew, dn, tr, ln, fo, err, ec = self._step_args()
         stream = ops._stream(self.device)
+        live = (self.autoreset_mode != "next_step" and self._lengths_ok and self._live_tile
+                and not self.record_actions)
         if self.autoreset_mode == "next_step":
             rec = self.record_actions
             st = self._lib.acx_step_next(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln,
@@ -346,12 +357,17 @@ class VecACEnv:
                                          self.episode_len.data_ptr() if rec else None, err, ec, self.num_envs,
                                          self.max_relator_length, self.horizon_length, int(self.cyclical), stream)
             _lib.check(st, "acx_step_next")
-        elif self._lengths_ok and self._live_tile and not self.record_actions:
-            # the rows' lengths are current: only their letters are read and written
-            st = self._lib.acx_step_lengths(s_in, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo, err, ec,
-                                            self.num_envs, self.max_relator_length, self.horizon_length,
-                                            int(self.cyclical), stream)
-            _lib.check(st, "acx_step_lengths")
+        elif live:
+            # the rows' lengths are current: only their letters are read and written (and of a
+            # reduced row only the relator a conjugation changes)
+            if not self._reduced_ok:
+                self.reduced.zero_()
+                self._reduced_ok = True
+            st = self._lib.acx_step_lengths_reduced(s_in, actions.data_ptr(), rs, cnt, rew, dn, tr, ln,
+                                                    self.reduced.data_ptr(), fo, err, ec, self.num_envs,
+                                                    self.max_relator_length, self.horizon_length,
+                                                    int(self.cyclical), stream)
+            _lib.check(st, "acx_step_lengths_reduced")
         elif self.record_actions:
             st = self._lib.acx_step_record(s_in, s_out, actions.data_ptr(), rs, cnt, rew, dn, tr, ln, fo,
                                            self.action_hist.data_ptr(), self.action_hist.shape[0],
@@ -365,6 +381,7 @@ class VecACEnv:
                                     stream)
             _lib.check(st, "acx_step")
         self._lengths_ok = True  # every step kernel writes the rows' lengths
+        self._reduced_ok = live  # ... only the lengths-carrying one the reduced flags
         if self.record_actions:
             self.hist_t += 1
         if self.check_errors:
@@ -422,6 +439,7 @@ class VecACEnv:
                     cyclical=self.cyclical, obs_traj=obs_traj, reward_traj=reward_traj, done_traj=done_traj,
                     trunc_traj=trunc_traj, err=self.err, err_count=self.err_count)
         self._lengths_ok = False  # the rollout does not write lengths
+        self._reduced_ok = False
         if self.check_errors:
             self.raise_if_errors()
 

@@ -100,11 +100,15 @@ def step(
     err: Optional[torch.Tensor] = None,
     err_count: Optional[torch.Tensor] = None,
     lengths_in: bool = False,
+    reduced: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """acx_step: batched ACEnv.step / ACMove.  Returns state_out (in place if given as state_in).
     lengths_in: `lengths` already holds the rows' relator lengths (the previous call's output,
     or (L, L) for "unknown") and the step is in place -> acx_step_lengths, which reads and writes
-    only the chunks inside the letters (ACMove's lengths in / lengths out, ac_moves.py:159,231)."""
+    only the chunks inside the letters (ACMove's lengths in / lengths out, ac_moves.py:159,231).
+    reduced (with lengths_in): (B,) uint8 per-row reduced flags, in/out (zeros for "unknown"; the
+    previous call's output) -> acx_step_lengths_reduced, which also leaves the relator a
+    conjugation does not touch unread when the row is known reduced (include/acx.h)."""
     lib = _lib.load()
     _need_gpu(state_in, "state_in")
     L = _L_of(state_in)
@@ -124,9 +128,20 @@ def step(
     _check(final_obs, "final_obs", _INT32, (B, 2 * L), dev)
     _check(err, "err", _UINT8, (B,), dev)
     _check(err_count, "err_count", _INT32, (1,), dev)
+    _check(reduced, "reduced", _UINT8, (B,), dev)
+    if reduced is not None and not lengths_in:
+        raise ValueError("reduced needs lengths_in (the lengths-carrying step)")
     if lengths_in:
         if lengths is None or state_out.data_ptr() != state_in.data_ptr():
             raise ValueError("lengths_in needs lengths and an in-place step (state_out is state_in)")
+        if reduced is not None:
+            st = lib.acx_step_lengths_reduced(
+                _ptr(state_in), _ptr(action), _ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done),
+                _ptr(truncated), _ptr(lengths), _ptr(reduced), _ptr(final_obs), _ptr(err), _ptr(err_count),
+                B, L, int(horizon), int(bool(cyclical)), _stream(dev),
+            )
+            _lib.check(st, "acx_step_lengths_reduced")
+            return state_out
         st = lib.acx_step_lengths(
             _ptr(state_in), _ptr(action), _ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done),
             _ptr(truncated), _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count),
@@ -324,7 +339,7 @@ class StepPlan:
     every call (a small batch stepped many times: BASELINE configs[1]) pays one ctypes call per
     step instead of ops.step's per-call checks -- at 65,536 envs the kernel is ~10 us, and the
     host, not the GPU, set the eager rate.  Same kernels and results as ops.step with the same
-    arguments (lengths_in=True: acx_step_lengths).  The plan keeps references to its tensors;
+    arguments (lengths_in=True: acx_step_lengths; with reduced: acx_step_lengths_reduced).  The plan keeps references to its tensors;
     their storage must not be resized or replaced."""
 
     def __init__(
@@ -344,6 +359,7 @@ class StepPlan:
         err: Optional[torch.Tensor] = None,
         err_count: Optional[torch.Tensor] = None,
         lengths_in: bool = False,
+        reduced: Optional[torch.Tensor] = None,
     ):
         lib = _lib.load()
         _need_gpu(state_in, "state_in")
@@ -359,21 +375,28 @@ class StepPlan:
                 (reward, "reward", _INT32, per_env), (done, "done", _UINT8, per_env),
                 (truncated, "truncated", _UINT8, per_env), (lengths, "lengths", _INT32, (B, 2)),
                 (final_obs, "final_obs", _INT32, rows), (err, "err", _UINT8, per_env),
-                (err_count, "err_count", _INT32, (1,))):
+                (err_count, "err_count", _INT32, (1,)), (reduced, "reduced", _UINT8, per_env)):
             _check(t, name, dt, shape, dev)
+        if reduced is not None and not lengths_in:
+            raise ValueError("reduced needs lengths_in (the lengths-carrying step)")
         self.B, self.L, self.device, self.state_out = B, L, dev, state_out
         self._didx = dev.index if dev.index is not None else torch.cuda.current_device()
         self._ashape = torch.Size((B,))
         self._keep = (state_in, state_out, reset_state, step_count, reward, done, truncated, lengths, final_obs, err,
-                      err_count)
+                      err_count, reduced)
         tail = (B, L, int(horizon), int(bool(cyclical)))
         if lengths_in:
             if lengths is None or state_out.data_ptr() != state_in.data_ptr():
                 raise ValueError("lengths_in needs lengths and an in-place step (state_out is state_in)")
-            self._fn, self._name = lib.acx_step_lengths, "acx_step_lengths"
             self._head = (_ptr(state_in),)
-            self._tail = (_ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done), _ptr(truncated),
-                          _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count)) + tail
+            if reduced is not None:
+                self._fn, self._name = lib.acx_step_lengths_reduced, "acx_step_lengths_reduced"
+                self._tail = (_ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done), _ptr(truncated),
+                              _ptr(lengths), _ptr(reduced), _ptr(final_obs), _ptr(err), _ptr(err_count)) + tail
+            else:
+                self._fn, self._name = lib.acx_step_lengths, "acx_step_lengths"
+                self._tail = (_ptr(reset_state), _ptr(step_count), _ptr(reward), _ptr(done), _ptr(truncated),
+                              _ptr(lengths), _ptr(final_obs), _ptr(err), _ptr(err_count)) + tail
         else:
             self._fn, self._name = lib.acx_step, "acx_step"
             self._head = (_ptr(state_in), _ptr(state_out))

@@ -451,6 +451,7 @@ struct FastTile {
     // wave-uniform mask `rows` (at most RPI of them: one wave-instruction) and returns each lane's
     // chunk; put_rows later writes the rows in `apply` (a subset) into the tile, as load_rows does
     static constexpr bool PREFETCH_OK = true;
+    static constexpr bool LIVE_ROWS = true;  // set_lim selects the chunks a live load reads
     static constexpr int RPI = WAVE / CPR;  // rows per wave-instruction
     __device__ __forceinline__ int4 fetch_rows(const int32_t* __restrict__ g, uint64_t rows, int lane) const {
         const int s = lane / CPR, c = lane - s * CPR;
@@ -909,6 +910,7 @@ struct CodeTile {
 
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
+    static constexpr bool LIVE_ROWS = true;  // see FastTile
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
     __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
@@ -1592,6 +1594,7 @@ struct CodeTile {
 template <int NW, int LC, int VEC>
 struct GenericTile {
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
+    static constexpr bool LIVE_ROWS = false;  // whole rows: set_lim is a no-op
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
     __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
@@ -1977,6 +1980,10 @@ struct StepArgs {
     // tests only (acx_internal_learner_ranking_fails): ranking waits give up at once, as one that
     // polled 2^20 times would (1: every wait, needs_host = 3; 2: only the last tile's total)
     int cur_fail;
+    // acx_step_lengths_reduced (live steps only; NULL: none): per env, bit 0 = both relators are
+    // non-empty and freely reduced, bit 1 = and cyclically reduced, as the previous step left them.
+    // A conjugation of such a row reads only its target relator (step_body).  Written every call.
+    uint8_t* reduced;
 };
 
 // ---------------------------------------------------------------------------------
@@ -2217,13 +2224,31 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     }
     int hb = 0;  // the move-history ring's row of this env's episode move 0
     if (LEARN && w.active && a.hist_base) hb = a.hist_base[env];
+    // Relator skip (acx_step_lengths_reduced): a conjugation (ids 4..11, ac_moves.py:79-156)
+    // reads and writes only its target r_i, and simplify_presentation (utils.py:246-283) leaves a
+    // reduced r_j as it is -- so when the previous step left both relators reduced (a.reduced) the
+    // untouched relator is not read at all; its length comes from the carried lengths.  Not
+    // skipped: an r_j of one letter (the triviality test, utils.py:57-87, needs it), a step that
+    // truncates (final_obs holds the whole row) and next-step resets.  The lane then holds r_j as
+    // empty (n = 0, no live chunks), which the move, the dirty image and the write-back leave alone.
+    bool skip = false;
+    int skip_h = 0, n_skip = 0;  // the relator left unread and its length
     if constexpr (LIVE) {
         int n_in0 = 0, n_in1 = 0;  // the rows' relator lengths on entry
         if (w.active) {
             n_in0 = a.lengths_out[2 * env];
             n_in1 = a.lengths_out[2 * env + 1];
         }
-        tile.set_lim(w.lane, n_in0, n_in1);
+        if constexpr (Tile::LIVE_ROWS) {
+            if (a.reduced && w.active) {
+                const uint32_t rf = a.reduced[env];
+                skip_h = act_in & 1;  // ids 4..11: the move's target is r_{(id + 1) & 1}
+                n_skip = skip_h ? n_in1 : n_in0;
+                skip = ((rf >> (a.cyclical ? 1 : 0)) & 1u) != 0u && act_in >= 4 && act_in < 12 && !pend &&
+                       n_skip >= 2 && n_skip <= L && !(a.step_count && cnt_in + 1 >= a.horizon);
+            }
+        }
+        tile.set_lim(w.lane, (skip && skip_h == 0) ? 0 : n_in0, (skip && skip_h == 1) ? 0 : n_in1);
         wave_sync();
         tile.template load<true, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     } else {
@@ -2264,6 +2289,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         const bool cyc = a.cyclical != 0;
         if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
         else if (bad) e = ACX_ERR_DOMAIN;
+        else if (skip) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);  // reduced: see above
         else if (pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         else {
                 const pl::MoveOut<PW> mo = pl::ac_move_call<PW>(p, act, L, cyc);
@@ -2273,10 +2299,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
         if (!keep) dm = tile.template unpack_dirty<LIVE>(w.lane, p);
+        // (a skipped relator is held as n = 0 in p and has >= 2 letters: never trivial)
         triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
         trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
         // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does
-        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1);
+        rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1 + n_skip * (int)skip);
         fin = triv || trunc;
         // same-step autoreset: an env that ends resets now; next-step: a pending env resets now and
         // an env that ends is reset by the next call
@@ -2365,8 +2392,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (a.lengths_out) {
             // lengths-carrying step: an out-of-domain row is read whole on the next call (L, L)
             const bool whole = LIVE && e == ACX_ERR_DOMAIN;
-            st_scalar<false, int32_t>(a.lengths_out + 2 * env, whole ? L : p.n0);
-            st_scalar<false, int32_t>(a.lengths_out + 2 * env + 1, whole ? L : p.n1);
+            st_scalar<false, int32_t>(a.lengths_out + 2 * env, whole ? L : (skip && skip_h == 0) ? n_skip : p.n0);
+            st_scalar<false, int32_t>(a.lengths_out + 2 * env + 1, whole ? L : (skip && skip_h == 1) ? n_skip : p.n1);
+        }
+        // a moved row is reduced: freely, and cyclically too when cyclical (simplify_presentation,
+        // utils.py:246-283) -- but may hold an empty relator (validity is asserted before the
+        // reduction, :264-266: an unreduced y^-1 y empties); a failed, reset or out-of-domain row
+        // is read whole next time
+        if (LIVE && a.reduced) {
+            const bool full = (p.n0 > 0 || (skip && skip_h == 0)) && (p.n1 > 0 || (skip && skip_h == 1));
+            st_scalar<false, uint8_t>(
+                a.reduced + env,
+                (uint8_t)((!keep && !reset && !pend && e == ACX_ERR_NONE && full) ? (a.cyclical ? 3 : 1) : 0));
         }
         if (a.err) st_scalar<false, uint8_t>(a.err + env, (uint8_t)e);
         if (e != ACX_ERR_NONE && a.err_count) atomicAdd(a.err_count, 1);
@@ -3795,6 +3832,23 @@ int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset
     StepArgs a{state, state, action, reset_state, step_count, reward, done, truncated, lengths, final_obs, err,
                err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, B, L, horizon, cyclical, 0};
     a.live = 1;
+    StepLaunch f{a, (hipStream_t)stream, false};
+    return dispatch(L, f);
+}
+
+int acx_step_lengths_reduced(int32_t* state, const int32_t* action, const int32_t* reset_state, int32_t* step_count,
+                             int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths, uint8_t* reduced,
+                             int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L,
+                             int32_t horizon, int32_t cyclical, void* stream) {
+    if (B < 0 || L < 1 || L > ACX_MAX_L) return ACX_E_ARG;
+    if (B == 0) return ACX_OK;
+    if (!state || !action || !lengths || !reduced) return ACX_E_ARG;
+    if (!aligned16(state)) return ACX_E_ARG;
+    if (reset_state && !step_count) return ACX_E_ARG;
+    StepArgs a{state, state, action, reset_state, step_count, reward, done, truncated, lengths, final_obs, err,
+               err_count, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, B, L, horizon, cyclical, 0};
+    a.live = 1;
+    a.reduced = reduced;
     StepLaunch f{a, (hipStream_t)stream, false};
     return dispatch(L, f);
 }

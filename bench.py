@@ -384,18 +384,20 @@ def restore(snap, tensors) -> None:
         x.copy_(y)
 
 
-def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=None) -> dict:
+def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=None, unread=None) -> dict:
     """What the n steps step_fn(0..n-1) will do from here, counted off the clock: they are run
     from a snapshot of `tensors` (every buffer the steps read and write; the kernels are
     deterministic, so the timed pass that follows takes this same walk) and the snapshot is put
     back.  Per env-step: "changed" relators (the in-place write-back's unit), with `lens` (the
     lengths-carrying step's (B, 2) lengths) the "live_read" / "live_written" bytes of 16-byte
-    chunks, with `finished` ((done, truncated) uint8 tensors) the "finished" envs."""
+    chunks, with `finished` ((done, truncated) uint8 tensors) the "finished" envs; `unread(t)`
+    ((B, 2) bool, evaluated before step t) marks the relators that step leaves unread
+    (acx_step_lengths_reduced's skipped relator)."""
     import torch
 
     snap = [t.clone() for t in tensors]
     B = state.shape[0]
-    chg = rd = wr = fin = srd = swr = lrd = 0.0
+    chg = rd = wr = fin = srd = swr = lrd = skp = 0.0
     if lens is not None:
         # byte offset of each relator in the (B, 2L) int32 state: the 64-B sectors its chunks touch
         rel0 = ((torch.arange(B, device=state.device, dtype=torch.int64) * 2 * L)[:, None]
@@ -407,6 +409,9 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
     for t in range(n):
         before = state.clone()
         n_before = lens.clone() if lens is not None else None
+        keep = (~unread(t)).to(torch.int64) if unread is not None else 1
+        if unread is not None:
+            skp += float((1 - keep).sum().item())
         step_fn(t)
         ch = (before.view(B, 2, L) != state.view(B, 2, L)).any(2)
         chg += float(ch.sum().item())
@@ -416,21 +421,21 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
             c_wr = torch.maximum(c_old, c_new)
             if L % 32 == 0:  # relators start on a 64-B sector: the kernel writes whole sectors (CodeTile::widen_lim)
                 c_wr = torch.clamp((c_wr + 3) // 4 * 4, max=L // 4)
-            rd += float(c_old.sum().item()) * 16
+            rd += float((c_old * keep).sum().item()) * 16
             wr += float((c_wr * ch).sum().item()) * 16
-            srd += float(sectors(c_old).sum().item()) * 64
+            srd += float((sectors(c_old) * keep).sum().item()) * 64
             swr += float(sectors(torch.maximum(c_old, c_new) * ch).sum().item()) * 64
             # HBM reads whole 128-B lines (tools/line_probe.py: a read of 16, 32 or 64 B of a line
             # takes the whole line's time and one 128-B request); relators start on a line at
             # L % 32 == 0
-            lrd += float(((c_old + 7) // 8).sum().item()) * 128
+            lrd += float((((c_old + 7) // 8) * keep).sum().item()) * 128
         if finished is not None:
             fin += float((finished[0] | finished[1]).sum().item())
         del before, n_before
     restore(snap, tensors)
     d = max(1, n) * B
     return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d,
-            "sector_read": srd / d, "sector_written": swr / d, "line_read": lrd / d}
+            "sector_read": srd / d, "sector_written": swr / d, "line_read": lrd / d, "unread": skp / d}
 
 
 def learner_buffers(lenv) -> list:
@@ -801,11 +806,23 @@ def run_rank(args):
             st2 = starts.clone()
             cnt2 = torch.zeros(B, dtype=torch.int32, device=dev)
             lens2 = torch.full((B, 2), L, dtype=torch.int32, device=dev)  # (L, L): read whole, once
+            # the rows' reduced flags (acx_step_lengths_reduced, VecACEnv.step's kernel): a
+            # conjugation of a row the previous step left reduced reads only its target relator
+            red2 = torch.zeros(B, dtype=torch.uint8, device=dev)
 
             def step2(a):
                 ops.step(st2, a, state_out=st2, reset_state=starts, step_count=cnt2, horizon=H, cyclical=True,
                          reward=rew1, done=dn1, truncated=tr1, lengths=lens2, err=err, err_count=err_count,
-                         lengths_in=True)
+                         lengths_in=True, reduced=red2)
+
+            def unread(t):
+                # the kernel's skip rule (step_body): flag for this mode, a conjugation (ids 4..11),
+                # the untouched relator r_{id & 1} of >= 2 letters, no truncation on this step
+                a = actions[W + t]
+                h = (a & 1).to(torch.int64)
+                n_sk = lens2.gather(1, h[:, None])[:, 0]
+                ok = (((red2 >> 1) & 1) != 0) & (a >= 4) & (a < 12) & (n_sk >= 2) & (n_sk <= L) & (cnt2 + 1 < H)
+                return torch.nn.functional.one_hot(h, 2).bool() & ok[:, None]
 
             err_count.zero_()
             for t in range(W):
@@ -820,10 +837,11 @@ def run_rank(args):
             # inside its old or new letters written; + lengths in/out 16 + 27 B of scalars.  The
             # live bytes follow the walk's lengths, which grow through a horizon and drop at the
             # synchronised resets, so a sample of other steps would not do.
-            rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, err_count), K, L, lens=lens2,
+            rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, red2, err_count), K, L,
+                             lens=lens2, unread=unread,
                              finished=(dn1, tr1))
             rd, wr = rp["live_read"], rp["live_written"]
-            sb_len = rd + wr + 16 + 27
+            sb_len = rd + wr + 16 + 27 + 2  # + the reduced flag in and out
             wall_len, s_len, wall_len_local = timed(go_steps2)
             n_err_len = int(err_count.item())
             same = bool(torch.equal(st1, st2))  # both walks took the same W + K steps
@@ -835,20 +853,23 @@ def run_rank(args):
                 "roofline": {"bound": "hbm", "achieved": a_len, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": a_len / HBM_PEAK_GBS, "kernel": len_kernel, "bytes_per_env_step": sb_len,
                              "live_bytes_read_per_env_step": rd, "live_bytes_written_per_env_step": wr,
-                             "sector_bytes_per_env_step": rp["sector_read"] + rp["sector_written"] + 16 + 27,
+                             "sector_bytes_per_env_step": rp["sector_read"] + rp["sector_written"] + 16 + 29,
                              # the same walk at the memory's read granularity: live chunks read in whole
                              # 128-B lines, plus the starting row each reset env loads whole
-                             "line_bytes_per_env_step": rp["line_read"] + wr + 16 + 27 + rp["finished"] * 8 * L,
+                             "line_bytes_per_env_step": rp["line_read"] + wr + 16 + 29 + rp["finished"] * 8 * L,
                              "resets_per_env_step": rp["finished"],
-                             "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator, changed relators' "
-                                           "chunks inside old or new letters written, lengths 16 B + 27 B of scalars, "
+                             "unread_relators_per_env_step": rp["unread"],
+                             "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator the step reads (a "
+                                           "conjugation of a row known reduced leaves the other relator unread), "
+                                           "changed relators' chunks inside old or new letters written, lengths 16 B "
+                                           "+ 27 B of scalars + the reduced flag in and out 2 B, "
                                            "summed over exactly the timed steps (a changed relator's written chunks "
                                            "rounded up to whole 64-B sectors at L = 128, as the kernel writes them); "
                                            "HBM reads whole 128-B lines, so a relator's last live chunk brings its "
                                            "line's dead ones (line_bytes: the same walk at that granularity, plus "
                                            "the starting rows of resets; tools/line_probe.py calibrates it, "
                                            "profiles/r06/r06i_line_probe.json; sector_bytes: 64-B sectors)"},
-                "workload": "per-call acx_step_lengths (VecACEnv.step's path), same walk as step_api",
+                "workload": "per-call acx_step_lengths_reduced (VecACEnv.step's path), same walk as step_api",
             }
             if not same:  # a lengths-path regression must not publish a headline
                 variants["step_api_lengths"]["error"] = "states differ from acx_step's on the same walk"
@@ -869,8 +890,8 @@ def run_rank(args):
                 "elapsed": wall_len, "kernel_s": s_len, "wall_local": wall_len_local, "frac": a_len / HBM_PEAK_GBS,
                 "roofline": dict(variants["step_api_lengths"]["roofline"], kernel_ms=s_len * 1e3, launches=K,
                                  launch_bytes=B * sb_len),
-                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step_lengths (the env's "
-                             f"step, ACMove's lengths in/out), {B} envs/GPU, L={L}, horizon {H}, cyclical=True, "
+                "workload": (f"random-action stepping (BASELINE configs[4]): per-call acx_step_lengths_reduced (the "
+                             f"env's step, ACMove's lengths in/out, per-row reduced flags), {B} envs/GPU, L={L}, horizon {H}, cyclical=True, "
                              f"in-place state, same-step autoreset; {K} launches"),
                 "env_errors": n_err_len,
             }

@@ -115,6 +115,24 @@ int acx_step_lengths(int32_t* state, const int32_t* action, const int32_t* reset
                      void* stream);
 
 /*
+ * acx_step_lengths plus a per-env reduced flag, reduced (B) uint8 in/out (required): bit 0 = both
+ * relators non-empty and freely reduced, bit 1 = and cyclically reduced, as the previous call left
+ * the row; 0 = unknown.  Every call writes it (a moved row: 3 when cyclical, else 1; a failed,
+ * reset or out-of-domain row: 0).  A conjugation (move ids 4..11, ac_moves.py:79-156) changes only
+ * its target relator, and simplify_presentation (utils.py:246-283) leaves a reduced relator as it
+ * is, so for a row whose flag holds for this call's mode the relator the move leaves alone is not
+ * read at all (its length is taken from `lengths`) -- except a one-letter relator (the triviality
+ * test reads it) and on a step that truncates (final_obs holds the whole row).  Results are
+ * acx_step's.  A caller that changes rows by other means zeroes their flags (as it resets their
+ * lengths to the rows' extents).  Replaces the same reference calls as acx_step_lengths
+ * (ACEnv.step -> ACMove, ac_env.py:91-111).
+ */
+int acx_step_lengths_reduced(int32_t* state, const int32_t* action, const int32_t* reset_state, int32_t* step_count,
+                             int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths, uint8_t* reduced,
+                             int32_t* final_obs, uint8_t* err, int32_t* err_count, int64_t B, int32_t L,
+                             int32_t horizon, int32_t cyclical, void* stream);
+
+/*
  * acx_step for the PPO learner (ac_solver/agents/training.py:221-356), state updated in place
  * with same-step autoreset to reset_state, plus the learner-side writes fused in:
  *   action / action_i64 : exactly one non-NULL; action_i64 = the policy's int64 samples

@@ -39,9 +39,30 @@ def _t(x):
     return torch.as_tensor(np.ascontiguousarray(x)).to(DEV)
 
 
+def _check_reduced_flags(flags, rows, L, where):
+    """acx_step_lengths_reduced's flags claim only what holds: bit 0 -> both relators non-empty and
+    freely reduced, bit 1 -> and cyclically reduced (include/acx.h)"""
+    f = flags.cpu().numpy()
+    s = rows.cpu().numpy() if torch.is_tensor(rows) else rows
+    assert ((f & ~np.uint8(3)) == 0).all(), where
+    assert not ((f & 2) & ~((f & 1) << 1)).any(), where  # cyclically reduced implies freely
+    for b in np.flatnonzero(f):
+        for h in range(2):
+            w = s[b, h * L:(h + 1) * L]
+            n = int(np.count_nonzero(w))
+            assert n > 0 and not w[n:].any() and (w[:n] != 0).all(), (where, b, h)
+            assert not (w[1:n] == -w[: n - 1]).any(), (where, b, h)
+            if f[b] & 2 and n > 1:
+                assert w[0] != -w[n - 1], (where, b, h)
+    return int((f != 0).sum())
+
+
 @pytest.mark.parametrize("L", [36, 128, 18, 64])
 @pytest.mark.parametrize("cyc", [0, 1])
-def test_step_lengths_matches_acx_step(L, cyc):
+@pytest.mark.parametrize("reduced", [False, True])
+def test_step_lengths_matches_acx_step(L, cyc, reduced):
+    """reduced: acx_step_lengths_reduced, the reduced flags carried from call to call (a
+    conjugation of a reduced row leaves its other relator unread)"""
     from acx import _lib
     lib = _lib.load()
     rng = np.random.default_rng(L * 7 + cyc)
@@ -62,8 +83,9 @@ def test_step_lengths_matches_acx_step(L, cyc):
     lens_a = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
     lens_b = _t(np.stack([np.count_nonzero(start[:, :L], 1), np.count_nonzero(start[:, L:], 1)], 1).astype(np.int32))
     lens_b[::13] = L  # (L, L): "read the whole row", always safe
+    red = torch.zeros(B, dtype=torch.uint8, device=DEV)
     stream = torch.cuda.current_stream(DEV).cuda_stream
-    n_reset = n_err = 0
+    n_reset = n_err = n_flagged = 0
     for t in range(T):
         a = rng.integers(0, 12, size=B).astype(np.int32)
         if t % 7 == 3:
@@ -74,6 +96,10 @@ def test_step_lengths_matches_acx_step(L, cyc):
             if k == "a":
                 rc = lib.acx_step(P(st), P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
                                   lens_a.data_ptr(), P(fo), P(err), P(ec), B, L, H, cyc, stream)
+            elif reduced:
+                rc = lib.acx_step_lengths_reduced(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn),
+                                                  P(tr), lens_b.data_ptr(), red.data_ptr(), P(fo), P(err), P(ec),
+                                                  B, L, H, cyc, stream)
             else:
                 rc = lib.acx_step_lengths(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
                                           lens_b.data_ptr(), P(fo), P(err), P(ec), B, L, H, cyc, stream)
@@ -81,6 +107,8 @@ def test_step_lengths_matches_acx_step(L, cyc):
         for name, d in (("state", st), ("reward", rew), ("done", dn), ("trunc", tr), ("count", cnt),
                         ("final_obs", fo), ("err", err), ("err_count", ec)):
             assert torch.equal(d["a"], d["b"]), (t, name)
+        if reduced:
+            n_flagged += _check_reduced_flags(red, st["b"], L, t)
         e = err["a"].cpu().numpy()
         dom = e == 3
         la, lb = lens_a.cpu().numpy(), lens_b.cpu().numpy()
@@ -94,10 +122,13 @@ def test_step_lengths_matches_acx_step(L, cyc):
         n_reset += int((dn["a"] | tr["a"]).sum())
         n_err += int((e != 0).sum())
     assert n_reset > B and n_err > n_ood  # resets, out-of-domain resets and failed moves exercised
+    if reduced:
+        assert n_flagged > T * B // 2  # most rows stepped as known-reduced
 
 
 @pytest.mark.parametrize("L", [36, 128, 17])
-def test_step_lengths_error_stream_matches_acx_step(L):
+@pytest.mark.parametrize("reduced", [False, True])
+def test_step_lengths_error_stream_matches_acx_step(L, reduced):
     """The error-contract stream of test_gpu_rollout_errors (moves that empty a relator from
     r0 == r1 rows, an unreduced relator whose conjugation raises, out-of-domain INPUT rows -- a
     letter 3, a zero inside r1, a letter 300 -- and out-of-domain starting rows, bad move ids,
@@ -119,6 +150,7 @@ def test_step_lengths_error_stream_matches_acx_step(L):
     ec = {k: torch.zeros(1, dtype=torch.int32, device=DEV) for k in "ab"}
     lens_a = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
     lens_b = _row_extent(st["b"], L).contiguous()
+    red = torch.zeros(B, dtype=torch.uint8, device=DEV)
     stream = torch.cuda.current_stream(DEV).cuda_stream
     seen = set()
     for t in range(T):
@@ -128,6 +160,10 @@ def test_step_lengths_error_stream_matches_acx_step(L):
             if k == "a":
                 rc = lib.acx_step(P(st), P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
                                   lens_a.data_ptr(), None, P(err), P(ec), B, L, H, 1, stream)
+            elif reduced:
+                rc = lib.acx_step_lengths_reduced(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn),
+                                                  P(tr), lens_b.data_ptr(), red.data_ptr(), None, P(err), P(ec),
+                                                  B, L, H, 1, stream)
             else:
                 rc = lib.acx_step_lengths(P(st), at.data_ptr(), rs.data_ptr(), P(cnt), P(rew), P(dn), P(tr),
                                           lens_b.data_ptr(), None, P(err), P(ec), B, L, H, 1, stream)
@@ -135,6 +171,8 @@ def test_step_lengths_error_stream_matches_acx_step(L):
         for name, d in (("state", st), ("reward", rew), ("done", dn), ("trunc", tr), ("count", cnt),
                         ("err", err), ("err_count", ec)):
             assert torch.equal(d["a"], d["b"]), (t, name)
+        if reduced:
+            _check_reduced_flags(red, st["b"], L, t)
         e = err["a"].cpu().numpy()
         dom = e == 3
         la, lb = lens_a.cpu().numpy(), lens_b.cpu().numpy()
@@ -154,6 +192,10 @@ def test_step_lengths_rejects_missing_lengths():
     rc = lib.acx_step_lengths(s.data_ptr(), a.data_ptr(), None, None, None, None, None, None, None, None, None,
                               B, L, 5, 1, stream)
     assert rc == _lib.E_ARG
+    ln = torch.full((B, 2), L, dtype=torch.int32, device=DEV)
+    rc = lib.acx_step_lengths_reduced(s.data_ptr(), a.data_ptr(), None, None, None, None, None, ln.data_ptr(), None,
+                                      None, None, None, B, L, 5, 1, stream)
+    assert rc == _lib.E_ARG  # the reduced flags are required
 
 
 @pytest.mark.parametrize("L", [128, 36])
@@ -196,11 +238,15 @@ def test_vec_env_lengths_after_rollout_and_direct_writes(L):
 # item 3): the reference's carried lengths are ac_env.py:81-95 (self.lengths from reset, passed to
 # and returned by ACMove) and ac_moves.py:159-231.
 # ---------------------------------------------------------------------------------------------
-def _lengths_step(lib, st, at, rs, cnt, rew, dn, tr, lens, fo, err, ec, B, L, H, cyc):
+def _lengths_step(lib, st, at, rs, cnt, rew, dn, tr, lens, fo, err, ec, B, L, H, cyc, red=None):
     stream = torch.cuda.current_stream(DEV).cuda_stream
     P = lambda x: None if x is None else x.data_ptr()  # noqa: E731
-    rc = lib.acx_step_lengths(P(st), P(at), P(rs), P(cnt), P(rew), P(dn), P(tr), P(lens), P(fo), P(err), P(ec),
-                              B, L, H, cyc, stream)
+    if red is not None:
+        rc = lib.acx_step_lengths_reduced(P(st), P(at), P(rs), P(cnt), P(rew), P(dn), P(tr), P(lens), P(red), P(fo),
+                                          P(err), P(ec), B, L, H, cyc, stream)
+    else:
+        rc = lib.acx_step_lengths(P(st), P(at), P(rs), P(cnt), P(rew), P(dn), P(tr), P(lens), P(fo), P(err), P(ec),
+                                  B, L, H, cyc, stream)
     assert rc == 0, rc
 
 
@@ -273,7 +319,8 @@ def test_step_lengths_reference_episodes():
 
 
 @pytest.mark.parametrize("cyc", [1, 0])
-def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc):
+@pytest.mark.parametrize("reduced", [False, True])
+def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc, reduced):
     """A random walk at L = 128 (config 5's kernel) with autoreset -- short horizon, desynchronised
     and synchronised resets, a few bad move ids -- every env, every step against the oracle's
     ACMove (oracle/acx_oracle.c, pinned to the reference's fixtures) under acx's error contract
@@ -296,13 +343,14 @@ def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc):
     tr = torch.zeros(B, dtype=torch.uint8, device=DEV)
     fo = torch.zeros((B, 2 * L), dtype=torch.int32, device=DEV)
     err = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    red = torch.zeros(B, dtype=torch.uint8, device=DEV) if reduced else None
     o_st, o_cnt = starts.copy(), count0.copy()
     n_reset = n_err = 0
     for t in range(T):
         a = rng.integers(0, 12, size=B).astype(np.int32)
         if t % 11 == 5:
             a[::97] = -1  # ACX_ERR_ACTION: state and count kept
-        _lengths_step(lib, st, _t(a), rs, cnt, rew, dn, tr, lens, fo, err, None, B, L, H, cyc)
+        _lengths_step(lib, st, _t(a), rs, cnt, rew, dn, tr, lens, fo, err, None, B, L, H, cyc, red)
         # the pre-reset states (final_observation), then the step under acx's error contract (a
         # failed move keeps state and count: conftest.env_step_contract, checked against the oracle)
         moved, _, merr = O.move_batch(o_st, a, L, cyc)
@@ -323,4 +371,6 @@ def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc):
         assert np.array_equal(got[:, 1], np.count_nonzero(o_st[:, L:], 1)), t
         n_reset += int(m.sum())
         n_err += int((~ok).sum())
+        if reduced:
+            _check_reduced_flags(red, o_st, L, t)
     assert n_reset > B and n_err > 0

@@ -13,6 +13,8 @@ An entry LIB@lengths steps through acx_step_lengths (the rows' lengths carried f
 set from the rows before the warmup), LIB@LL through acx_step_lengths with every row's lengths
 reset to (L, L) -- "read the whole row" -- before each call (the refill is a separate timed
 launch, reported apart): the cost of the lengths dependency without the byte saving.
+LIB@reduced steps through acx_step_lengths_reduced (lengths and per-row reduced flags carried;
+a conjugation of a known-reduced row leaves the other relator unread).
 """
 import argparse
 import ctypes
@@ -39,6 +41,8 @@ def load(path):
     lib.acx_step.argtypes = [P] * 12 + [I64, I32, I32, I32, P]
     if hasattr(lib, "acx_step_lengths"):
         lib.acx_step_lengths.argtypes = [P] * 11 + [I64, I32, I32, I32, P]
+    if hasattr(lib, "acx_step_lengths_reduced"):
+        lib.acx_step_lengths_reduced.argtypes = [P] * 12 + [I64, I32, I32, I32, P]
     return lib
 
 
@@ -117,6 +121,7 @@ def main():
         tr = torch.empty(B, dtype=torch.uint8, device=dev)
         lens = torch.empty((B, 2), dtype=torch.int32, device=dev)
         err = torch.zeros(B, dtype=torch.uint8, device=dev)
+        red = torch.zeros(B, dtype=torch.uint8, device=dev)
         ec = torch.zeros(1, dtype=torch.int32, device=dev)
         s = torch.cuda.current_stream().cuda_stream
 
@@ -126,6 +131,10 @@ def main():
                 rc = lib.acx_step(st.data_ptr(), st.data_ptr(), acts[t].data_ptr(), starts.data_ptr(), cnt.data_ptr(),
                                   rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), lens.data_ptr(), None, err.data_ptr(),
                                   ec.data_ptr(), B, L, H, 1, s)
+            elif mode == "reduced":
+                rc = lib.acx_step_lengths_reduced(st.data_ptr(), acts[t].data_ptr(), starts.data_ptr(), cnt.data_ptr(),
+                                                  rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), lens.data_ptr(),
+                                                  red.data_ptr(), None, err.data_ptr(), ec.data_ptr(), B, L, H, 1, s)
             else:
                 if mode == "LL":
                     lens.fill_(L)
@@ -142,6 +151,7 @@ def main():
                 st.copy_(starts)
                 cnt.zero_()
                 ec.zero_()
+                red.zero_()
                 nz = st.view(B, 2, L) != 0
                 lens.copy_((nz * torch.arange(1, L + 1, device=dev, dtype=torch.int32)).amax(2))
                 for t in range(W):

@@ -22,6 +22,8 @@
 #                  a kernel trace plus separate FETCH_SIZE / WRITE_SIZE passes
 #   c2prof         kernel trace and SQ counters of config 2's step (tools/step_pmc.py)
 #   script:PATH    any python script of the repo, no arguments
+#   py:PATH,ARGS   a python script of the repo with arguments (commas for spaces); output
+#                  gpurun_out/TAG_<script name>.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:?tag}
@@ -72,6 +74,11 @@ for step in "$@"; do
          timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
              SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/${TAG}_c2pmc -o c2 --output-format csv \
              -- python3 $R/tools/step_pmc.py --L 36 --B 65536 --K 50 > $OUT/${TAG}_c2pmc.log 2>&1) || exit 10 ;;
+    py:*)
+        spec=${step#py:}
+        args=${spec//,/ }
+        name=$(basename ${args%% *} .py)
+        timeout -k 10 300 python -u $args > $OUT/${TAG}_${name}.json 2> $OUT/${TAG}_${name}.err || exit 12 ;;
     script:*)
         s=${step#script:}
         timeout -k 10 300 python -u $s > $OUT/${TAG}_$(basename $s .py).json 2> $OUT/${TAG}_$(basename $s .py).err || exit 11 ;;
