@@ -1048,12 +1048,20 @@ def run_rank(args):
         dist.destroy_process_group()
 
 
+def profile_tags(suffix: str) -> list:
+    """tags of the committed profiles/rNN/<tag>_summary.json whose tag ends in _<suffix>, newest
+    first (a round's run letters sort after its earlier ones: r06m > r06g > r05z > r05)"""
+    import glob
+    tags = [os.path.basename(p)[: -len("_summary.json")]
+            for p in glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", f"*_{suffix}_summary.json"))]
+    return sorted(tags, reverse=True)
+
+
 def committed_traffic(B, L, K, launch_bytes):
     """(HBM bytes of the headline launch from the newest committed rocprofv3 PMC profile of this
     workload, where from) or (None, None)"""
     cands = []
-    for tag in ("r05_k20", "r04_k20", "r04", "r03v_k20", "r03v", "r03m_k20", "r03m", "r02o_k20", "r02o", "r02h_k20", "r02h",
-                "r02_k20", "r02", "r01"):
+    for tag in profile_tags("k20") + ["r04", "r03v", "r03m", "r02o", "r02h", "r02", "r01"]:
         prof = os.path.join(REPO, "profiles", tag.split("_")[0][:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
@@ -1080,7 +1088,7 @@ def committed_step_traffic(B, L, launch_bytes, kernel):
     measured/algorithmic ratio applied to this launch's algorithmic bytes (the changed-relator
     rate, hence the bytes, vary slightly with the walk); or (None, None)"""
     want = kernel.replace(" ", "")
-    for tag in ("r05_step128", "r04w_step128", "r04n_step128", "r04n_step36", "r04_step128", "r04_step36"):
+    for tag in profile_tags("step128") + profile_tags("step36"):
         prof = os.path.join(REPO, "profiles", tag[:3], f"{tag}_summary.json")
         if not os.path.exists(prof):
             continue
