@@ -176,11 +176,9 @@ int64_t acx_internal_curriculum_fused_offset(int64_t B);
 int64_t acx_curriculum_workspace(int64_t B) {
     if (B < 0) return 0;
     const int64_t tiles = (B + WAVE - 1) / WAVE, groups = (tiles + WAVE - 1) / WAVE;
-    // acx_learner_step's part: [0] sequence number, [1, 2] base, tile counts, group totals, the
-    // groups' arrival words ACX_CUR_ARRIVE_STRIDE apart, and two mask words per tile (delegation)
-    // (acx_kernels.hip, CurLayout)
-    return acx_internal_curriculum_fused_offset(B) +
-           2 * (3 + tiles + groups + groups * ACX_CUR_ARRIVE_STRIDE + 2 * tiles);
+    // acx_learner_step's part: [0] sequence number, [1, 2] base, tile counts, group totals, and
+    // the groups' arrival words ACX_CUR_ARRIVE_STRIDE apart (acx_kernels.hip, CurLayout)
+    return acx_internal_curriculum_fused_offset(B) + 2 * (3 + tiles + groups + groups * ACX_CUR_ARRIVE_STRIDE);
 }
 
 int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const int32_t* curriculum_states,

@@ -616,11 +616,9 @@ struct FastTile {
 
     // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from their
     // fallback row (fb_src: `fallback`, or `fallback2` for FB_RESET rows; both pitch fpitch)
-    // skip (wave-uniform): rows left unwritten (the learner's delegated finished envs, step_body)
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
-                                          uint64_t skip = 0) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -628,25 +626,8 @@ struct FastTile {
             // contiguous rows, nothing flagged: chunk c goes to g + 4c (immediate offsets); a
             // full tile (wave-uniform) needs no per-chunk guards
             int4* dst = reinterpret_cast<int4*>(g) + ln;
-            if (skip) {  // the row of chunk c is c / CPR: one test against the scalar mask per chunk
-#pragma unroll
-                for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
-                    uint32_t p[STAGE_UNROLL];
-#pragma unroll
-                    for (int u = 0; u < STAGE_UNROLL; ++u)
-                        if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
-#pragma unroll
-                    for (int u = 0; u < STAGE_UNROLL; ++u) {
-                        const int c = ln + (u0 + u) * WAVE;
-                        if (u0 + u < CPR && c < nc && !((skip >> (c / CPR)) & 1ull))
-                            out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
-                    }
-                }
-            } else if (R == WAVE) {
-                store_flat<NT, F32, true>(dst, ln, nc);
-            } else {
-                store_flat<NT, F32, false>(dst, ln, nc);
-            }
+            if (R == WAVE) store_flat<NT, F32, true>(dst, ln, nc);
+            else store_flat<NT, F32, false>(dst, ln, nc);
             return;
         }
 #pragma unroll
@@ -658,7 +639,7 @@ struct FastTile {
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
                 const int c = ln + (u0 + u) * WAVE;
-                if (u0 + u < CPR && c < nc && !((skip >> (c / CPR)) & 1ull)) {
+                if (u0 + u < CPR && c < nc) {
                     const int r = c / CPR;
                     const int pos = 4 * (c - r * CPR);
                     int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
@@ -1291,8 +1272,7 @@ struct CodeTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
-                                          uint64_t skip = 0) const {  // skip: see FastTile::store
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -1306,7 +1286,6 @@ struct CodeTile {
                 const int c = ln + (u0 + u) * WAVE;
                 if (c >= nc) continue;
                 const int r = c / CPR;
-                if ((skip >> r) & 1ull) continue;
                 const int pos = 4 * (c - r * CPR);
                 int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
                 if (FB && tile_bad && flags[r]) {
@@ -1740,8 +1719,7 @@ struct GenericTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
-                                          uint64_t skip = 0) const {  // skip: see FastTile::store
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
         const int nc = (R * twoL) / VEC;
         It it(lane, twoL);
         for (int b0 = lane; b0 < nc; b0 += WAVE * STAGE_UNROLL) {
@@ -1761,7 +1739,7 @@ struct GenericTile {
             }
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
-                if (b0 + u * WAVE >= nc || ((skip >> rows[u]) & 1ull)) continue;
+                if (b0 + u * WAVE >= nc) continue;
                 int32_t* dst = g + (int64_t)rows[u] * gpitch + poss[u];
                 const uint32_t fc = FB ? flags[rows[u]] : 0u;
                 const bool fb = fc != 0u;
@@ -2037,11 +2015,9 @@ struct StepArgs {
 //     next_index from curr_index), since a give-up can leave a group's arrival word incomplete;
 //     CurriculumRecord.process raises on the word.  Concurrent launches on one workspace are not
 //     supported (they would overwrite each other's words; nothing detects it).
-//   * delegation (round 6, cur_copier): when the table surely lasts the launch, a tile with a few
-//     finished envs publishes their mask and goes on; the tile that completes the group copies them.
 // cur_ws (uint64 words): [0] sequence number, [1] base, [2] sticky failure word, [3, 3 + T) tile
-// counts, [3 + T, 3 + T + G) group totals, then the group arrival words ACX_CUR_ARRIVE_STRIDE
-// apart, then two mask words per tile (T tiles, G groups).
+// counts, [3 + T, 3 + T + G) group totals, [3 + T + G, 3 + T + 2G) group arrival words (T tiles,
+// G groups).
 // ---------------------------------------------------------------------------------
 constexpr uint64_t CUR_SET = 1ull << 62;
 constexpr uint32_t CUR_FAIL = 0xffffffffu;
@@ -2068,7 +2044,7 @@ __device__ __forceinline__ void cur_store(uint64_t* p, uint64_t v) {
 #define ACX_CUR_ARRIVE_STRIDE 32
 struct CurLayout {
     int64_t tiles, groups;
-    uint64_t *base, *tile, *group, *arrive, *mask;
+    uint64_t *base, *tile, *group, *arrive;
     __device__ __forceinline__ CurLayout(const StepArgs& a) {
         tiles = (a.B + WAVE - 1) / WAVE;
         groups = (tiles + WAVE - 1) / WAVE;
@@ -2076,7 +2052,6 @@ struct CurLayout {
         tile = a.cur_ws + 3;
         group = tile + tiles;
         arrive = group + groups;
-        mask = arrive + groups * ACX_CUR_ARRIVE_STRIDE;  // two words per tile (delegation)
     }
 };
 
@@ -2088,20 +2063,13 @@ struct CurLayout {
 // cnext: next_index as this wave read it, before publishing -- the last tile overwrites it once
 // every tile has published, so the read must complete first: the published word takes an opaque
 // dependency on it, both words being relaxed agent-scope atomics
-// deleg: the tile hands its finished envs (fm) to its group's copier (cur_copier): the mask goes
-// out first, as two seq-tagged 32-bit halves, and the count word carries CUR_DELEG
-constexpr uint32_t CUR_DELEG = 0x80000000u;
 __device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
-                                                int64_t cnext, bool deleg = false, uint64_t fm = 0) {
+                                                int64_t cnext) {
     if (w.lane != 0) return 0;
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
     if (t == 0) cur_store(c.base, cur_word(seq, (uint32_t)*a.cur_next));
-    if (deleg) {
-        cur_store(c.mask + 2 * t, cur_word(seq, (uint32_t)fm));
-        cur_store(c.mask + 2 * t + 1, cur_word(seq, (uint32_t)(fm >> 32)));
-    }
-    uint64_t word = cur_word(seq, cnt | (deleg ? CUR_DELEG : 0u));
+    uint64_t word = cur_word(seq, cnt);
     asm volatile("" : "+v"(word) : "s"((uint32_t)cnext));
     cur_store(c.tile + t, word);
     return __hip_atomic_fetch_add(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, (1ull << 32) | cnt, __ATOMIC_RELAXED,
@@ -2111,35 +2079,27 @@ __device__ __forceinline__ uint64_t cur_publish(const StepArgs& a, const WaveCtx
 __device__ __forceinline__ void cur_set_failed(const StepArgs& a) { cur_store(a.cur_ws + 2, 1ull); }
 
 // the add that completed its group publishes the group's total and clears the arrival word for
-// the next launch; returns (wave-uniform) whether this tile's add completed its group
-__device__ __forceinline__ bool cur_publish_end(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
+// the next launch
+__device__ __forceinline__ void cur_publish_end(const StepArgs& a, const WaveCtx& w, uint32_t seq, uint32_t cnt,
                                                 uint64_t old) {
-    bool last = false;
-    if (w.lane == 0) {
-        const CurLayout c(a);
-        const int64_t t = w.r0 / WAVE, g = t / WAVE;
-        const int64_t gsize = (c.tiles - g * WAVE) < WAVE ? (c.tiles - g * WAVE) : WAVE;
-        if ((int64_t)(old >> 32) + 1 == gsize) {
-            cur_store(c.group + g, cur_word(seq, (uint32_t)old + cnt));
-            cur_store(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, 0ull);
-            last = true;
-        }
+    if (w.lane != 0) return;
+    const CurLayout c(a);
+    const int64_t t = w.r0 / WAVE, g = t / WAVE;
+    const int64_t gsize = (c.tiles - g * WAVE) < WAVE ? (c.tiles - g * WAVE) : WAVE;
+    if ((int64_t)(old >> 32) + 1 == gsize) {
+        cur_store(c.group + g, cur_word(seq, (uint32_t)old + cnt));
+        cur_store(c.arrive + g * ACX_CUR_ARRIVE_STRIDE, 0ull);
     }
-    return __builtin_amdgcn_readfirstlane((int)last) != 0;
 }
 
-// base + the counts of every tile before this one (CUR_TILE: the totals of the groups before its
-// own and its group's earlier tiles; CUR_ALL: every group's total -- the last tile's next_index;
-// CUR_GROUP: the groups before its own only -- cur_copier's group base), or CUR_FAIL.  Wave-uniform
-// control flow.  A word, once seen with this
+// base + the counts of every tile before this one (all_groups: + every group's total instead: the
+// last tile's next_index), or CUR_FAIL.  Wave-uniform control flow.  A word, once seen with this
 // launch's seq, is final: each lane re-reads only the words it has not seen yet (`pend`), so the
 // polls of the waiting tiles thin out as the prefix fills in (re-reading every word on every poll
 // put ~4k waiting waves on the same few dozen lines).  Group totals are taken 4 per lane, 256 per
 // round; the base (lane 0) and the own group's earlier tile counts (a lane each) with the first.
 // (s_sleep 8 between polls instead: the same, r05v)
-enum { CUR_TILE = 0, CUR_ALL = 1, CUR_GROUP = 2 };
-__device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, int mode) {
-    const bool all_groups = mode == CUR_ALL;
+__device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx& w, uint32_t seq, bool all_groups) {
     if (a.cur_fail == 1 || (a.cur_fail == 2 && all_groups)) return CUR_FAIL;  // test hook
     const CurLayout c(a);
     const int64_t t = w.r0 / WAVE, g = t / WAVE;
@@ -2152,7 +2112,7 @@ __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx&
     };
     uint32_t pend = group_bits(0);
     if (w.lane == 0) pend |= 1u << 5;                            // the base
-    if (mode == CUR_TILE && g * WAVE + w.lane < t) pend |= 1u << 4;  // a tile before this one in its group
+    if (!all_groups && g * WAVE + w.lane < t) pend |= 1u << 4;  // a tile before this one in its group
     uint32_t x = 0, polls = 0;
     int64_t k0 = 0;
     while (true) {
@@ -2164,7 +2124,7 @@ __device__ __forceinline__ uint32_t cur_prefix(const StepArgs& a, const WaveCtx&
 #pragma unroll
         for (int i = 0; i < 6; ++i)
             if (((pend >> i) & 1u) && cur_is(v[i], seq)) {
-                x += (uint32_t)v[i] & ~CUR_DELEG;
+                x += (uint32_t)v[i];
                 pend &= ~(1u << i);
             }
         if (__all(pend == 0u)) {
@@ -2221,145 +2181,6 @@ __device__ __forceinline__ void copy_rows(const StepArgs& a, const WaveCtx& w, u
     }
 }
 
-// wave-inclusive prefix sum of v over the lanes
-__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_up((int)v, o, WAVE);
-        if (lane >= o) v += u;
-    }
-    return v;
-}
-
-// Delegation (acx_learner_step when the table surely lasts the launch, step_body).  A tile with
-// 1..cur_deleg_max finished envs does not wait for its ranking: it leaves their state and
-// observation rows unwritten, publishes which envs they are (cur_publish, deleg) and goes on; the
-// tile whose arrival completed the group -- every tile of the group has published by then -- copies
-// the group's delegated rows here: a finished env of tile t, j-th in its tile, takes initial state
-// k = base + the totals of the groups before g + the counts of g's tiles before t + j
-// (training.py:329-336; the same k as cur_prefix would give it): its state, obs_f32 and reset_state
-// rows <- curriculum row k as it is (acx_curriculum_assign's copy), curr_index = k, needs_host = 0.
-// The waiting is left to the 1 in 64 tiles that complete a group, not the ~1 in 4 that hold a
-// finished env in a steady-state step.  If a wait gives up, the delegated envs get their own
-// starting rows and needs_host = 3, and the sticky failure word is set, as for a tile's own
-// give-up.  `ent`: the wave's LDS tile area, >= cap int2 entries (cap >= 64 x cur_deleg_max).
-__device__ __forceinline__ void cur_copier(const StepArgs& a, const WaveCtx& w, uint32_t seq, int twoL, int2* ent,
-                                           int cap) {
-    const CurLayout c(a);
-    const int64_t g = (w.r0 / WAVE) / WAVE, t0 = g * WAVE;
-    const int64_t gsize = (c.tiles - t0) < WAVE ? (c.tiles - t0) : WAVE;
-    uint32_t gbase = cur_prefix(a, w, seq, CUR_GROUP);
-    bool ok = gbase != CUR_FAIL;
-    // the group's tile words, then the masks of its delegating tiles (words seen with this launch's
-    // seq are final; the group is complete, so every one of them has been written)
-    uint64_t tw = 0, fm = 0;
-    {
-        uint32_t pend = w.lane < gsize ? 1u : 0u, polls = 0;
-        while (true) {
-            if (pend & 1u) {
-                const uint64_t v = cur_load(c.tile + t0 + w.lane);
-                if (cur_is(v, seq)) {
-                    tw = v;
-                    pend = ((uint32_t)v & CUR_DELEG) ? 6u : 0u;
-                }
-            }
-            if (pend & 2u) {
-                const uint64_t v = cur_load(c.mask + 2 * (t0 + w.lane));
-                if (cur_is(v, seq)) {
-                    fm |= (uint64_t)(uint32_t)v;
-                    pend &= ~2u;
-                }
-            }
-            if (pend & 4u) {
-                const uint64_t v = cur_load(c.mask + 2 * (t0 + w.lane) + 1);
-                if (cur_is(v, seq)) {
-                    fm |= (uint64_t)(uint32_t)v << 32;
-                    pend &= ~4u;
-                }
-            }
-            if (__all(pend == 0u)) break;
-            if (++polls > (1u << 20)) {
-                // cannot happen once the group is complete (bounded anyway): which rows were handed
-                // over is unknown, so they stay unwritten; the sticky word makes the host re-zero
-                if (w.lane == 0) cur_set_failed(a);
-                return;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    const uint32_t cnt = (uint32_t)tw & ~CUR_DELEG;
-    const bool dl = ((uint32_t)tw & CUR_DELEG) != 0u;
-    const uint32_t pre = wave_inclusive_sum(cnt, w.lane) - cnt;  // the group's finished envs before tile t
-    const uint32_t dcnt = dl ? (uint32_t)__popcll(fm) : 0u;
-    const uint32_t dpre = wave_inclusive_sum(dcnt, w.lane) - dcnt;
-    const int D = __builtin_amdgcn_readlane((int)(dpre + dcnt), WAVE - 1);
-    if (D == 0) return;
-    if (D > cap) ok = false;  // (a delegating tile holds <= cur_deleg_max envs: cannot happen)
-    if (!ok && w.lane == 0) cur_set_failed(a);
-    // the entries (row in the batch, curriculum row k) in rank order
-    if (dl && D <= cap) {
-        uint64_t m = fm;
-        for (uint32_t j = 0; m; ++j, m &= m - 1) {
-            const int r = __builtin_ctzll(m);
-            ent[dpre + j] = make_int2((int)((t0 + w.lane) * WAVE + r), (int)(gbase + pre + j));
-        }
-    }
-    wave_sync();
-    const int nd = D <= cap ? D : 0;
-    int32_t* rs = const_cast<int32_t*>(a.reset_state);  // learner: writable
-    // each entry's row: 16-byte chunks over the lanes, CU loads in flight per lane before the stores
-    // (a failed ranking: the env's own starting row, not written to reset_state)
-    if ((twoL & 3) == 0) {
-        constexpr int CU = 4;
-        const int cpr = twoL >> 2, n = nd * cpr;
-        for (int i0 = 0; i0 < n; i0 += CU * WAVE) {
-            int4 v[CU];
-            int dst[CU];
-#pragma unroll
-            for (int u = 0; u < CU; ++u) {
-                const int i = i0 + u * WAVE + w.lane;
-                dst[u] = -1;
-                if (i < n) {
-                    const int q = i / cpr, cc = i - q * cpr;
-                    const int2 e = ent[q];
-                    const int32_t* src = ok ? a.cur_states + (int64_t)e.y * twoL : a.reset_state + (int64_t)e.x * twoL;
-                    v[u] = reinterpret_cast<const int4*>(src)[cc];
-                    dst[u] = e.x * cpr + cc;  // chunk index in the batch (B * 2L / 4 < 2^31)
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < CU; ++u) {
-                if (dst[u] < 0) continue;
-                reinterpret_cast<int4*>(a.state_out)[dst[u]] = v[u];
-                if (ok) reinterpret_cast<int4*>(rs)[dst[u]] = v[u];
-                if (a.obs_f32)
-                    reinterpret_cast<float4*>(a.obs_f32)[dst[u]] = make_float4((float)v[u].x, (float)v[u].y,
-                                                                               (float)v[u].z, (float)v[u].w);
-            }
-        }
-    } else {
-        for (int i = w.lane; i < nd * twoL; i += WAVE) {
-            const int q = i / twoL, cc = i - q * twoL;
-            const int2 e = ent[q];
-            const int32_t v = ok ? a.cur_states[(int64_t)e.y * twoL + cc] : a.reset_state[(int64_t)e.x * twoL + cc];
-            a.state_out[(int64_t)e.x * twoL + cc] = v;
-            if (ok) rs[(int64_t)e.x * twoL + cc] = v;
-            if (a.obs_f32) a.obs_f32[(int64_t)e.x * twoL + cc] = (float)v;
-        }
-    }
-    for (int q = w.lane; q < nd; q += WAVE) {
-        const int2 e = ent[q];
-        if (ok) a.curr_index[e.x] = e.y;
-        a.needs_host[e.x] = ok ? 0 : 3;
-    }
-}
-// the most finished envs a tile delegates (cur_copier's entries fit the wave's LDS tile area)
-template <class Tile>
-__device__ __forceinline__ int cur_deleg_max(int L) {
-    const int fit = (int)((Tile::wave_bytes(L) - 8) / (sizeof(int2) * WAVE));  // (8-byte aligned start)
-    return fit < 8 ? fit : 8;
-}
-
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
 // LIVE: the lengths-carrying step (its own kernel, so the plain step's registers stay its own)
 template <int NW, int LC, int VEC, bool LEARN, bool LIVE, int BATCH = 0>
@@ -2375,6 +2196,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // next_index as this launch found it (the last tile replaces it only after every tile has
     // published, i.e. read it).  exhausted (round 1 complete): no finished env gets a state from
     // the table, so no tile waits for its ranking; the host draws for every finished env.
+    // (Leaving a finished env's rows out of the tile's stores when the table surely lasts the
+    // launch, so that its copy needs no drain, was slower: the tile's obs store then takes its
+    // per-chunk flagged path, 0.164 vs 0.150 ms per steady-state step, r05zg.)
     const int64_t cnext = cur ? (int64_t)__builtin_amdgcn_readfirstlane(
                                     __hip_atomic_load(a.cur_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                               : 0;
@@ -2382,10 +2206,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // a give-up in an earlier launch (cur_set_failed) left the workspace unusable until the host
     // re-zeroes it: this launch ranks nothing
     const bool broken = cur && __builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws + 2)) != 0;
-    // the table surely lasts the launch (every finished env of it gets a state): a tile with a few
-    // finished envs may delegate them to its group's copier instead of waiting (cur_copier)
-    const bool sure = cur && !broken && !exhausted && a.n_states - cnext >= a.B;
-    const int tdel = sure ? cur_deleg_max<Tile>(a.L) : 0;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2447,7 +2267,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (a.reset_state && a.step_count && !a.pending) {  // kernel arguments: uniform
             pre = __ballot(w.active && cnt_in + 1 >= a.horizon);
             if (__popcll(pre) > Tile::RPI) pre = 0;  // more (a synchronised truncation): the tile reload below
-            if (__popcll(pre) <= tdel) pre = 0;      // delegated (below, unless dones add to them): no reset row
             if (pre) pv = tile.fetch_rows(a.reset_state + w.r0 * twoL, pre, w.lane);
         }
     }
@@ -2490,12 +2309,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // an env that ends is reset by the next call
         reset = a.pending ? pend : (fin && a.reset_state && !keep);
     }
-    // delegation (cur_copier): a tile with 1..tdel finished envs leaves them to its group's copier --
-    // no autoreset here (their rows are not written at all), step count 0 as for any ended episode
-    const uint64_t fm = cur ? __ballot(fin) : 0ull;
-    const bool deleg = fm != 0ull && __popcll(fm) <= tdel;  // wave-uniform
-    const bool creset = deleg && fin;
-    if (creset) reset = false;
     if constexpr (PREF) {
         if (pre) tile.put_rows(pv, pre, pre & __ballot(reset), w.lane);
     }
@@ -2530,10 +2343,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     }
     // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
     // count now; the ranking itself waits until the tile's stores are issued (the tail below)
-    bool copier = false;  // this tile completed its group (cur_copier)
-    if (cur && !broken) {
+    uint64_t fm = 0;
+    if (cur) {
+        fm = __ballot(fin);
         const uint32_t cnt = (uint32_t)__popcll(fm);
-        copier = cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext, deleg, fm));
+        if (!broken) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
     }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
@@ -2572,10 +2386,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
         if (reset) cnt = 0;
-    }
-    if (creset) {  // delegated: the copier writes the row (rb is 0 here: no finished env was reset)
-        cnt = 0;
-        dm = 0u;
     }
     if (w.active) {
         if (a.step_count) st_scalar<false, int32_t>(a.step_count + env, cnt);
@@ -2620,8 +2430,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, NT_OBS, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
-                                               a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL,
-                                               deleg ? fm : 0ull);
+                                               a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
     if (cur) {
         // The curriculum's tail (training.py:329-336, 349-352).  A finished env was reset to its own
         // starting row above like any env; now -- every store of the tile issued, so the memory
@@ -2633,11 +2442,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // (round 1 complete) needs_host = 1 and the host draws.  The last tile waits for the total
         // (the new next_index).  The copies are made by the whole wave, 16-byte chunks over the
         // lanes (copy_rows): one lane copying its own row made the steady-state step 0.165 ms
-        // instead of 0.150 (r05zg).  A delegating tile skips all of this (cur_copier).
-        const uint32_t first =
-            broken ? CUR_FAIL : (fm && !exhausted && !deleg) ? cur_prefix(a, w, cseq, CUR_TILE) : 0u;
+        // instead of 0.150 (r05zg).
+        const uint32_t first = broken ? CUR_FAIL : (fm && !exhausted) ? cur_prefix(a, w, cseq, false) : 0u;
         if (!broken && w.r0 + w.R == a.B) {
-            const uint32_t tot = cur_prefix(a, w, cseq, CUR_ALL);
+            const uint32_t tot = cur_prefix(a, w, cseq, true);
             if (w.lane == 0) {
                 // every group is complete: no wave of this launch reads next_index or the sequence
                 // number again -- advance both for the next one.  A total that never arrived leaves
@@ -2654,7 +2462,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (failed && !broken && w.lane == 0) cur_set_failed(a);
         // finished envs with index k = first + (finished envs before it in the tile) < n_states
         uint64_t take = 0;
-        if (fm && !exhausted && !failed && !deleg) {
+        if (fm && !exhausted && !failed) {
             const int64_t nq = a.n_states - (int64_t)first;  // how many of the tile's finished envs get a state
             take = fm;
             while (take && (int64_t)__popcll(take) > nq) take &= ~(1ull << (63 - __builtin_clzll(take)));
@@ -2665,14 +2473,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             copy_rows(a, w, take, twoL, [&](int q, int) { return a.cur_states + ((int64_t)first + q) * twoL; }, true);
         }
-        if (copier && sure) {
-            // this tile completed its group: the group's delegated envs (the wave's LDS tile area,
-            // its stores issued, holds the entries)
-            char* area = smem + w.wid * Tile::wave_bytes(a.L);
-            int2* ent = reinterpret_cast<int2*>((reinterpret_cast<uintptr_t>(area) + 7u) & ~(uintptr_t)7u);
-            cur_copier(a, w, cseq, twoL, ent, WAVE * cur_deleg_max<Tile>(a.L));
-        }
-        if (w.active && !creset) {  // a delegated env's needs_host / curr_index: its copier's
+        if (w.active) {
             uint8_t nh = 0;
             if (fin) {
                 if (failed) nh = 3;
