@@ -452,7 +452,6 @@ struct FastTile {
     // chunk; put_rows later writes the rows in `apply` (a subset) into the tile, as load_rows does
     static constexpr bool PREFETCH_OK = true;
     static constexpr bool LIVE_ROWS = true;  // set_lim selects the chunks a live load reads
-    static constexpr bool ENDS_OK = false;   // ends_quiet: CodeTile rows only
     static constexpr int RPI = WAVE / CPR;  // rows per wave-instruction
     __device__ __forceinline__ int4 fetch_rows(const int32_t* __restrict__ g, uint64_t rows, int lane) const {
         const int s = lane / CPR, c = lane - s * CPR;
@@ -912,7 +911,6 @@ struct CodeTile {
     static __host__ __device__ constexpr size_t wave_bytes(int) { return (size_t)WAVE * S * 4 + 4 * WAVE; }
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
     static constexpr bool LIVE_ROWS = true;  // see FastTile
-    static constexpr bool ENDS_OK = true;    // ends_quiet (step_body)
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
     __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
@@ -1597,7 +1595,6 @@ template <int NW, int LC, int VEC>
 struct GenericTile {
     static constexpr bool PREFETCH_OK = false;  // fetch_rows / put_rows: FastTile only
     static constexpr bool LIVE_ROWS = false;  // whole rows: set_lim is a no-op
-    static constexpr bool ENDS_OK = false;
     static constexpr int RPI = 1;
     __device__ __forceinline__ int4 fetch_rows(const int32_t*, uint64_t, int) const { return int4{0, 0, 0, 0}; }
     __device__ __forceinline__ void put_rows(const int4&, uint64_t, uint64_t, int) {}
@@ -2184,68 +2181,6 @@ __device__ __forceinline__ void copy_rows(const StepArgs& a, const WaveCtx& w, u
     }
 }
 
-// ENDS (acx_step_lengths_reduced on CodeTile rows, L = 128): whether the move provably changes
-// nothing, decided from a few 16-byte chunks at the relators' ends read straight from the row by
-// the env's lane -- the tile load then leaves the whole row out.  The row is reduced for this
-// call's mode (its flag) with n0, n1 >= 2.  Conjugation r_i <- g r_i g^-1 (ac_moves.py:79-156):
-// start_cancel = r_i[0] == g^-1, end_cancel = r_i[n-1] == g (:119-120); cyclically (ACEnv's
-// cyclical=True) the result reduces back to r_i when both or neither hold (a cyclically reduced
-// r_i cannot have both), otherwise it is a rotation; not cyclically, only the gate
-// n + 2 - 2(sc + ec) > L (:123-126) leaves r_i unchanged.  Concatenation r_i <- r_i r_j^{+-1}
-// (ac_moves.py:4-76): the junction count acc (:56-60) from r_i's last letters and r_j^{+-1}'s first
-// ones, gated when n_i + n_j - 2 acc > L (:62-64); the chunks read hold >= 5 letters of each side,
-// and an acc that could reach past them counts as undecided (the row is loaded and moved as
-// usual).  simplify_presentation (utils.py:246-283) leaves the reduced relators as they are, so a
-// quiet move leaves the row, its lengths and its flag unchanged (pl::ac_move_clean: same outcome).
-__device__ __forceinline__ bool ends_quiet(const int32_t* row, int L, int n0, int n1, int act, bool cyc) {
-    auto chunk = [&](int rel, int c) { return reinterpret_cast<const int4*>(row + rel * L)[c]; };
-    auto pick = [](const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
-    const int i = (act + 1) & 1;  // the target relator (ac_moves.py:192-206)
-    const int ni = i ? n1 : n0;
-    if (act >= 4) {
-        const uint32_t gc = (CONJ_G >> (2 * (act - 4))) & 3u;  // x = 0, x^-1 = 1, y = 2, y^-1 = 3
-        const int gl = (gc & 2u) ? ((gc & 1u) ? -2 : 2) : ((gc & 1u) ? -1 : 1);
-        const int4 a0 = chunk(i, 0), a1 = chunk(i, (ni - 1) >> 2);
-        const bool sc = a0.x == -gl, ec = pick(a1, (ni - 1) & 3) == gl;
-        if (cyc) return sc == ec;
-        return ni + 2 - 2 * ((int)sc + (int)ec) > L;
-    }
-    const int j = 1 - i;
-    const int nj = j ? n1 : n0;
-    const bool inv = act == 1 || act == 2;
-    // r_i's last letters: its chunks ci0, ci0 + 1; B = r_j^{+-1}'s first letters: r_j's chunks 0, 1,
-    // or (inverted) its last two, read backwards and negated
-    const int ci = (ni - 1) >> 2, ci0 = ci > 0 ? ci - 1 : 0;
-    const int4 t0 = chunk(i, ci0), t1 = chunk(i, ci);
-    const int cj = inv ? (nj - 1) >> 2 : 1, cj0 = inv ? (cj > 0 ? cj - 1 : 0) : 0;
-    const int4 h0 = chunk(j, cj0), h1 = chunk(j, cj);
-    const int avail_i = ni - 4 * ci0;
-    const int avail_j = inv ? nj - 4 * cj0 : (nj < 8 ? nj : 8);
-    const int mn = ni < nj ? ni : nj;
-    const int lim = mn < avail_i ? (mn < avail_j ? mn : avail_j) : (avail_i < avail_j ? avail_i : avail_j);
-    int acc = -1;
-    for (int k = 0; k < lim; ++k) {
-        const int pi = ni - 1 - k - 4 * ci0;
-        const int x = pi < 4 ? pick(t0, pi) : pick(t1, pi - 4);
-        int b;
-        if (inv) {
-            const int pj = nj - 1 - k - 4 * cj0;
-            b = -(pj < 4 ? pick(h0, pj) : pick(h1, pj - 4));
-        } else {
-            b = k < 4 ? pick(h0, k) : pick(h1, k - 4);
-        }
-        if (x != -b) {
-            acc = k;
-            break;
-        }
-    }
-    if (acc < 0) {
-        if (lim < mn) return false;  // undecided: every letter read cancels
-        acc = mn;
-    }
-    return ni + nj - 2 * acc > L;
-}
-
 // LEARN: acx_step_learner's extra inputs/outputs (compiled out of the plain acx_step path);
 // LIVE: the lengths-carrying step (its own kernel, so the plain step's registers stay its own)
 template <int NW, int LC, int VEC, bool LEARN, bool LIVE, int BATCH = 0>
@@ -2298,9 +2233,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // empty (n = 0, no live chunks), which the move, the dirty image and the write-back leave alone.
     bool skip = false;
     int skip_h = 0, n_skip = 0;  // the relator left unread and its length
-    bool quiet = false;          // ENDS: the move changes nothing (ends_quiet); the row is not loaded
-    int n_in0 = 0, n_in1 = 0;    // LIVE: the rows' relator lengths on entry
     if constexpr (LIVE) {
+        int n_in0 = 0, n_in1 = 0;  // the rows' relator lengths on entry
         if (w.active) {
             n_in0 = a.lengths_out[2 * env];
             n_in1 = a.lengths_out[2 * env + 1];
@@ -2308,20 +2242,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if constexpr (Tile::LIVE_ROWS) {
             if (a.reduced && w.active) {
                 const uint32_t rf = a.reduced[env];
-                const bool known = ((rf >> (a.cyclical ? 1 : 0)) & 1u) != 0u && act_in >= 0 && act_in < 12 && !pend &&
-                                   !(a.step_count && cnt_in + 1 >= a.horizon);
                 skip_h = act_in & 1;  // ids 4..11: the move's target is r_{(id + 1) & 1}
                 n_skip = skip_h ? n_in1 : n_in0;
-                skip = known && act_in >= 4 && n_skip >= 2 && n_skip <= L;
-                if constexpr (Tile::ENDS_OK) {
-                    if (known && n_in0 >= 2 && n_in1 >= 2 && n_in0 <= L && n_in1 <= L)
-                        quiet = ends_quiet(a.state_in + env * twoL, L, n_in0, n_in1, act_in, a.cyclical != 0);
-                }
-                if (quiet) skip = false;
+                skip = ((rf >> (a.cyclical ? 1 : 0)) & 1u) != 0u && act_in >= 4 && act_in < 12 && !pend &&
+                       n_skip >= 2 && n_skip <= L && !(a.step_count && cnt_in + 1 >= a.horizon);
             }
         }
-        if (quiet) tile.set_lim(w.lane, 0, 0);
-        else tile.set_lim(w.lane, (skip && skip_h == 0) ? 0 : n_in0, (skip && skip_h == 1) ? 0 : n_in1);
+        tile.set_lim(w.lane, (skip && skip_h == 0) ? 0 : n_in0, (skip && skip_h == 1) ? 0 : n_in1);
         wave_sync();
         tile.template load<true, true, Tile::NT_STEP_LOADS>(a.state_in + w.r0 * twoL, w.R, w.lane);
     } else {
@@ -2361,7 +2288,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         const bool bad = tile.template pack<LIVE>(w.lane, p);
         const bool cyc = a.cyclical != 0;
         if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
-        else if (quiet) e = ACX_ERR_NONE;  // nothing loaded, nothing changes (ends_quiet)
         else if (bad) e = ACX_ERR_DOMAIN;
         else if (skip) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);  // reduced: see above
         else if (pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
@@ -2372,14 +2298,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             }
         keep = e != ACX_ERR_NONE;
         if (keep) cnt = cnt0;  // the reference raises before count_steps += 1 (ac_env.py:93-102)
-        if (!keep && !quiet) dm = tile.template unpack_dirty<LIVE>(w.lane, p);
-        if (quiet) {  // the row as it is: its lengths (the planes stay empty; nothing reads them)
-            p.n0 = n_in0;
-            p.n1 = n_in1;
-        }
-        // (a skipped relator is held as n = 0 in p and has >= 2 letters: never trivial; a quiet
-        // row has two relators of >= 2 letters)
-        triv = !pend && !keep && !quiet && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
+        if (!keep) dm = tile.template unpack_dirty<LIVE>(w.lane, p);
+        // (a skipped relator is held as n = 0 in p and has >= 2 letters: never trivial)
+        triv = !pend && !keep && pl::is_trivial<PW>(p.w0, p.n0, p.w1, p.n1);
         trunc = !pend && !keep && a.step_count && cnt >= a.horizon;
         // a resetting step (next-step autoreset) returns reward 0, as the vector env's reset does
         rwd = pend ? 0 : triv ? a.horizon * L * 2 : -(p.n0 + p.n1 + n_skip * (int)skip);
@@ -2446,9 +2367,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
             tile.load(a.reset_state + w.r0 * twoL, w.R, w.lane);
             if (reset) rbad = tile.pack(w.lane, p);
             wave_sync();
-            // (a quiet row's planes are empty and its row in HBM is current: left out)
-            if (w.active && !keep && !quiet && !rbad) tile.unpack(w.lane, p);
-            dm = (w.active && !keep && !quiet) ? 3u : 0u;  // the tile now holds starting rows: write every kept-moving row
+            if (w.active && !keep && !rbad) tile.unpack(w.lane, p);
+            dm = (w.active && !keep) ? 3u : 0u;  // the tile now holds starting rows: write every kept-moving row
             tile.restore_flags(w.lane, (w.active && keep) ? FB_IN : (rbad ? FB_RESET : 0u));
         } else {
             // a few lanes: the wave loads just their rows (scattered resets cost their rows only),

@@ -384,21 +384,20 @@ def restore(snap, tensors) -> None:
         x.copy_(y)
 
 
-def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=None, reads=None) -> dict:
+def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=None, unread=None) -> dict:
     """What the n steps step_fn(0..n-1) will do from here, counted off the clock: they are run
     from a snapshot of `tensors` (every buffer the steps read and write; the kernels are
     deterministic, so the timed pass that follows takes this same walk) and the snapshot is put
     back.  Per env-step: "changed" relators (the in-place write-back's unit), with `lens` (the
     lengths-carrying step's (B, 2) lengths) the "live_read" / "live_written" bytes of 16-byte
-    chunks, with `finished` ((done, truncated) uint8 tensors) the "finished" envs; `reads(t)`
-    (evaluated before step t; acx_step_lengths_reduced) gives (unread, ends_chunks, ends_lines):
-    (B, 2) bool, the relators the tile load leaves out (a conjugation's other relator, or both
-    for a quiet move), and per env the 16-byte chunks / 128-B lines ends_quiet reads first."""
+    chunks, with `finished` ((done, truncated) uint8 tensors) the "finished" envs; `unread(t)`
+    ((B, 2) bool, evaluated before step t) marks the relators that step leaves unread
+    (acx_step_lengths_reduced's skipped relator)."""
     import torch
 
     snap = [t.clone() for t in tensors]
     B = state.shape[0]
-    chg = rd = wr = fin = srd = swr = lrd = skp = ech = eln = 0.0
+    chg = rd = wr = fin = srd = swr = lrd = skp = 0.0
     if lens is not None:
         # byte offset of each relator in the (B, 2L) int32 state: the 64-B sectors its chunks touch
         rel0 = ((torch.arange(B, device=state.device, dtype=torch.int64) * 2 * L)[:, None]
@@ -410,13 +409,9 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
     for t in range(n):
         before = state.clone()
         n_before = lens.clone() if lens is not None else None
-        keep, e_ch, e_ln = 1, None, None
-        if reads is not None:
-            un, e_ch, e_ln = reads(t)
-            keep = (~un).to(torch.int64)
-            skp += float(un.sum().item())
-            ech += float(e_ch.sum().item())
-            eln += float(e_ln.sum().item())
+        keep = (~unread(t)).to(torch.int64) if unread is not None else 1
+        if unread is not None:
+            skp += float((1 - keep).sum().item())
         step_fn(t)
         ch = (before.view(B, 2, L) != state.view(B, 2, L)).any(2)
         chg += float(ch.sum().item())
@@ -439,76 +434,8 @@ def replay_walk(step_fn, state, tensors, n: int, L: int, lens=None, finished=Non
         del before, n_before
     restore(snap, tensors)
     d = max(1, n) * B
-    # the ends' chunks are read on top of the tile's live chunks (a moving row reads them again
-    # with its tile: counted twice); each is its own 64-B sector
-    rd += ech * 16
-    srd += ech * 64
-    lrd += eln * 128
     return {"changed": chg / d, "live_read": rd / d, "live_written": wr / d, "finished": fin / d,
-            "sector_read": srd / d, "sector_written": swr / d, "line_read": lrd / d, "unread": skp / d,
-            "ends_chunks": ech / d, "ends_lines": eln / d}
-
-
-def step_reads(st, lens, red, a, cnt, H: int, L: int, ends: bool, cyc: bool = True):
-    """acx_step_lengths_reduced's reads at one step, restated in torch for the byte count (its
-    kernel decides the same per env, step_body / ends_quiet): (unread (B, 2) bool, ends chunks (B,),
-    ends lines (B,))"""
-    import torch
-
-    B = st.shape[0]
-    dev = st.device
-    ar = torch.arange(B, device=dev)
-    a = a.to(torch.int64)
-    n0, n1 = lens[:, 0].to(torch.int64), lens[:, 1].to(torch.int64)
-    known = (((red >> (1 if cyc else 0)) & 1) != 0) & (a >= 0) & (a < 12) & (cnt.to(torch.int64) + 1 < H)
-    h = a & 1  # a conjugation leaves r_{id & 1} alone
-    n_sk = torch.where(h == 1, n1, n0)
-    skip = known & (a >= 4) & (n_sk >= 2) & (n_sk <= L)
-    zero = torch.zeros(B, dtype=torch.int64, device=dev)
-    if not ends:
-        return torch.nn.functional.one_hot(h, 2).bool() & skip[:, None], zero, zero
-    ev = known & (n0 >= 2) & (n1 >= 2) & (n0 <= L) & (n1 <= L)
-    rows = st.view(B, 2, L).to(torch.int64)
-    i = (a + 1) & 1
-    j = 1 - i
-    ni, nj = torch.where(i == 1, n1, n0), torch.where(j == 1, n1, n0)
-    ri, rj = rows[ar, i], rows[ar, j]
-    # conjugation: start / end cancel (ac_moves.py:119-120)
-    conj_g = (1 << 0) | (3 << 2) | (3 << 4) | (0 << 6) | (0 << 8) | (2 << 10) | (2 << 12) | (1 << 14)
-    gc = (conj_g >> (2 * (a - 4).clamp(min=0))) & 3
-    gl = torch.tensor([1, -1, 2, -2], device=dev)[gc]
-    first = ri[:, 0]
-    last = ri.gather(1, (ni - 1).clamp(0, L - 1)[:, None])[:, 0]
-    sc, ec = first == -gl, last == gl
-    conj_quiet = (sc == ec) if cyc else (ni + 2 - 2 * (sc.long() + ec.long()) > L)
-    c_last = (ni - 1).clamp(min=0) >> 2
-    conj_ch = 1 + (c_last != 0).long()
-    conj_ln = 1 + ((c_last >> 3) != 0).long()
-    # concatenation: the junction count from the ends read (ac_moves.py:56-64)
-    inv = (a == 1) | (a == 2)
-    ci = (ni - 1).clamp(min=0) >> 2
-    ci0 = (ci - 1).clamp(min=0)
-    cj = torch.where(inv, (nj - 1).clamp(min=0) >> 2, torch.ones_like(nj))
-    cj0 = torch.where(inv, (cj - 1).clamp(min=0), torch.zeros_like(nj))
-    avail_i = ni - 4 * ci0
-    avail_j = torch.where(inv, nj - 4 * cj0, nj.clamp(max=8))
-    mn = torch.minimum(ni, nj)
-    lim = torch.minimum(mn, torch.minimum(avail_i, avail_j))
-    k = torch.arange(8, device=dev)[None, :]
-    x = ri.gather(1, (ni[:, None] - 1 - k).clamp(0, L - 1))
-    b = torch.where(inv[:, None], -rj.gather(1, (nj[:, None] - 1 - k).clamp(0, L - 1)), rj[:, :8])
-    nc = (x != -b) & (k < lim[:, None])
-    has = nc.any(1)
-    acc = torch.where(has, nc.to(torch.int64).argmax(1), torch.where(lim < mn, torch.full_like(mn, -1), mn))
-    cat_quiet = (acc >= 0) & (ni + nj - 2 * acc > L)
-    cat_ch = 2 + (ci != ci0).long() + (cj != cj0).long()
-    cat_ln = 1 + ((ci >> 3) != (ci0 >> 3)).long() + 1 + ((cj >> 3) != (cj0 >> 3)).long()
-    conj = a >= 4
-    quiet = ev & torch.where(conj, conj_quiet, cat_quiet)
-    ech = torch.where(ev, torch.where(conj, conj_ch, cat_ch), zero)
-    eln = torch.where(ev, torch.where(conj, conj_ln, cat_ln), zero)
-    un = (torch.nn.functional.one_hot(h, 2).bool() & (skip & ~quiet)[:, None]) | quiet[:, None]
-    return un, ech, eln
+            "sector_read": srd / d, "sector_written": swr / d, "line_read": lrd / d, "unread": skp / d}
 
 
 def learner_buffers(lenv) -> list:
@@ -888,12 +815,14 @@ def run_rank(args):
                          reward=rew1, done=dn1, truncated=tr1, lengths=lens2, err=err, err_count=err_count,
                          lengths_in=True, reduced=red2)
 
-            def reads(t):
-                # the kernel's rules (step_body): a row flagged reduced for this mode, a valid move
-                # id, no truncation on this step -> known; a conjugation of a known row leaves
-                # r_{id & 1} unread (>= 2 letters); at L = 128 a known row with two relators of
-                # >= 2 letters reads the ends first (ends_quiet) and, when the move is quiet, no more
-                return step_reads(st2, lens2, red2, actions[W + t], cnt2, H, L, ends=L == 128)
+            def unread(t):
+                # the kernel's skip rule (step_body): flag for this mode, a conjugation (ids 4..11),
+                # the untouched relator r_{id & 1} of >= 2 letters, no truncation on this step
+                a = actions[W + t]
+                h = (a & 1).to(torch.int64)
+                n_sk = lens2.gather(1, h[:, None])[:, 0]
+                ok = (((red2 >> 1) & 1) != 0) & (a >= 4) & (a < 12) & (n_sk >= 2) & (n_sk <= L) & (cnt2 + 1 < H)
+                return torch.nn.functional.one_hot(h, 2).bool() & ok[:, None]
 
             err_count.zero_()
             for t in range(W):
@@ -909,7 +838,7 @@ def run_rank(args):
             # live bytes follow the walk's lengths, which grow through a horizon and drop at the
             # synchronised resets, so a sample of other steps would not do.
             rp = replay_walk(lambda t: step2(actions[W + t]), st2, (st2, cnt2, lens2, red2, err_count), K, L,
-                             lens=lens2, reads=reads,
+                             lens=lens2, unread=unread,
                              finished=(dn1, tr1))
             rd, wr = rp["live_read"], rp["live_written"]
             sb_len = rd + wr + 16 + 27 + 2  # + the reduced flag in and out
@@ -930,7 +859,6 @@ def run_rank(args):
                              "line_bytes_per_env_step": rp["line_read"] + wr + 16 + 29 + rp["finished"] * 8 * L,
                              "resets_per_env_step": rp["finished"],
                              "unread_relators_per_env_step": rp["unread"],
-                             "ends_chunks_per_env_step": rp["ends_chunks"], "ends_lines_per_env_step": rp["ends_lines"],
                              "bytes_note": "live chunks only: ceil(n/4) x 16 B read per relator the step reads (a "
                                            "conjugation of a row known reduced leaves the other relator unread), "
                                            "changed relators' chunks inside old or new letters written, lengths 16 B "
