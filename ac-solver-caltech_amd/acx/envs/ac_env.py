@@ -264,8 +264,9 @@ class VecACEnv:
         # write the flags); the next lengths-carrying step zeroes them first
         self.reduced = torch.zeros(B, dtype=torch.uint8, device=dev)
         self._reduced_ok = True
-        # the lengths-carrying step where it measured faster (ops.LENGTHS_STEP_L, L = 128)
-        self._live_tile = L in ops.LENGTHS_STEP_L
+        # the lengths-carrying step where it measured faster (ops.lengths_step_for: L = 128, and L = 36
+        # above the small-batch range)
+        self._live_tile = ops.lengths_step_for(B, L)
         self.err = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.err_count = torch.zeros(1, dtype=torch.int32, device=dev)
         if autoreset_mode not in ("same_step", "next_step"):

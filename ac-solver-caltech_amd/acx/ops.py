@@ -74,6 +74,15 @@ LENGTHS_STEP_L = (128,)
 SMALL_STEP_MAX_B = 2 * 4 * 256 * 64
 
 
+def lengths_step_for(B: int, L: int) -> bool:
+    """whether VecACEnv.step (and bench.py's step headline) take the lengths-carrying step with
+    reduced flags (acx_step_lengths_reduced): at L = 128, and at L = 36 above the small-batch
+    range -- there a conjugation's unread relator makes it 5 % faster than acx_step at 2^20 envs
+    (0.0683 vs 0.0719 ms, profiles/r06/r06k_ab_reduced_L36.json), while acx_step's two-lane kernel
+    keeps the small batches"""
+    return L in LENGTHS_STEP_L or (L == 36 and B > SMALL_STEP_MAX_B)
+
+
 def step_kernel_name(B: int, L: int) -> str:
     """the kernel acx_step launches for B envs at max_relator_length L (bench lines, profiles)"""
     nw = 1 if L <= 16 else 2 if L <= 32 else 3 if L <= 48 else 4 if L <= 64 else 8

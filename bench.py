@@ -800,7 +800,7 @@ def run_rank(args):
         # the same walk through the lengths-carrying step (acx_step_lengths), where VecACEnv.step
         # takes it (ops.LENGTHS_STEP_L) or with --workload step; at L = 36 it ties with acx_step
         # (DESIGN.md "The lengths-carrying step") and the default line leaves it out
-        run_len = not rollout_head or L in ops.LENGTHS_STEP_L
+        run_len = not rollout_head or ops.lengths_step_for(B, L)
         same = True
         if run_len:
             st2 = starts.clone()
@@ -874,7 +874,7 @@ def run_rank(args):
             if not same:  # a lengths-path regression must not publish a headline
                 variants["step_api_lengths"]["error"] = "states differ from acx_step's on the same walk"
             del st2, cnt2, lens2
-        if not rollout_head and (L not in ops.LENGTHS_STEP_L or not same):
+        if not rollout_head and (not ops.lengths_step_for(B, L) or not same):
             # whole-row tiles (or a lengths walk that left acx_step's states): the headline is acx_step
             a_api = B * sb / (s_api / K) / 1e9
             head = {

@@ -814,13 +814,17 @@ def test_packed_rollout_full_horizon_every_env_vs_oracle():
     assert int(ec.item()) == 0
 
 
-def test_config5_shard_every_env_vs_oracle():
+@pytest.mark.parametrize("L", [128, 36])
+def test_config5_shard_every_env_vs_oracle(L):
     """BASELINE configs[4]'s per-GPU shard (2^20 envs, L = 128, Miller-Schupp starts, random moves,
-    horizon 200) through VecACEnv.step -- acx_step_lengths once the rows' lengths are current --
-    on every env and step against the C oracle: states, rewards, flags and the carried lengths."""
+    horizon 200) through VecACEnv.step -- acx_step_lengths_reduced once the rows' lengths are
+    current (lengths and reduced flags carried) -- on every env and step against the C oracle:
+    states, rewards, flags and the carried lengths.  L = 36: the same batch at configs[2]'s L,
+    which VecACEnv also steps with the reduced lengths-carrying kernel (ops.lengths_step_for)."""
     import bench
-    from acx import VecACEnv
-    L, B, K, H = 128, 1 << 20, 8, 200
+    from acx import VecACEnv, ops
+    B, K, H = 1 << 20, 8, 200
+    assert ops.lengths_step_for(B, L)
     init = bench.ms_starts(L, B)
     env = VecACEnv(init, horizon_length=H, device=DEV, track_final_obs=False)
     g = torch.Generator(device=DEV)
@@ -837,6 +841,7 @@ def test_config5_shard_every_env_vs_oracle():
         assert np.array_equal(dn.cpu().numpy(), d_) and np.array_equal(tr.cpu().numpy(), t_), t
         assert np.array_equal(env.lengths.cpu().numpy(), lens), t
     assert np.array_equal(env.step_count.cpu().numpy(), c)
+    assert int((env.reduced != 0).sum().item()) == B  # every row stepped cleanly: known reduced
 
 
 def test_config2_full_horizon_every_env_vs_oracle():

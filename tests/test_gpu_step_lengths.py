@@ -208,7 +208,7 @@ def test_vec_env_lengths_after_rollout_and_direct_writes(L):
     rng = np.random.default_rng(3)
     start = _rows(L, B, rng)
     env = VecACEnv(start, horizon_length=H, device=DEV)
-    assert env._live_tile == (L in ops.LENGTHS_STEP_L)
+    assert env._live_tile == ops.lengths_step_for(B, L)
     twin = VecACEnv(start, horizon_length=H, device=DEV)
     twin._lengths_ok = False  # the twin always takes acx_step (it rewrites its lengths each call)
     T = 6
