@@ -616,9 +616,12 @@ struct FastTile {
 
     // LDS -> global rows with row pitch `gpitch` int32; FB: flagged rows copied from their
     // fallback row (fb_src: `fallback`, or `fallback2` for FB_RESET rows; both pitch fpitch)
+    // skip (wave-uniform): rows left unwritten (the learner's finished envs when the curriculum
+    // table surely lasts the launch: their copy writes them, step_body)
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
+                                          uint64_t skip = 0) const {
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -626,8 +629,25 @@ struct FastTile {
             // contiguous rows, nothing flagged: chunk c goes to g + 4c (immediate offsets); a
             // full tile (wave-uniform) needs no per-chunk guards
             int4* dst = reinterpret_cast<int4*>(g) + ln;
-            if (R == WAVE) store_flat<NT, F32, true>(dst, ln, nc);
-            else store_flat<NT, F32, false>(dst, ln, nc);
+            if (skip) {  // the row of chunk c is c / CPR: one test against the scalar mask per chunk
+#pragma unroll
+                for (int u0 = 0; u0 < CPR; u0 += STAGE_UNROLL) {
+                    uint32_t p[STAGE_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < STAGE_UNROLL; ++u)
+                        if (u0 + u < CPR && ln + (u0 + u) * WAVE < nc) p[u] = lds[lds_index(ln, u0 + u)];
+#pragma unroll
+                    for (int u = 0; u < STAGE_UNROLL; ++u) {
+                        const int c = ln + (u0 + u) * WAVE;
+                        if (u0 + u < CPR && c < nc && !((skip >> (c / CPR)) & 1ull))
+                            out16<NT, F32>(dst + (u0 + u) * WAVE, widen4(p[u]));
+                    }
+                }
+            } else if (R == WAVE) {
+                store_flat<NT, F32, true>(dst, ln, nc);
+            } else {
+                store_flat<NT, F32, false>(dst, ln, nc);
+            }
             return;
         }
 #pragma unroll
@@ -639,7 +659,7 @@ struct FastTile {
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
                 const int c = ln + (u0 + u) * WAVE;
-                if (u0 + u < CPR && c < nc) {
+                if (u0 + u < CPR && c < nc && !((skip >> (c / CPR)) & 1ull)) {
                     const int r = c / CPR;
                     const int pos = 4 * (c - r * CPR);
                     int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
@@ -1272,7 +1292,8 @@ struct CodeTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
+                                          uint64_t skip = 0) const {  // skip: see FastTile::store
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int nc = R * CPR;
@@ -1286,6 +1307,7 @@ struct CodeTile {
                 const int c = ln + (u0 + u) * WAVE;
                 if (c >= nc) continue;
                 const int r = c / CPR;
+                if ((skip >> r) & 1ull) continue;
                 const int pos = 4 * (c - r * CPR);
                 int4* dst = reinterpret_cast<int4*>(g + (int64_t)r * gpitch + pos);
                 if (FB && tile_bad && flags[r]) {
@@ -1719,7 +1741,8 @@ struct GenericTile {
 
     template <bool FB, bool NT = false, bool F32 = false>
     __device__ __forceinline__ void store(int32_t* g, int64_t gpitch, int R, const int32_t* fallback,
-                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr) const {
+                                          int64_t fpitch, int lane, const int32_t* fallback2 = nullptr,
+                                          uint64_t skip = 0) const {  // skip: see FastTile::store
         const int nc = (R * twoL) / VEC;
         It it(lane, twoL);
         for (int b0 = lane; b0 < nc; b0 += WAVE * STAGE_UNROLL) {
@@ -1739,7 +1762,7 @@ struct GenericTile {
             }
 #pragma unroll
             for (int u = 0; u < STAGE_UNROLL; ++u) {
-                if (b0 + u * WAVE >= nc) continue;
+                if (b0 + u * WAVE >= nc || ((skip >> rows[u]) & 1ull)) continue;
                 int32_t* dst = g + (int64_t)rows[u] * gpitch + poss[u];
                 const uint32_t fc = FB ? flags[rows[u]] : 0u;
                 const bool fb = fc != 0u;
@@ -2206,6 +2229,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     // a give-up in an earlier launch (cur_set_failed) left the workspace unusable until the host
     // re-zeroes it: this launch ranks nothing
     const bool broken = cur && __builtin_amdgcn_readfirstlane((int)(uint32_t)cur_load(a.cur_ws + 2)) != 0;
+    // the table surely lasts the launch (every finished env gets an initial state from it): a
+    // finished env is not autoreset here -- its rows are left out of the tile's stores and written
+    // once, by the curriculum copy, which then needs no drain of the tile's stores (below)
+    const bool sure = cur && !broken && !exhausted && a.n_states - cnext >= a.B;
     Tile tile(smem + w.wid * Tile::wave_bytes(a.L), a.L);
     const int L = tile.Lr(), twoL = 2 * L;
     const int64_t env = w.r0 + w.lane;
@@ -2266,7 +2293,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     if constexpr (PREF) {
         if (a.reset_state && a.step_count && !a.pending) {  // kernel arguments: uniform
             pre = __ballot(w.active && cnt_in + 1 >= a.horizon);
-            if (__popcll(pre) > Tile::RPI) pre = 0;  // more (a synchronised truncation): the tile reload below
+            if (__popcll(pre) > Tile::RPI || sure) pre = 0;  // more (a synchronised truncation): the tile reload below
             if (pre) pv = tile.fetch_rows(a.reset_state + w.r0 * twoL, pre, w.lane);
         }
     }
@@ -2307,7 +2334,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         fin = triv || trunc;
         // same-step autoreset: an env that ends resets now; next-step: a pending env resets now and
         // an env that ends is reset by the next call
-        reset = a.pending ? pend : (fin && a.reset_state && !keep);
+        reset = a.pending ? pend : (fin && a.reset_state && !keep && !sure);
     }
     if constexpr (PREF) {
         if (pre) tile.put_rows(pv, pre, pre & __ballot(reset), w.lane);
@@ -2387,6 +2414,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (rbad) e = ACX_ERR_DOMAIN;  // lengths_out: the non-zero counts of the starting row
         if (reset) cnt = 0;
     }
+    if (sure && fin) {  // the curriculum copy writes the row (no autoreset above: rb has none of them)
+        cnt = 0;
+        dm = 0u;
+    }
     if (w.active) {
         if (a.step_count) st_scalar<false, int32_t>(a.step_count + env, cnt);
         if (a.lengths_out) {
@@ -2430,7 +2461,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     }
     if (LEARN && a.obs_f32)  // the same rows as float32, straight into the learner's buffer
         tile.template store<true, NT_OBS, true>(reinterpret_cast<int32_t*>(a.obs_f32) + w.r0 * twoL, twoL, w.R,
-                                               a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL);
+                                               a.state_in + w.r0 * twoL, twoL, w.lane, a.reset_state + w.r0 * twoL,
+                                               sure ? fm : 0ull);
     if (cur) {
         // The curriculum's tail (training.py:329-336, 349-352).  A finished env was reset to its own
         // starting row above like any env; now -- every store of the tile issued, so the memory
@@ -2469,10 +2501,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         }
         if (take) {
             // the rows were autoreset above (a failed ranking leaves them so): the tile's own
-            // stores of them complete first
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // stores of them complete first -- unless `sure`: the tile left them out
+            if (!sure) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             copy_rows(a, w, take, twoL, [&](int q, int) { return a.cur_states + ((int64_t)first + q) * twoL; }, true);
         }
+        // `sure` and a finished env without a state (a failed ranking): its own starting row, as the
+        // autoreset would have left it
+        const uint64_t own = sure ? (fm & ~take) : 0ull;
+        if (own) copy_rows(a, w, own, twoL, [&](int, int r) { return a.reset_state + (w.r0 + r) * twoL; }, false);
         if (w.active) {
             uint8_t nh = 0;
             if (fin) {
