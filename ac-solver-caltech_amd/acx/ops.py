@@ -63,10 +63,9 @@ def _L_of(states: torch.Tensor) -> int:
 # relator lengths for which acx_step_lengths reads and writes only the live chunks (the kernels'
 # compile-time tiles); at any other L it reads whole rows like acx_step
 LIVE_TILE_L = (36, 128)
-# where the lengths-carrying step measured faster than acx_step, so VecACEnv.step (and
-# bench.py's step headline) take it: L = 128 (config 5: 4.8e9 vs 3.8e9 env-steps/s per GPU over a
-# horizon); at L = 36 the two tie (0.0793 vs 0.0799 ms per 2^20-env step in-process, 4 % the
-# other way in a bench line: 288-B rows leave little to save against the per-chunk live test)
+# where the lengths-carrying step measured faster than acx_step at any batch: L = 128 (config 5:
+# 4.8e9 vs 3.8e9 env-steps/s per GPU over a horizon, round 4; with the reduced flags 7.5e9).  At
+# L = 36 it wins only above the small-batch range (lengths_step_for)
 LENGTHS_STEP_L = (128,)
 # acx_step at a compile-time L = 36 tile with B <= this many envs runs the small-batch kernel
 # (step_pair_kernel: two lanes per env, one per relator, so config 2's 65,536 envs are two waves

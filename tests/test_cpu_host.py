@@ -56,6 +56,19 @@ def test_rollout_move_id_path_choice():
                         torch.zeros(4, dtype=torch.int32), T=3, horizon=5)
 
 
+def test_step_path_choice():
+    """The per-call step kernels VecACEnv / bench.py pick: the two-lane small-batch kernel for
+    acx_step at L = 36 and B <= 131,072; the lengths-carrying step with reduced flags at L = 128
+    and at L = 36 above that range (ops.lengths_step_for); whole rows at any other L."""
+    from acx import ops
+    S = ops.SMALL_STEP_MAX_B
+    assert ops.step_kernel_name(65536, 36) == "acx::step_pair_kernel<3,36,4>"
+    assert ops.step_kernel_name(S + 1, 36) == "acx::step_kernel<3,36,4,false>"
+    assert ops.lengths_step_for(1 << 20, 128) and ops.lengths_step_for(64, 128)
+    assert ops.lengths_step_for(1 << 20, 36) and not ops.lengths_step_for(S, 36)
+    assert not ops.lengths_step_for(1 << 20, 18) and not ops.lengths_step_for(1 << 20, 64)
+
+
 def test_host_utils_match_reference_cases():
     with open(os.path.join(GOLDEN, "unit_cases.json")) as f:
         unit = json.load(f)
