@@ -2336,6 +2336,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // an env that ends is reset by the next call
         reset = a.pending ? pend : (fin && a.reset_state && !keep && !sure);
     }
+    // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
+    // count as soon as it is known (before its reset rows and scalar stores); the ranking itself
+    // waits until the tile's stores are issued (the tail below)
+    uint64_t fm = 0;
+    if (cur) {
+        fm = __ballot(fin);
+        const uint32_t cnt = (uint32_t)__popcll(fm);
+        if (!broken) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
+    }
     if constexpr (PREF) {
         if (pre) tile.put_rows(pv, pre, pre & __ballot(reset), w.lane);
     }
@@ -2367,14 +2376,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         if (a.pending) a.pending[env] = fin ? 1 : 0;
         // final_obs <- post-move state (per lane: rare, and only with final_obs)
         if (reset && a.final_obs) regs_to_global<PW>(a.final_obs + env * twoL, p, L);
-    }
-    // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
-    // count now; the ranking itself waits until the tile's stores are issued (the tail below)
-    uint64_t fm = 0;
-    if (cur) {
-        fm = __ballot(fin);
-        const uint32_t cnt = (uint32_t)__popcll(fm);
-        if (!broken) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
     }
     // out-of-domain rows the load did not flag (a zero inside a relator: CodeTile's slots cannot
     // hold it) are stored from their input row too
