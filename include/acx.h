@@ -216,7 +216,12 @@ int acx_curriculum_assign(const uint8_t* done, const uint8_t* truncated, const i
  * finished envs in env order itself (per-64-env-tile counts and per-group totals in the
  * workspace) and, after a tile's own stores, a finished env with index k < n_states takes initial
  * state k -- its state, obs_f32 and reset_state rows become that row as it is, curr_index[env] = k;
- * past the table's end needs_host[env] = 1.  needs_host[env] = 3: the ranking gave up (an earlier
+ * past the table's end needs_host[env] = 1.  When the table surely lasts the launch
+ * (*next_index + B <= n_states) a finished env is not autoreset first: its rows are written once,
+ * from the curriculum row, and its err reports the step alone (acx_step_learner's autoreset would
+ * add err 3 for an out-of-domain reset_state row; LearnerEnv's rows never differ that way: an env
+ * holding an out-of-domain row fails every step and never finishes).
+ * needs_host[env] = 3: the ranking gave up (an earlier
  * tile not scheduled within ~seconds); the env kept its own starting row and was not ranked.  Any
  * give-up -- a tile's ranking, or the last tile's total, after which *next_index is stale -- also
  * sets the workspace's sticky failure word (acx_learner_failure_word); from then on every launch
