@@ -374,3 +374,42 @@ def test_step_lengths_walk_with_resets_vs_oracle_L128(cyc, reduced):
         if reduced:
             _check_reduced_flags(red, o_st, L, t)
     assert n_reset > B and n_err > 0
+
+
+@pytest.mark.parametrize("L", [128, 36])
+def test_step_lengths_reduced_flags_across_cyclical_modes(L):
+    """The reduced flags carried through calls that alternate cyclical=True / False (bit 1 set only
+    by cyclical calls, bit 0 by both): every call equals acx_step on the same rows, and a flagged
+    row is reduced in the sense its bits claim."""
+    from acx import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(L + 99)
+    B, T, H = 64 * 19 + 7, 24, 11
+    start = _rows(L, B, rng)
+    st = {k: _t(start) for k in "ab"}
+    rs = _t(start)
+    cnt = {k: torch.zeros(B, dtype=torch.int32, device=DEV) for k in "ab"}
+    rew = {k: torch.zeros(B, dtype=torch.int32, device=DEV) for k in "ab"}
+    dn = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    tr = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    err = {k: torch.zeros(B, dtype=torch.uint8, device=DEV) for k in "ab"}
+    lens_a = torch.zeros((B, 2), dtype=torch.int32, device=DEV)
+    lens_b = _t(np.stack([np.count_nonzero(start[:, :L], 1), np.count_nonzero(start[:, L:], 1)], 1).astype(np.int32))
+    red = torch.zeros(B, dtype=torch.uint8, device=DEV)
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    seen = set()
+    for t in range(T):
+        cyc = (t // 3) % 2  # three steps in each mode
+        at = _t(rng.integers(0, 12, size=B).astype(np.int32))
+        P = lambda x, k: x[k].data_ptr()  # noqa: E731
+        assert lib.acx_step(P(st, "a"), P(st, "a"), at.data_ptr(), rs.data_ptr(), P(cnt, "a"), P(rew, "a"),
+                            P(dn, "a"), P(tr, "a"), lens_a.data_ptr(), None, P(err, "a"), None, B, L, H, cyc,
+                            stream) == 0
+        assert lib.acx_step_lengths_reduced(P(st, "b"), at.data_ptr(), rs.data_ptr(), P(cnt, "b"), P(rew, "b"),
+                                            P(dn, "b"), P(tr, "b"), lens_b.data_ptr(), red.data_ptr(), None,
+                                            P(err, "b"), None, B, L, H, cyc, stream) == 0
+        for name, d in (("state", st), ("reward", rew), ("done", dn), ("trunc", tr), ("count", cnt), ("err", err)):
+            assert torch.equal(d["a"], d["b"]), (t, name)
+        _check_reduced_flags(red, st["b"], L, t)
+        seen |= set(np.unique(red.cpu().numpy()).tolist())
+    assert {0, 1, 3} <= seen  # both modes' flags and unflagged (reset) rows occurred
