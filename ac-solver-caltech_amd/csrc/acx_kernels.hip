@@ -2308,16 +2308,45 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
     int act = 0;
     bool triv = false, trunc = false;
     int32_t rwd = 0;
+    bool bad = false, clean = false;
+    const bool cyc = a.cyclical != 0;
     if (w.active) {
         act = act_in;
         cnt0 = cnt_in;
         cnt = a.step_count ? cnt0 + 1 : 0;
-        const bool bad = tile.template pack<LIVE>(w.lane, p);
-        const bool cyc = a.cyclical != 0;
+        bad = tile.template pack<LIVE>(w.lane, p);
+        clean = !bad && !skip && pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc);
+    }
+    // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
+    // count as soon as it is known; the ranking itself waits until the tile's stores are issued
+    // (the tail below).  Usually that is before the move: a truncating env finishes unless its move
+    // fails, which on a reduced row only an emptying concatenation (n_i == n_j) can; any other env
+    // finishes only if the move makes it trivial, which needs the relator it leaves alone at one
+    // letter.  A tile with an env outside those cases publishes after the move.
+    uint64_t fm = 0;
+    bool early = false;  // wave-uniform: published before the move
+    uint32_t early_cnt = 0;
+    if (cur && !broken) {
+        bool unc = false, f0 = false;
+        if (w.active && !pend && !bad && act_in >= 0 && act_in < 12) {
+            const bool i1 = ((act_in + 1) & 1) != 0;  // the move's target relator (ac_moves.py:192-206)
+            const int nt = i1 ? p.n1 : p.n0, nu = i1 ? p.n0 : p.n1;
+            const bool tr = a.step_count && cnt0 + 1 >= a.horizon;
+            if (!clean) unc = true;  // the general path reduces both relators: anything can happen
+            else if (tr) { unc = act_in < 4 && nt == nu; f0 = true; }
+            else unc = nu <= 1;
+        }
+        if (!__any(unc)) {
+            early = true;
+            early_cnt = (uint32_t)__popcll(__ballot(f0));
+            cur_publish_end(a, w, cseq, early_cnt, cur_publish(a, w, cseq, early_cnt, cnext));
+        }
+    }
+    if (w.active) {
         if (pend) e = ACX_ERR_NONE;  // no move: the env resets (gymnasium >= 1.0 NEXT_STEP autoreset)
         else if (bad) e = ACX_ERR_DOMAIN;
         else if (skip) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);  // reduced: see above
-        else if (pl::is_clean<PW>(p.w0, p.n0, p.w1, p.n1, cyc)) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
+        else if (clean) e = pl::ac_move_clean<PW>(p.w0, p.n0, p.w1, p.n1, act, L, cyc);
         else {
                 const pl::MoveOut<PW> mo = pl::ac_move_call<PW>(p, act, L, cyc);
                 p = mo.p;
@@ -2336,14 +2365,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a) {
         // an env that ends is reset by the next call
         reset = a.pending ? pend : (fin && a.reset_state && !keep && !sure);
     }
-    // the curriculum (acx_learner_step, training.py:319-336): every tile publishes its finished
-    // count as soon as it is known (before its reset rows and scalar stores); the ranking itself
-    // waits until the tile's stores are issued (the tail below)
-    uint64_t fm = 0;
     if (cur) {
         fm = __ballot(fin);
         const uint32_t cnt = (uint32_t)__popcll(fm);
-        if (!broken) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
+        if (!broken) {
+            if (!early) cur_publish_end(a, w, cseq, cnt, cur_publish(a, w, cseq, cnt, cnext));
+            else if (cnt != early_cnt && w.lane == 0) cur_set_failed(a);  // cannot happen: made loud
+        }
     }
     if constexpr (PREF) {
         if (pre) tile.put_rows(pv, pre, pre & __ballot(reset), w.lane);
