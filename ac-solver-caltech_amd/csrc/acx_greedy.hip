@@ -69,6 +69,12 @@ struct DevArgs {
     uint64_t bmask;
     int64_t lo, hi;           // commit: node ids [lo, hi)
     int n, L, kw, cyc;
+    // round completion (greedy_round_kernel): blocks done so far (device word, back to 0 by the
+    // last block) and the host-visible word the last block sets to `seq` -- the host sees the
+    // round's outputs (pinned memory) without waiting for the stream
+    uint32_t* blocks_done;
+    uint32_t* done_flag;
+    uint32_t seq;
 };
 
 // lane per (parent, action): one move, the child's key, its hash, its id if it is a node below
@@ -156,12 +162,25 @@ __global__ __launch_bounds__(256) void greedy_commit_kernel(DevArgs a) {
 // round, the others expand the round's parents against the nodes committed before (ids < lo).
 // The two halves touch disjoint key-store rows; a probe that meets a concurrent table insert
 // sees the slot empty or holding an id >= lo (skipped), and either way reaches every older entry.
+// Every block then releases its writes at system scope and counts itself done; the last one sets
+// done_flag = seq, so the host can take the outputs (and reuse the staging buffers, which the
+// commit blocks read) as soon as the last block is through, ahead of the stream's own completion.
 template <int NW>
 __global__ __launch_bounds__(256) void greedy_round_kernel(DevArgs a, int cblocks) {
     if ((int)blockIdx.x < cblocks)
         commit_lane<NW + 1>(a, a.lo + (int64_t)blockIdx.x * 256 + threadIdx.x);
     else
         expand_lane<NW>(a, ((int)blockIdx.x - cblocks) * 256 + threadIdx.x);
+    if (a.done_flag == nullptr) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        const uint32_t old = __hip_atomic_fetch_add(a.blocks_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == gridDim.x) {
+            __hip_atomic_store(a.blocks_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // host restatement of bfs::khash (the kernels' hash): the host tables index by it
@@ -228,6 +247,9 @@ struct Engine {
     DevArgs d{};
     uint64_t *h_in = nullptr, *h_out = nullptr;    // pinned, host view
     uint64_t *hd_in = nullptr, *hd_out = nullptr;  // the same memory, device view
+    uint32_t *h_flag = nullptr, *hd_flag = nullptr;  // the rounds' completion word (pinned)
+    uint32_t* d_blocks = nullptr;                    // the rounds' block count (device)
+    uint32_t round_seq = 0;                          // the last round's completion value
     int64_t commit_cap = 0;
 
     // wait for the stream by polling (hipStreamSynchronize may sleep on an interrupt: tens of us
@@ -238,13 +260,25 @@ struct Engine {
         }
         return e == hipSuccess ? ACX_OK : ACX_E_LAUNCH;
     }
+    // a round: until its last block has set the completion word (greedy_round_kernel), or the
+    // stream is through (checked every 256 polls: a launch that failed never sets the word)
+    int wait_round(uint32_t seq) const {
+        for (uint32_t i = 1;; ++i) {
+            if (__atomic_load_n(h_flag, __ATOMIC_ACQUIRE) == seq) return ACX_OK;
+            if ((i & 255u) == 0u) {
+                const hipError_t e = hipStreamQuery(stream);
+                if (e == hipSuccess) return ACX_OK;
+                if (e != hipErrorNotReady) return ACX_E_LAUNCH;
+            }
+        }
+    }
 
     ~Engine() {
         if (stream) (void)hipStreamSynchronize(stream);
-        void* dp[] = {d.nkeys, d.table};
+        void* dp[] = {d.nkeys, d.table, d_blocks};
         for (void* p : dp)
             if (p) (void)hipFree(p);
-        void* hp[] = {h_in, h_out};
+        void* hp[] = {h_in, h_out, h_flag};
         for (void* p : hp)
             if (p) (void)hipHostFree(p);
         if (stream) (void)hipStreamDestroy(stream);
@@ -272,7 +306,11 @@ struct Engine {
         bool ok = hipHostMalloc((void**)&h_in, in_words * 8, hipHostMallocMapped) == hipSuccess &&
                   hipHostMalloc((void**)&h_out, out_words * 8, hipHostMallocMapped) == hipSuccess &&
                   hipHostGetDevicePointer((void**)&hd_in, h_in, 0) == hipSuccess &&
-                  hipHostGetDevicePointer((void**)&hd_out, h_out, 0) == hipSuccess;
+                  hipHostGetDevicePointer((void**)&hd_out, h_out, 0) == hipSuccess &&
+                  hipHostMalloc((void**)&h_flag, 64, hipHostMallocMapped) == hipSuccess &&
+                  hipHostGetDevicePointer((void**)&hd_flag, h_flag, 0) == hipSuccess &&
+                  hipMalloc((void**)&d_blocks, 64) == hipSuccess && hipMemset(d_blocks, 0, 64) == hipSuccess;
+        if (ok) *h_flag = 0u;
         // the device store starts at min(budget, INIT_DCAP) nodes and doubles as the search grows
         // (the reference's set grows with the search: a large budget on a search that ends early
         // must not fail on an up-front allocation)
@@ -774,11 +812,14 @@ int Engine::expand_round(const std::vector<int64_t>& batch) {
     d.chash = hd_out + (size_t)n * ACT * kw;
     d.cknown = reinterpret_cast<int64_t*>(d.chash + (size_t)n * ACT);
     if (n == 0 && n_nodes == lo) return ACX_OK;
+    d.blocks_done = d_blocks;
+    d.done_flag = hd_flag;
+    d.seq = ++round_seq;
     RoundLaunch rl{this};
     bfs::by_nw(L, rl);
-    if (n == 0) return hipGetLastError() == hipSuccess ? wait() : ACX_E_LAUNCH;
+    if (n == 0) return hipGetLastError() == hipSuccess ? wait_round(d.seq) : ACX_E_LAUNCH;
     const int64_t tw = now_ns();
-    if (hipGetLastError() != hipSuccess || wait() != ACX_OK) return ACX_E_LAUNCH;
+    if (hipGetLastError() != hipSuccess || wait_round(d.seq) != ACX_OK) return ACX_E_LAUNCH;
     const int64_t tc = now_ns();
     ns_wait += tc - tw;
     const uint64_t* ck = h_out;
