@@ -1050,11 +1050,16 @@ def run_rank(args):
 
 def profile_tags(suffix: str) -> list:
     """tags of the committed profiles/rNN/<tag>_summary.json whose tag ends in _<suffix>, newest
-    first (a round's run letters sort after its earlier ones: r06m > r06g > r05z > r05)"""
+    first (a round's runs are lettered a..z, then aa..: r06ad > r06u > r06g > r05zz > r05z > r05)"""
     import glob
     tags = [os.path.basename(p)[: -len("_summary.json")]
             for p in glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", f"*_{suffix}_summary.json"))]
-    return sorted(tags, reverse=True)
+    def age(tag):  # r06ad after r06z after r06u after r06 (the letters count up: a..z, then aa..)
+        run = tag.split("_")[0]
+        letters = run[3:]
+        return (run[:3], len(letters), letters)
+
+    return sorted(tags, key=age, reverse=True)
 
 
 def committed_traffic(B, L, K, launch_bytes):
