@@ -2724,6 +2724,8 @@ __global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
     Planes<1> w;
     int n;
     bool bad = pair_pack<HALF>(mine, w, n) || flagged;
+    const Planes<1> w_in = w;  // the relator as loaded: "changed" is decided on the planes
+    const int n_in = n;
     const Planes<1> rw = pl::prev<1>(w, n);
     bool clean = pl::relator_clean<1>(w, n, cyc);
     Planes<1> pw, prw;
@@ -2785,9 +2787,13 @@ __global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
         fin = triv || trunc;
         reset = a.pending ? pend : (fin && a.reset_state && !keep);
     }
-    // this lane's relator re-imaged (a failed env keeps its loaded image)
+    // this lane's relator changed (a failed env keeps its row): compared on the planes (canonical:
+    // no bits past the letters), so the common store below needs no re-imaged tile
     bool chg = false;
-    if (active && !keep) chg = pair_image<HALF>(mine, w, n);
+    if (active && !keep) {
+        const uint64_t m = pl::bmask<1>(n).b[0];
+        chg = n != n_in || (((w.s[0] ^ w_in.s[0]) | (w.y[0] ^ w_in.y[0])) & m) != 0ull;
+    }
     // same-step autoreset (or a pending env's reset): the lane loads its relator of the starting
     // row into the image (FastTile::load_rows' result; an out-of-domain starting row is taken as it
     // is and stored from reset_state, FB_RESET)
@@ -2842,6 +2848,27 @@ __global__ __launch_bounds__(BLOCK, 4) void step_pair_kernel(StepArgs a) {
     const uint64_t fb_rst = __ballot(active && reset && rbad);
     const uint64_t fb_in = __ballot(active && !reset && e == ACX_ERR_DOMAIN);
     const uint64_t dirty = __ballot(active && chg);
+    if (a.in_place && fb_rst == 0ull && R == ENVS) {
+        // the common case (wave-uniform): each lane writes its own changed relator, 9 contiguous
+        // 16-byte chunks, straight from its planes (or, reset, from the starting row it loaded
+        // into its image) -- no re-imaged tile, no tile-wide LDS pass
+        if (dirty == 0ull) return;
+        if (chg) {
+            int4* d = reinterpret_cast<int4*>(a.state_out + env * twoL + h * L);
+            if (reset) {
+#pragma unroll
+                for (int k = 0; k < HALF; ++k) out16<NT_WRITEBACK, false>(d + k, widen4(mine[k]));
+            } else {
+#pragma unroll
+                for (int k = 0; k < HALF; ++k)
+                    out16<NT_WRITEBACK, false>(
+                        d + k, widen4(pl::nibbles_to_i8x4(pl::nib<1>(w.s, k), pl::nib<1>(w.y, k), clamp_bits(8 * n - 32 * k))));
+            }
+        }
+        return;
+    }
+    // otherwise the tile's image (moved relators re-imaged) and the coalesced stores below
+    if (active && !keep && !reset) pair_image<HALF>(mine, w, n);
     wave_sync();
     const int nc = R * CPR;
     int4* dst = reinterpret_cast<int4*>(a.state_out + r0 * twoL);
