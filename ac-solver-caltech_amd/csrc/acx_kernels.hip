@@ -2566,12 +2566,14 @@ __global__ __launch_bounds__(BLOCK, Occupancy<LC>::waves_per_simd) void step_ker
 //     int8 image in LDS; relator q of the tile (q = 2e + h) is chunks [9q, 9q + 9) -- lane q's;
 //   * lane q packs ITS relator into bit planes (pl::, one 64-bit word per plane at L <= 64) and
 //     takes its partner's planes and length with four DPP quad-permutes (quad_perm [1,0,3,2]);
-//   * both lanes run the env's move (acx_planes.h: the junction cancellation count and the
-//     cyclic peel are the first set bit of a mismatch mask, the splice is shifts of the planes);
-//   * lane q re-images only its relator and compares it with the loaded image: the per-relator
-//     "changed" bits, the rows' fallback codes and the error flags are wave ballots -- one bit per
-//     relator, bit q <-> chunks [9q, 9q + 9) -- so the coalesced in-place write-back tests chunk c
-//     against bit c / 9 of a 64-bit scalar mask, no per-row flag bytes.
+//   * the move is split over the pair (pl::pair_move_clean: the target lane moves its relator,
+//     the junction cancellation count and the cyclic peel are the first set bit of a mismatch
+//     mask, the splice is shifts of the planes); an unreduced env runs the general move on both;
+//   * lane q decides on the planes whether its relator changed; in the common case (in place, full
+//     tile, no out-of-domain reset) it writes that relator's 9 chunks straight from its planes.
+//     Otherwise the moved relators are re-imaged into the tile and the "changed" bits, the rows'
+//     fallback codes and the error flags -- wave ballots, one bit per relator, bit q <-> chunks
+//     [9q, 9q + 9) -- steer a coalesced write-back that tests chunk c against bit c / 9.
 // Results are those of step_body<..., LEARN = false, LIVE = false> (the same pack, move,
 // image and error contract; tests/test_gpu_*: every acx_step test at L = 36 and B <= 131,072 runs
 // here); only the instruction schedule differs.  launch_step takes it for B <= SMALL_STEP_MAX_B.
