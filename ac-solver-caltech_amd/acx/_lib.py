@@ -29,6 +29,9 @@ SIGNATURES = {
     "acx_step": ([_P] * 12 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_step_lengths": ([_P] * 11 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_step_lengths_reduced": ([_P] * 12 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),
+    "acx_step_plan_create": ([_I32] + [_P] * 12 + [_I64, _I32, _I32, _I32], ctypes.c_void_p),
+    "acx_step_plan_launch": ([_P, _P, _P], ctypes.c_int),
+    "acx_step_plan_destroy": ([_P], None),
     # ..., action_hist, hist_cap, hist_base, hist_t, episode_len, ...
     "acx_step_learner": ([_P] * 11 + [_I32, _P, _I64, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _P], ctypes.c_int),
     "acx_step_record": ([_P] * 11 + [_I32, _P, _I64] + [_P] * 3 + [_I64, _I32, _I32, _I32, _P], ctypes.c_int),

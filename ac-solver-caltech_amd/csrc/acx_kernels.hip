@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <new>
+
 #include <type_traits>
 
 #include "acx.h"
@@ -3946,6 +3948,66 @@ int acx_step_lengths_reduced(int32_t* state, const int32_t* action, const int32_
     StepLaunch f{a, (hipStream_t)stream, false};
     return dispatch(L, f);
 }
+
+// a per-call step with everything but the move ids resolved once (acx.h): the launch is then a
+// three-argument call -- at 65,536 envs a caller's ctypes call with 17 arguments took as long as
+// half the kernel, and the host, not the GPU, set the eager rate
+struct acx_step_plan {
+    int32_t kind;
+    const int32_t* state_in;
+    int32_t* state_out;
+    const int32_t* reset_state;
+    int32_t* step_count;
+    int32_t* reward;
+    uint8_t* done;
+    uint8_t* truncated;
+    int32_t* lengths;
+    uint8_t* reduced;
+    int32_t* final_obs;
+    uint8_t* err;
+    int32_t* err_count;
+    int64_t B;
+    int32_t L, horizon, cyclical;
+};
+
+acx_step_plan* acx_step_plan_create(int32_t kind, const int32_t* state_in, int32_t* state_out,
+                                    const int32_t* reset_state, int32_t* step_count, int32_t* reward, uint8_t* done,
+                                    uint8_t* truncated, int32_t* lengths, uint8_t* reduced, int32_t* final_obs,
+                                    uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                                    int32_t cyclical) {
+    // the checks of the entry the plan calls (acx_step / acx_step_lengths / _reduced), made once
+    if (kind < ACX_STEP_PLAN_STEP || kind > ACX_STEP_PLAN_LENGTHS_REDUCED) return nullptr;
+    if (B < 0 || L < 1 || L > ACX_MAX_L) return nullptr;
+    if (B > 0) {
+        if (!state_in || !state_out || !aligned16(state_in) || !aligned16(state_out)) return nullptr;
+        if (reset_state && !step_count) return nullptr;
+        if (kind != ACX_STEP_PLAN_STEP && (state_out != state_in || !lengths)) return nullptr;
+        if (kind == ACX_STEP_PLAN_LENGTHS_REDUCED && !reduced) return nullptr;
+    }
+    if (kind != ACX_STEP_PLAN_LENGTHS_REDUCED && reduced) return nullptr;
+    return new (std::nothrow) acx_step_plan{kind, state_in, state_out, reset_state, step_count, reward, done, truncated,
+                                            lengths, reduced, final_obs, err, err_count, B, L, horizon, cyclical};
+}
+
+int acx_step_plan_launch(const acx_step_plan* p, const int32_t* action, void* stream) {
+    if (!p) return ACX_E_ARG;
+    switch (p->kind) {
+    case ACX_STEP_PLAN_STEP:
+        return acx_step(p->state_in, p->state_out, action, p->reset_state, p->step_count, p->reward, p->done,
+                        p->truncated, p->lengths, p->final_obs, p->err, p->err_count, p->B, p->L, p->horizon,
+                        p->cyclical, stream);
+    case ACX_STEP_PLAN_LENGTHS:
+        return acx_step_lengths(p->state_out, action, p->reset_state, p->step_count, p->reward, p->done, p->truncated,
+                                p->lengths, p->final_obs, p->err, p->err_count, p->B, p->L, p->horizon, p->cyclical,
+                                stream);
+    default:
+        return acx_step_lengths_reduced(p->state_out, action, p->reset_state, p->step_count, p->reward, p->done,
+                                        p->truncated, p->lengths, p->reduced, p->final_obs, p->err, p->err_count,
+                                        p->B, p->L, p->horizon, p->cyclical, stream);
+    }
+}
+
+void acx_step_plan_destroy(acx_step_plan* p) { delete p; }
 
 int acx_step_next(const int32_t* state_in, int32_t* state_out, const int32_t* action, const int32_t* reset_state,
                   int32_t* step_count, int32_t* reward, uint8_t* done, uint8_t* truncated, int32_t* lengths_out,

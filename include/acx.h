@@ -133,6 +133,30 @@ int acx_step_lengths_reduced(int32_t* state, const int32_t* action, const int32_
                              int32_t horizon, int32_t cyclical, void* stream);
 
 /*
+ * A per-call step plan: acx_step, acx_step_lengths or acx_step_lengths_reduced (kind
+ * ACX_STEP_PLAN_STEP / _LENGTHS / _LENGTHS_REDUCED) with every argument but the move ids and the
+ * stream resolved once, for a caller that steps the same buffers every call (BASELINE configs[1]:
+ * 65,536 envs stepped 200 times; ACEnv.step per call, ac_env.py:91-111).  acx_step_plan_create
+ * takes that entry's arguments (state_out == state_in and lengths required for the lengths kinds,
+ * reduced only and required for _LENGTHS_REDUCED) and makes its argument checks once; it returns
+ * NULL when they fail or memory is short.  acx_step_plan_launch(plan, action, stream) is then that
+ * entry with those arguments -- same kernels, results and return codes (ACX_E_ARG for a NULL
+ * plan).  The plan holds the pointers, not the buffers: they must outlive it.  The plan is host
+ * memory; launches from several threads may share one plan, destroy it once (NULL is a no-op).
+ */
+typedef struct acx_step_plan acx_step_plan;
+#define ACX_STEP_PLAN_STEP 0
+#define ACX_STEP_PLAN_LENGTHS 1
+#define ACX_STEP_PLAN_LENGTHS_REDUCED 2
+acx_step_plan* acx_step_plan_create(int32_t kind, const int32_t* state_in, int32_t* state_out,
+                                    const int32_t* reset_state, int32_t* step_count, int32_t* reward, uint8_t* done,
+                                    uint8_t* truncated, int32_t* lengths, uint8_t* reduced, int32_t* final_obs,
+                                    uint8_t* err, int32_t* err_count, int64_t B, int32_t L, int32_t horizon,
+                                    int32_t cyclical);
+int acx_step_plan_launch(const acx_step_plan* plan, const int32_t* action, void* stream);
+void acx_step_plan_destroy(acx_step_plan* plan);
+
+/*
  * acx_step for the PPO learner (ac_solver/agents/training.py:221-356), state updated in place
  * with same-step autoreset to reset_state, plus the learner-side writes fused in:
  *   action / action_i64 : exactly one non-NULL; action_i64 = the policy's int64 samples

@@ -34,6 +34,31 @@ def test_library_exports_header_symbols():
     assert lib.acx_version().startswith(b"acx")
 
 
+def test_step_plan_argument_checks():
+    """acx_step_plan_create makes the entry's argument checks once (include/acx.h) and returns
+    NULL when they fail; no GPU call is made by create, destroy or a launch of a NULL plan."""
+    lib = _lib.load()
+    st, st2, lens, red = 1 << 20, 2 << 20, 3 << 20, 4 << 20  # 16-byte aligned addresses, never dereferenced
+
+    def make(kind, state_out=st, lengths=None, reduced=None, B=64, L=36, reset=None, count=None):
+        return lib.acx_step_plan_create(kind, st, state_out, reset, count, None, None, None, lengths, reduced, None,
+                                        None, None, B, L, 200, 1)
+
+    good = [make(0), make(0, state_out=st2, lengths=lens), make(1, lengths=lens), make(2, lengths=lens, reduced=red),
+            make(0, B=0)]
+    assert all(good)
+    for p in good:
+        lib.acx_step_plan_destroy(p)
+    lib.acx_step_plan_destroy(None)
+    for bad in (make(3), make(-1), make(0, L=0), make(0, L=_lib.MAX_L + 1), make(0, B=-1),
+                make(0, reset=5 << 20),                      # reset_state needs step_count
+                make(1), make(1, state_out=st2, lengths=lens),  # lengths kinds: in place, lengths
+                make(2, lengths=lens), make(0, reduced=red), make(1, lengths=lens, reduced=red),
+                make(0, state_out=st + 4)):                  # 16-byte alignment
+        assert not bad
+    assert lib.acx_step_plan_launch(None, None, None) == _lib.E_ARG
+
+
 def test_no_cpu_fallback():
     s = torch.zeros((4, 8), dtype=torch.int32)
     a = torch.zeros(4, dtype=torch.int32)
