@@ -54,7 +54,17 @@ def main():
         tr = torch.zeros(B, dtype=torch.uint8, device=dev)
         act = torch.randint(0, 12, (B,), dtype=torch.int32, device=dev)
         plan = ops.StepPlan(st, reset_state=starts, step_count=cnt, horizon=200, reward=rew, done=dn, truncated=tr)
-        out[f"stepplan_B{B}_us"] = per_call(lambda: plan(act), a.n if B == 64 else 2000)
+        n = a.n if B == 64 else 2000
+        out[f"stepplan_B{B}_us"] = per_call(lambda: plan(act), n)
+        # the same step through the entry's own 17-argument ctypes call (what StepPlan made before
+        # acx_step_plan_launch), and the plan's launch alone (no Python-side action checks)
+        lib, sget = plan._lib, ops._stream
+        args = (st.data_ptr(), st.data_ptr())
+        tail = (starts.data_ptr(), cnt.data_ptr(), rew.data_ptr(), dn.data_ptr(), tr.data_ptr(), None, None, None,
+                None, B, L, 200, 1)
+        out[f"direct17_B{B}_us"] = per_call(lambda: lib.acx_step(*args, act.data_ptr(), *tail, sget(dev)), n)
+        out[f"plan_launch_B{B}_us"] = per_call(lambda: lib.acx_step_plan_launch(plan._plan, act.data_ptr(), sget(dev)),
+                                               n)
     out["note"] = "(host issue time per call, issue + drain per call) in microseconds"
     print(json.dumps(out))
 
