@@ -168,7 +168,8 @@ def main():
                 sig = (int(st.sum(dtype=torch.int64)), int((st * st).sum(dtype=torch.int64)),
                        int(cnt.sum(dtype=torch.int64)), int(rew.sum(dtype=torch.int64)), int(ec.item()))
                 ref = ref or sig
-                assert sig == ref, (n, sig, ref)
+                if os.environ.get("AB_NOCHECK") != "1":  # 1: diagnostic builds whose results differ on purpose
+                    assert sig == ref, (n, sig, ref)
                 if chg is None:
                     c = 0.0
                     for t in range(W + K, W + K + 8):
